@@ -1,0 +1,83 @@
+"""Golden-vector case table (plain data; shared by make_golden.py and the tests).
+
+Each case is a tiny instance of one BASELINE.json config family. Shapes follow the reference's
+own configs (configs/model/*.yaml, configs/experiment/*.yaml) scaled down so the CPU oracle
+finishes in well under a second.
+"""
+
+CASES = {
+    # BaseVAE with attention at a non-mid level (attn_resolutions=[16] at 16x16 -> 256 tokens),
+    # GroupNorm with 1 and 2 channels per group, Downsample 16->8 and Upsample 8->16.
+    "base_attn": dict(
+        cls="BaseVAE",
+        kwargs=dict(input_channels=3, latent_dim=8, hidden_channels=32, ch_mult=[1, 2],
+                    num_res_blocks=1, attn_resolutions=[16], dropout=0.0, resolution=16),
+        batch=2, cond="none",
+        loss=dict(type="vae", recon_loss_type="mse", kl_weight=1.0, recon_weight=1.0),
+        optimizer=dict(type="adamw", lr=2e-4, weight_decay=1e-4, betas=[0.9, 0.999]),
+        clip=1.0,
+    ),
+    # Config 2 family (path_beta_vae at 28x28x3, ch_mult (1,2,4)): odd spatial sizes 28->14->7.
+    "beta_c2": dict(
+        cls="BetaVAE",
+        kwargs=dict(input_channels=3, latent_dim=16, hidden_channels=32, ch_mult=[1, 2, 4],
+                    num_res_blocks=2, attn_resolutions=[], dropout=0.0, resolution=28, beta=6.0),
+        batch=3, cond="none",
+        loss=dict(type="vae", recon_loss_type="mse", kl_weight=6.0, recon_weight=1.0),
+        optimizer=dict(type="adamw", lr=1e-4, weight_decay=1e-4, betas=[0.9, 0.999]),
+        clip=1.0,
+    ),
+    # Config 1 family (chest_base_vae, 1-channel input).
+    "base_c1": dict(
+        cls="BaseVAE",
+        kwargs=dict(input_channels=1, latent_dim=16, hidden_channels=32, ch_mult=[1, 2, 4],
+                    num_res_blocks=1, attn_resolutions=[], dropout=0.0, resolution=28),
+        batch=2, cond="none",
+        loss=dict(type="vae", recon_loss_type="mse", kl_weight=1.0, recon_weight=1.0),
+        optimizer=dict(type="adamw", lr=2e-4, weight_decay=1e-4, betas=[0.9, 0.999]),
+        clip=1.0,
+    ),
+    # Config 4 family (multi_modal_cvae: ConditionalVAE concat, 12-way one-hot, ch_mult (1,2,4,8),
+    # attention at 16) at 32x32 so that 16x16 attention sits at level 1.
+    "cvae_c4": dict(
+        cls="ConditionalVAE",
+        kwargs=dict(input_channels=3, latent_dim=8, hidden_channels=16, ch_mult=[1, 2, 4, 8],
+                    num_res_blocks=1, attn_resolutions=[16], dropout=0.0, resolution=32,
+                    condition_method="concat"),
+        batch=3, cond="onehot",
+        loss=dict(type="vae", recon_loss_type="mse", kl_weight=1.0, recon_weight=1.0),
+        optimizer=dict(type="adamw", lr=1e-4, weight_decay=1e-5, betas=[0.5, 0.999]),
+        clip=1.0,
+    ),
+    # Config 3 family (disentangled_multi_modal_cvae_quick), dropout forced to 0 for parity,
+    # mixed gray/colour batch with an out-of-range modality index (7 -> clamped to 4).
+    "dis_c3": dict(
+        cls="DisentangledConditionalVAE",
+        kwargs=dict(num_modalities=5, shared_latent_dim=8, modality_latent_dim=8,
+                    hidden_channels=32, ch_mult=[1, 2, 4], num_res_blocks=1, attn_resolutions=[],
+                    dropout=0.0, resolution=28, modality_separation_weight=0.1,
+                    contrastive_weight=0.05),
+        batch=8, cond="idx", idx=[0, 1, 2, 3, 4, 7, 1, 0],
+        loss=dict(type="disentangled_vae", recon_loss_type="mse", kl_weight=1.0,
+                  recon_weight=1.0, separation_weight=0.1, contrastive_weight=0.05),
+        optimizer=dict(type="adam", lr=5e-4, weight_decay=0.0, betas=[0.9, 0.999]),
+        clip=0.5,
+    ),
+}
+
+MODALITY_CHANNELS = {0: 1, 1: 3, 2: 3, 3: 1, 4: 3}
+
+# Parameters whose full gradient / updated value is stored in the fixture (others: sum + sumsq).
+FULL_GRADS = {
+    "base_attn": ["encoder.conv_in.weight", "encoder.down.0.attn.0.q.weight",
+                  "decoder.up.0.block.1.norm1.weight", "decoder.conv_out.bias",
+                  "encoder.down.0.downsample.conv.weight", "decoder.up.1.upsample.conv.bias"],
+    "beta_c2": ["encoder.conv_out.weight", "decoder.mid.attn_1.proj_out.weight",
+                "encoder.down.1.block.0.nin_shortcut.weight"],
+    "base_c1": ["encoder.conv_in.weight", "decoder.conv_out.weight"],
+    "cvae_c4": ["condition_proj.0.weight", "condition_proj.0.bias", "encoder.conv_in.weight",
+                "encoder.down.1.attn.0.k.weight"],
+    "dis_c3": ["modality_input_projectors.0.weight", "modality_output_projectors.3.weight",
+               "modality_decoders.4.0.weight", "modality_decoders.1.2.bias",
+               "encoder.conv_in.weight"],
+}

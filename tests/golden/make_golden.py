@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Generate golden input/output vectors from the REFERENCE implementation (run in the build
+container only; /root/reference does not exist on the GPU box).
+
+    python3 -B tests/golden/make_golden.py
+
+For every case in cases.py this script
+  1. imports the reference's own model classes (`src.models`, reference commit mounted read-only
+     at /root/reference) and instantiates the case's model with its constructor kwargs,
+  2. loads the deterministic synthetic weights of weights.py (no weights are stored),
+  3. runs the reference training-step semantics on a synthetic MedMNIST-shaped batch:
+       forward (src/lightning_module.py:115-128) with an injected reparameterization eps,
+       loss (VAELoss src/losses/vae_losses.py:17-64 -- restated here with the same two torch
+       calls because src.losses needs lpips/open_clip, which are not installed --, or the
+       reference's own DisentangledVAELoss src/models/disentangled_conditional_vae.py:485-573),
+       backward, zero non-finite grads (src/lightning_module.py:468-477), global-norm clip
+       (:452-466, torch.nn.utils.clip_grad_norm_) and one Adam/AdamW step (:390-408),
+  4. writes tests/golden/<case>.npz (plain arrays, allow_pickle=False) + <case>.json (metadata).
+
+Only data leaves this script: inputs, outputs, loss terms, gradient and post-step checksums, and a
+few full gradient tensors. No reference source is copied.
+"""
+from __future__ import annotations
+
+import contextlib
+import json
+import os
+import sys
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+REF = os.environ.get("MEDVAE_REFERENCE", "/root/reference")
+sys.path.insert(0, REF)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+from torch.distributions import kl_divergence  # noqa: E402
+
+import src.models as ref_models  # noqa: E402  (the reference)
+from cases import CASES, FULL_GRADS  # noqa: E402
+from weights import synth_state, state_checksum  # noqa: E402
+
+
+@contextlib.contextmanager
+def injected_randn_like(eps: torch.Tensor):
+    """BaseVAE.reparameterize (src/models/base_vae.py:83-87) draws eps with torch.randn_like;
+    replace it by the fixture's eps so the CPU reference is deterministic."""
+    orig = torch.randn_like
+
+    def fake(t, *a, **k):
+        assert tuple(t.shape) == tuple(eps.shape), (t.shape, eps.shape)
+        return eps.clone()
+
+    torch.randn_like = fake
+    try:
+        yield
+    finally:
+        torch.randn_like = orig
+
+
+def make_inputs(case_name, case, model):
+    rng = np.random.Generator(np.random.PCG64(2024 + len(case_name)))
+    B = case["batch"]
+    res = case["kwargs"]["resolution"]
+    if case["cls"] == "DisentangledConditionalVAE":
+        C = 3
+    else:
+        C = case["kwargs"]["input_channels"]
+    x = rng.integers(0, 256, size=(B, C, res, res)).astype(np.float32) / np.float32(255.0)
+    x = x * np.float32(2.0) - np.float32(1.0)
+    ins = {"x": x}
+    if case["cond"] == "onehot":
+        idx = rng.integers(0, 12, size=(B,))
+        oh = np.zeros((B, 12), np.float32)
+        oh[np.arange(B), idx] = 1.0
+        ins["cond"] = oh
+    elif case["cond"] == "idx":
+        idx = np.asarray(case["idx"], np.int64)
+        # mixed_modality_collate_fn (src/data/medmnist_data.py:16-72): 1-channel modalities are
+        # zero-padded to 3 channels.
+        for b, m in enumerate(idx):
+            mm = min(int(m), 4)
+            if mm in (0, 3):
+                x[b, 1:] = 0.0
+        ins["cond"] = idx
+    lat = model.latent_dim
+    r = model.encoder_out_res
+    ins["eps"] = rng.standard_normal(size=(B, lat, r, r)).astype(np.float32)
+    return ins
+
+
+def vae_loss(cfg, x, out):
+    """VAELoss.forward, src/losses/vae_losses.py:37-64 (mse branch)."""
+    rec = F.mse_loss(out["reconstruction"], x, reduction="mean")
+    kl = kl_divergence(out["posterior"], out["prior"]).mean()
+    loss = cfg.get("recon_weight", 1.0) * rec + cfg.get("kl_weight", 1.0) * kl
+    return {"loss": loss, "recon_loss": rec, "kl_loss": kl}
+
+
+def run_case(name, case):
+    torch.manual_seed(0)
+    cls = getattr(ref_models, case["cls"])
+    kw = dict(case["kwargs"])
+    if "ch_mult" in kw:
+        kw["ch_mult"] = tuple(kw["ch_mult"])
+    model = cls(**kw)
+    model.train()
+    seeded_init = {k: (float(v.double().sum()), float((v.double() ** 2).sum()))
+                   for k, v in model.state_dict().items()}
+    named = [(k, tuple(v.shape)) for k, v in model.state_dict().items()]
+    state = synth_state(named)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in state.items()})
+
+    ins = make_inputs(name, case, model)
+    x = torch.from_numpy(ins["x"])
+    eps = torch.from_numpy(ins["eps"])
+    with injected_randn_like(eps):
+        if case["cond"] == "none":
+            out = model(x)
+        elif case["cond"] == "onehot":
+            out = model(x, torch.from_numpy(ins["cond"]))
+        else:
+            out = model(x, torch.from_numpy(ins["cond"]))
+
+    lcfg = case["loss"]
+    if lcfg["type"] == "vae":
+        ld = vae_loss(lcfg, x, out)
+    else:
+        crit = ref_models.DisentangledVAELoss(
+            recon_loss_type=lcfg["recon_loss_type"], kl_weight=lcfg["kl_weight"],
+            recon_weight=lcfg["recon_weight"], separation_weight=lcfg["separation_weight"],
+            contrastive_weight=lcfg["contrastive_weight"])
+        ld = crit(out, x)
+    loss = ld["loss"]
+
+    params = dict(model.named_parameters())
+    for p in params.values():
+        p.grad = None
+    loss.backward()
+    # on_before_optimizer_step: zero non-finite grads per tensor (lightning_module.py:468-477)
+    for p in params.values():
+        if p.grad is not None and (torch.isnan(p.grad).any() or torch.isinf(p.grad).any()):
+            p.grad.zero_()
+    rec = {}
+    meta_grads = {}
+    for k, p in params.items():
+        if p.grad is None:
+            meta_grads[k] = None
+            continue
+        g = p.grad.double()
+        rec[f"gradsum.{k}"] = np.array([float(g.sum()), float((g * g).sum())])
+        if k in FULL_GRADS.get(name, []):
+            rec[f"grad.{k}"] = p.grad.numpy().copy()
+        meta_grads[k] = True
+    grads_with = [p for p in params.values() if p.grad is not None]
+    total_norm = torch.nn.utils.clip_grad_norm_(grads_with, case["clip"])
+    o = case["optimizer"]
+    if o["type"] == "adam":
+        opt = torch.optim.Adam(params.values(), lr=o["lr"], weight_decay=o["weight_decay"],
+                               betas=tuple(o["betas"]))
+    else:
+        opt = torch.optim.AdamW(params.values(), lr=o["lr"], weight_decay=o["weight_decay"],
+                                betas=tuple(o["betas"]))
+    opt.step()
+    for k, p in params.items():
+        v = p.detach().double()
+        rec[f"stepsum.{k}"] = np.array([float(v.sum()), float((v * v).sum())])
+        if k in FULL_GRADS.get(name, []):
+            rec[f"step.{k}"] = p.detach().numpy().copy()
+
+    for k, v in ins.items():
+        rec[f"in.{k}"] = v
+    for k in ("reconstruction", "mean", "logvar", "z"):
+        rec[f"out.{k}"] = out[k].detach().numpy().copy()
+    for k in ("separation_loss", "contrastive_loss"):
+        if k in out:
+            rec[f"out.{k}"] = np.array(float(out[k]))
+    for k, v in ld.items():
+        rec[f"loss.{k}"] = np.array(float(v))
+    rec["clip.total_norm"] = np.array(float(total_norm))
+    np.savez(os.path.join(HERE, f"{name}.npz"), **rec)
+    meta = dict(case=case, params=[[k, list(s)] for k, s in named],
+                param_has_grad={k: bool(v) for k, v in meta_grads.items()},
+                weight_checksum=state_checksum(state), seeded_init_torch_seed0=seeded_init,
+                reference="parsakzr/medvae-disentangled-multimodal @ 2025-08-24",
+                torch=torch.__version__)
+    with open(os.path.join(HERE, f"{name}.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print(f"{name}: loss={float(loss):.8f} recon={float(ld['recon_loss']):.8f} "
+          f"kl={float(ld['kl_loss']):.8f} |g|={float(total_norm):.6f}")
+
+
+def known_answer_anchor():
+    """SURVEY.md section 8(c) known-answer anchor, run on the reference itself."""
+    torch.manual_seed(0)
+    m = ref_models.BaseVAE(input_channels=3, latent_dim=16, hidden_channels=32, ch_mult=(1, 2, 4),
+                           num_res_blocks=1, attn_resolutions=[], dropout=0.0, resolution=28)
+    m.train()
+    g = torch.Generator().manual_seed(1)
+    x = torch.randint(0, 256, (4, 3, 28, 28), generator=g).float() / 255 * 2 - 1
+    eps = torch.randn(4, 16, 7, 7, generator=g)
+    with injected_randn_like(eps):
+        out = m(x)
+    ld = vae_loss({}, x, out)
+    res = {k: float(v) for k, v in ld.items()}
+    with open(os.path.join(HERE, "kat_anchor.json"), "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+    print("anchor", res)
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    sel = sys.argv[1:] or list(CASES)
+    for n in sel:
+        run_case(n, CASES[n])
+    known_answer_anchor()
