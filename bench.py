@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Training-throughput benchmark of the MI355X conv-VAE hot path.
+
+Workload (BASELINE.json metric, config 4): multimodal ConditionalVAE at 64x64x3, batch 256 per GPU
+(configs/experiment/multi_modal_cvae.yaml + model.resolution=64, training.loss.type=vae;
+AdamW lr 1e-4 betas (0.5, 0.999) wd 1e-5, gradient clip 1.0 -- configs/training/advanced.yaml),
+927 M parameters, fp32 semantics. One step = one Lightning automatic-optimisation step:
+forward + VAE loss + backward + [gradient all-reduce] + non-finite zeroing + clip + AdamW.
+Synthetic MedMNIST-shaped data resident in HBM (x = randint(0,256)/255*2-1, random one-hot of 12).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL all-reduce)
+
+Rank 0 prints ONE JSON line (value = images/s over all ranks, max-over-ranks timing), with
+  roofline:     the implicit-GEMM MFMA kernel family, live HIP-event timing of every launch in one
+                instrumented step after the timed region (algorithmic FLOPs = the reference's conv /
+                bmm FLOPs), peak = the 3xBF16 ceiling (bf16 dense MFMA 2.5 PF / 3 products)
+  cpu_baseline: the CPU oracle (reference algorithm restated, tests-pinned) timed on this host on a
+                bounded sample (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MODALITIES = ["chestmnist", "pathmnist", "octmnist", "pneumoniamnist", "dermamnist", "bloodmnist", "tissuemnist",
+              "retinamnist", "breastmnist", "organamnist", "organcmnist", "organsmnist"]
+
+CONFIGS = {
+    # BASELINE config 4 (the metric's config): multi_modal_cvae @ 64x64, bs 256 per GPU
+    "c4": dict(cls="ConditionalVAE", res=64, batch=256,
+               kwargs=dict(input_channels=3, latent_dim=256, hidden_channels=256, ch_mult=(1, 2, 4, 8),
+                           num_res_blocks=2, attn_resolutions=[16], dropout=0.0, resolution=64,
+                           modalities=MODALITIES, condition_method="concat"),
+               opt=dict(type="adamw", lr=1e-4, weight_decay=1e-5, betas=[0.5, 0.999]), clip=1.0,
+               loss=dict(type="vae", recon_loss_type="mse", kl_weight=1.0, recon_weight=1.0)),
+    # BASELINE config 2: path_beta_vae at 28x28x3 with the 3-level ch_mult, bs 256
+    "c2": dict(cls="BetaVAE", res=28, batch=256,
+               kwargs=dict(input_channels=3, latent_dim=128, hidden_channels=128, ch_mult=(1, 2, 4),
+                           num_res_blocks=2, attn_resolutions=[16], dropout=0.0, resolution=28, beta=6.0),
+               opt=dict(type="adamw", lr=1e-4, weight_decay=1e-4, betas=[0.9, 0.999]), clip=1.0,
+               loss=dict(type="vae", recon_loss_type="mse", kl_weight=6.0, recon_weight=1.0)),
+}
+
+BF16_DENSE_PEAK_TF = 2500.0
+PEAK_3XBF16_TF = BF16_DENSE_PEAK_TF / 3.0
+
+
+def make_batch(cfg, device, gen):
+    B, r = cfg["batch"], cfg["res"]
+    C = cfg["kwargs"]["input_channels"]
+    x = torch.randint(0, 256, (B, C, r, r), generator=gen, device=device).float() / 255 * 2 - 1
+    labels = torch.zeros(B, 1, dtype=torch.long, device=device)
+    if cfg["cls"] == "ConditionalVAE":
+        idx = torch.randint(0, 12, (B,), generator=gen, device=device)
+        oh = torch.nn.functional.one_hot(idx, 12).float()
+        return (x, labels, oh)
+    return (x, labels)
+
+
+def cpu_baseline(cfg, seconds_budget=20.0):
+    """Time the CPU oracle (oracle/torch_ref.py: the reference algorithm, pinned by the golden tests)
+    on a bounded sample: one training step (fwd+loss+bwd+clip+AdamW) at batch 2."""
+    from oracle import torch_ref as R
+    threads = torch.get_num_threads()
+    a = R.make_arch(cfg["cls"], dict(cfg["kwargs"]))
+    g = torch.Generator().manual_seed(0)
+    P = {k: torch.randn(s, generator=g) * 0.02 for k, s in R.param_shapes(a)}
+    bs = 2
+    x = torch.randint(0, 256, (bs, a.input_channels, a.resolution, a.resolution), generator=g).float() / 255 * 2 - 1
+    cond = None
+    if a.cls == "ConditionalVAE":
+        cond = torch.nn.functional.one_hot(torch.randint(0, 12, (bs,), generator=g), 12).float()
+    eps = torch.randn(bs, a.latent_dim, a.enc_res, a.enc_res, generator=g)
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        R.train_step(P, a, x, cond, eps, cfg["loss"], cfg["opt"], cfg["clip"])
+        steps += 1
+        if time.perf_counter() - t0 > seconds_budget / 2 or steps >= 3:
+            break
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": round(bs / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} oracle training step(s) at batch {bs} of the same model (fp32, CPU), "
+                      f"{dt:.2f} s/step"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch override (default: config)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    import medvae_disentangled_multimodal_amd as M
+    from medvae_disentangled_multimodal_amd import ddp, ops
+
+    rank, world, local = ddp.init_from_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    cfg = dict(CONFIGS[args.config])
+    if args.batch:
+        cfg["batch"] = args.batch
+
+    torch.manual_seed(42)
+    model = getattr(M, cfg["cls"])(**cfg["kwargs"]).to(dev)
+    mod = M.VAELightningModule(model, cfg["opt"], {"type": "none"}, cfg["loss"], gradient_clip_val=cfg["clip"])
+    mod.configure_optimizers()
+    if world > 1:
+        ddp.DataParallel(mod)
+    nparams = sum(p.numel() for p in model.parameters())
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    batches = [make_batch(cfg, dev, gen) for _ in range(2)]
+
+    for i in range(args.warmup):
+        mod.fit_step(batches[i % 2], i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = mod.fit_step(batches[i % 2], i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    loss_v = float(loss)
+
+    roofline = None
+    if not args.no_kernel_timing:
+        ops.PROFILE = []
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        mod.fit_step(batches[0], 0)
+        torch.cuda.synchronize()
+        step_ms = (time.perf_counter() - t1) * 1e3
+        rec = ops.PROFILE
+        ops.PROFILE = None
+        tot_ms = sum(s.elapsed_time(e) for _, _, s, e in rec)
+        tot_fl = sum(f for _, f, _, _ in rec)
+        by = {}
+        for tag, f, s, e in rec:
+            d = by.setdefault(tag, [0, 0.0, 0.0])
+            d[0] += 1
+            d[1] += f
+            d[2] += s.elapsed_time(e)
+        ach = tot_fl / (tot_ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "kernel": "gemm3x_kernel (implicit-GEMM conv + attention bmm, all launches)",
+                    "achieved": round(ach, 2), "peak": round(PEAK_3XBF16_TF, 1), "unit": "TFLOP/s",
+                    "frac": round(ach / PEAK_3XBF16_TF, 4), "traffic": None,
+                    "peak_note": "3xBF16 fp32-emulation ceiling = bf16 dense MFMA 2.5 PF/s / 3; "
+                                 "native fp32 MFMA peak is 157.3 TF/s",
+                    "launches_per_step": len(rec), "avg_launch_us": round(tot_ms * 1e3 / len(rec), 2),
+                    "gemm_ms_per_step": round(tot_ms, 2), "instrumented_step_ms": round(step_ms, 2),
+                    "gemm_share_of_step": round(tot_ms / step_ms, 3),
+                    "by_pass": {k: {"launches": v[0], "ms": round(v[2], 2),
+                                    "TFLOP/s": round(v[1] / (v[2] * 1e-3) / 1e12, 1)} for k, v in by.items()}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg)
+
+    if rank == 0:
+        imgs = cfg["batch"] * world * args.steps
+        out = {"metric": "training images/sec (whole node), multimodal CVAE 64x64 bs=256/GPU"
+               if args.config == "c4" else f"training images/sec, config {args.config}",
+               "value": round(imgs / dt, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (3xBF16 MFMA, fp32 accumulate)",
+               "data": "synthetic (MedMNIST-shaped, resident in HBM; random-init weights)",
+               "config": {"workload": f"{cfg['cls']} {cfg['res']}x{cfg['res']}x{cfg['kwargs']['input_channels']} "
+                                      f"train step (fwd+loss+bwd+clip+AdamW)", "model": cfg["cls"],
+                          "params": nparams, "global_batch": cfg["batch"] * world, "per_gpu_batch": cfg["batch"],
+                          "resolution": cfg["res"], "parallelism": f"dp{world}"},
+               "loss": round(loss_v, 6), "roofline": roofline, "cpu_baseline": cpu}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,123 @@
+/*
+ * medvae_hip.h -- C ABI of the MI355X (gfx950) conv-VAE training hot path.
+ *
+ * The reference (parsakzr/medvae-disentangled-multimodal) is pure Python/PyTorch: it has no FFI,
+ * so each entry point below replaces the ATen call(s) that the named reference line issues on its
+ * CPU path. The Python package medvae_disentangled_multimodal_amd binds these with ctypes (see
+ * INTEGRATION.md) behind the reference's own model / LightningModule API.
+ *
+ * Conventions
+ *   - all tensors are fp32 device pointers (HBM), activations NHWC ([n][h][w][c], c contiguous),
+ *     conv weights KRSC ([cout][kh][kw][cin], i.e. torch channels_last OIHW);
+ *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream);
+ *   - kernels never allocate: scratch comes in `workspace` (size from the *_workspace_bytes query);
+ *   - return 0 on success, MVAE_EINVAL (-1) / MVAE_EWORKSPACE (-2) on a bad argument, or the
+ *     hipError_t of a failed launch; mvae_last_error() describes the last failure (per thread);
+ *   - every reduction is two-stage and fixed-order: results are bitwise reproducible.
+ */
+#ifndef MEDVAE_HIP_H
+#define MEDVAE_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MVAE_OK 0
+#define MVAE_EINVAL (-1)
+#define MVAE_EWORKSPACE (-2)
+
+const char* mvae_last_error(void);
+int mvae_abi_version(void);
+
+/* ---- convolutions (implicit GEMM on MFMA, 3xBF16 split arithmetic, fp32 accumulate) ------------
+ * Replaces nn.Conv2d forward in ResnetBlock/AttnBlock/Encoder/Decoder
+ * (src/models/encoder_decoder.py:123-146,76-81,250-299,356-418), Downsample's F.pad + stride-2 conv
+ * (:184-188, mode 0 with pad_t=pad_l=0 and zero fill beyond H/W) and Upsample's F.interpolate +
+ * conv (:205-209, mode 1). mode 2 = transposed gather (input gradient of a strided conv).
+ * y = conv(x) + bias[cout] + residual (residual: ResnetBlock/AttnBlock skip add, :170, :107). */
+int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y,
+                     int nb, int h, int w_, int cin, int cout, int kh, int kw, int stride, int pad_t,
+                     int pad_l, int ho, int wo, int mode, void* stream);
+
+/* Weight gradient of mvae_conv2d_nhwc (modes 0/1): dw = beta*dw + sum_pixels dy (x) x.
+ * Replaces the weight half of aten::convolution_backward for the convolutions above. */
+int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float beta, int nb, int h, int w_,
+                           int cin, int cout, int kh, int kw, int stride, int pad_t, int pad_l, int ho,
+                           int wo, int mode, float* workspace, size_t workspace_bytes, void* stream);
+size_t mvae_conv2d_wgrad_workspace_bytes(int nb, int cin, int cout, int kh, int kw, int ho, int wo);
+
+/* Weight re-layouts for the input gradient: KRSC -> [cin][kh][kw][cout]; and the 4x4 tap-summed
+ * kernel [cin][4][4][cout] for Upsample's conv (encoder_decoder.py:205-209). */
+int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int kw, int cin, void* stream);
+int mvae_conv_weight_upsample_dgrad(const float* w, float* wt, int cout, int cin, void* stream);
+
+/* Bias gradient: out[n] = beta*out[n] + sum_rows x[row*ld + n] (conv bias, encoder_decoder.py:123-146). */
+int mvae_bias_grad(const float* x, long long rows, int n, long long ld, float* out, float beta,
+                   void* workspace, size_t workspace_bytes, void* stream);
+size_t mvae_bias_grad_workspace_bytes(long long rows, int n);
+
+/* ---- batched GEMM (AttnBlock's torch.bmm pair, encoder_decoder.py:90-103) ----------------------
+ * C[b] = alpha*op(A[b]) op(B[b]) + bias + residual[b] + beta*C[b], row-major.
+ * trans_a: A stored [K][M]; trans_b: B stored [N][K]. */
+int mvae_gemm_strided_batched(int trans_a, int trans_b, int m, int n, int k, float alpha,
+                              const float* A, long long lda, long long stride_a, const float* B,
+                              long long ldb, long long stride_b, float beta, float* C, long long ldc,
+                              long long stride_c, int batch, const float* bias, const float* residual,
+                              long long ldr, long long stride_r, float* workspace,
+                              size_t workspace_bytes, void* stream);
+size_t mvae_gemm_workspace_bytes(int m, int n, int k, int batch);
+
+/* Row softmax of the attention scores (F.softmax(w_, dim=2), encoder_decoder.py:97) and its grad. */
+int mvae_softmax_rows(const float* x, float* y, long long rows, int n, void* stream);
+int mvae_softmax_rows_bwd(const float* y, const float* dy, float* dx, long long rows, int n, void* stream);
+
+/* ---- GroupNorm (+SiLU, +inverted dropout) -------------------------------------------------------
+ * Normalize() = nn.GroupNorm(min(32,C), C, eps=1e-6) (encoder_decoder.py:28-33) fused with
+ * nonlinearity() (:13-15) and ResnetBlock's nn.Dropout (:163). mean/rstd: [nb*groups].
+ * Backward ACCUMULATES into dgamma/dbeta (flat grad buffer). */
+int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* beta, float* y, float* mean,
+                             float* rstd, int nb, int hw, int c, int groups, float eps, int silu,
+                             float drop_p, unsigned long long seed, void* workspace,
+                             size_t workspace_bytes, void* stream);
+int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
+                             const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta,
+                             int nb, int hw, int c, int groups, int silu, float drop_p,
+                             unsigned long long seed, void* workspace, size_t workspace_bytes,
+                             void* stream);
+size_t mvae_group_norm_workspace_bytes(int nb, int hw, int c);
+
+/* ---- reparameterization / KL / reconstruction ---------------------------------------------------
+ * BaseVAE.reparameterize (src/models/base_vae.py:83-87) with explicit eps; mu/logvar are channel
+ * slices of the encoder output (row stride ld >= zc), torch.chunk (:76) costs nothing. */
+int mvae_reparam_fwd(const float* mu, const float* logvar, long long ld, const float* eps, float* z,
+                     long long npix, int zc, void* stream);
+int mvae_reparam_bwd(const float* dz, const float* eps, const float* logvar, long long ld, float* dlogvar,
+                     long long npix, int zc, void* stream);
+/* out[0] = scale * sum(term): kind 0 = KL(N(mu,e^{lv/2})||N(0,1)) (vae_losses.py:58),
+ * 1 = squared error (mse, :41), 2 = absolute error (l1, :43), 3 = -0.5*(1+lv-mu^2-e^lv)
+ * (DisentangledVAELoss, disentangled_conditional_vae.py:524). Device scalar out, no host sync. */
+int mvae_loss_reduce(int kind, const float* a, const float* b, long long ld, long long npix, int zc,
+                     double scale, float* out, void* workspace, size_t workspace_bytes, void* stream);
+size_t mvae_reduce_workspace_bytes(void);
+int mvae_kl_bwd(const float* mu, const float* logvar, long long ld, const float* gscale, double mult,
+                float* dmu, float* dlogvar, long long npix, int zc, void* stream);
+int mvae_recon_bwd(int kind, const float* a, const float* b, const float* gscale, double mult, float* da,
+                   long long n, void* stream);
+
+/* ---- optimizer step over one flat buffer ----------------------------------------------------------
+ * on_before_optimizer_step (lightning_module.py:468-477) + configure_gradient_clipping (:452-466) +
+ * Adam/AdamW (configure_optimizers, :390-408). scalars[0] = total grad norm, scalars[1] = coef. */
+int mvae_multi_tensor_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                           const int* chunk_tensor, const long long* chunk_start, const int* chunk_len,
+                           int nchunks, const int* tensor_chunk_begin, int ntensors, const int* used,
+                           int* step, float grad_scale, float max_norm, int do_clip, float lr, float beta1,
+                           float beta2, float eps, float weight_decay, int decoupled, void* workspace,
+                           size_t workspace_bytes, float* scalars, void* stream);
+size_t mvae_multi_tensor_adam_workspace_bytes(int nchunks, int ntensors);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MEDVAE_HIP_H */

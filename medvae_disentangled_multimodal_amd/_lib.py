@@ -1,0 +1,87 @@
+"""ctypes binding of the C-ABI hot-path library (include/medvae_hip.h -> libmvae_hip.so).
+
+There is deliberately NO fallback: if the shared library is missing or fails to load, every op
+raises. The product path is the HIP path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_double, c_float, c_int, c_longlong, c_size_t, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MVAE_HIP_LIB", os.path.join(_HERE, "libmvae_hip.so"))
+
+P = c_void_p
+I = c_int
+L = c_longlong
+F = c_float
+D = c_double
+Z = c_size_t
+
+# name -> (restype, argtypes); mirrors include/medvae_hip.h one-to-one
+SIGNATURES = {
+    "mvae_last_error": (ctypes.c_char_p, []),
+    "mvae_abi_version": (I, []),
+    "mvae_conv2d_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P]),
+    "mvae_conv2d_wgrad_nhwc": (I, [P, P, P, F, I, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),
+    "mvae_conv2d_wgrad_workspace_bytes": (Z, [I, I, I, I, I, I, I]),
+    "mvae_conv_weight_transpose": (I, [P, P, I, I, I, I, P]),
+    "mvae_conv_weight_upsample_dgrad": (I, [P, P, I, I, P]),
+    "mvae_bias_grad": (I, [P, L, I, L, P, F, P, Z, P]),
+    "mvae_bias_grad_workspace_bytes": (Z, [L, I]),
+    "mvae_gemm_strided_batched": (I, [I, I, I, I, I, F, P, L, L, P, L, L, F, P, L, L, I, P, P, L, L, P, Z, P]),
+    "mvae_gemm_workspace_bytes": (Z, [I, I, I, I]),
+    "mvae_softmax_rows": (I, [P, P, L, I, P]),
+    "mvae_softmax_rows_bwd": (I, [P, P, P, L, I, P]),
+    "mvae_group_norm_fwd_nhwc": (I, [P, P, P, P, P, P, I, I, I, I, F, I, F, c_uint64, P, Z, P]),
+    "mvae_group_norm_bwd_nhwc": (I, [P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, c_uint64, P, Z, P]),
+    "mvae_group_norm_workspace_bytes": (Z, [I, I, I]),
+    "mvae_reparam_fwd": (I, [P, P, L, P, P, L, I, P]),
+    "mvae_reparam_bwd": (I, [P, P, P, L, P, L, I, P]),
+    "mvae_loss_reduce": (I, [I, P, P, L, L, I, D, P, P, Z, P]),
+    "mvae_reduce_workspace_bytes": (Z, []),
+    "mvae_kl_bwd": (I, [P, P, L, P, D, P, P, L, I, P]),
+    "mvae_recon_bwd": (I, [I, P, P, P, D, P, L, P]),
+    "mvae_multi_tensor_adam": (I, [P, P, P, P, P, P, P, I, P, I, P, P, F, F, I, F, F, F, F, F, I, P, Z, P, P]),
+    "mvae_multi_tensor_adam_workspace_bytes": (Z, [I, I]),
+}
+
+
+class HipLibraryError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libmvae_hip.so (raises HipLibraryError if it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HipLibraryError(
+            f"{LIB_PATH} not found: build it with `make` (or __graft_entry__.build()); "
+            "the MI355X path has no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Invoke an int-returning entry point and raise on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.mvae_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (status {rc}): {msg}")
+    return rc
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)

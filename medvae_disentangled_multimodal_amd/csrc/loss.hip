@@ -1,0 +1,173 @@
+// Reparameterization, KL and reconstruction (MSE) terms of the VAE objective.
+//   reparameterize  z = mu + eps * exp(0.5*logvar)                 base_vae.py:83-87
+//   KL(N(mu, e^{lv/2}) || N(0,1)) = 0.5*(s^2 + mu^2 - 1 - log s^2)  torch.distributions (vae_losses.py:58)
+//   MSE mean                                                       vae_losses.py:41-42
+// mu / logvar are channel slices of the encoder's [pixels][2z] output (row stride `ld`), so no
+// chunk copy is needed. Reductions are deterministic: fp64 block partials, then one fixed-order pass.
+#include "common.h"
+#include <algorithm>
+
+namespace mvae {
+
+constexpr int RED_BLOCKS = 1024;
+
+__device__ __forceinline__ double block_sum_d(double v, double* sh) {
+  v = wave_sum_d(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  double t = 0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
+  return t;  // valid in thread 0
+}
+
+__global__ void __launch_bounds__(256) reparam_fwd_kernel(const float* __restrict__ mu, const float* __restrict__ lv,
+                                                          long long ld, const float* __restrict__ eps,
+                                                          float* __restrict__ z, long long npix, int zc) {
+  const long long n = npix * zc;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const long long p = e / zc;
+    const int c = (int)(e - p * zc);
+    const float m = mu[p * ld + c], l = lv[p * ld + c];
+    z[e] = m + eps[e] * expf(0.5f * l);
+  }
+}
+
+// dlogvar = dz * eps * 0.5 * exp(0.5*logvar)   (dmu = dz is passed through by the host)
+__global__ void __launch_bounds__(256) reparam_bwd_kernel(const float* __restrict__ dz, const float* __restrict__ eps,
+                                                          const float* __restrict__ lv, long long ld,
+                                                          float* __restrict__ dlv, long long npix, int zc) {
+  const long long n = npix * zc;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const long long p = e / zc;
+    const int c = (int)(e - p * zc);
+    dlv[e] = dz[e] * eps[e] * 0.5f * expf(0.5f * lv[p * ld + c]);
+  }
+}
+
+// kind 0: KL elementwise sum (torch.distributions form) ; kind 1: squared error sum ;
+// kind 2: absolute error sum ; kind 3: "-0.5*(1 + lv - mu^2 - exp(lv))" sum (DisentangledVAELoss)
+__global__ void __launch_bounds__(256) reduce_partial_kernel(int kind, const float* __restrict__ a,
+                                                             const float* __restrict__ b, long long ld, long long npix,
+                                                             int zc, double* __restrict__ part) {
+  __shared__ double sh[4];
+  const long long n = npix * zc;
+  double acc = 0;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    if (kind == 0 || kind == 3) {
+      const long long p = e / zc;
+      const int c = (int)(e - p * zc);
+      const float m = a[p * ld + c], l = b[p * ld + c];
+      if (kind == 0) {
+        const float s = expf(0.5f * l);
+        const float r = s * s;
+        acc += 0.5f * (r + m * m - 1.f - logf(r));
+      } else {
+        acc += 1.f + l - m * m - expf(l);
+      }
+    } else {
+      const float d = a[e] - b[e];
+      acc += kind == 1 ? (double)d * d : (double)fabsf(d);
+    }
+  }
+  const double t = block_sum_d(acc, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+__global__ void reduce_final_kernel(const double* __restrict__ part, int nparts, double scale, float* out) {
+  __shared__ double sh[4];
+  double acc = 0;
+  // fixed assignment of partials to threads + fixed-order combine => deterministic
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += part[i];
+  const double t = block_sum_d(acc, sh);
+  if (threadIdx.x == 0) out[0] = (float)(t * scale);
+}
+
+// dmu = g*mu ; dlv = g*0.5*(exp(lv) - 1), g = gscale[0] * mult (device scalar, no host sync)
+// kind 0: torch KL form, kind 3: Disentangled closed form (same derivative)
+__global__ void __launch_bounds__(256) kl_bwd_kernel(const float* __restrict__ mu, const float* __restrict__ lv,
+                                                     long long ld, const float* __restrict__ gscale, double mult,
+                                                     float* __restrict__ dmu, float* __restrict__ dlv, long long npix,
+                                                     int zc) {
+  const float g = (float)(gscale[0] * mult);
+  const long long n = npix * zc;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const long long p = e / zc;
+    const int c = (int)(e - p * zc);
+    const float m = mu[p * ld + c], l = lv[p * ld + c];
+    const float s = expf(0.5f * l);
+    dmu[e] = g * m;
+    dlv[e] = g * 0.5f * (s * s - 1.f);
+  }
+}
+
+// d/da of mean((a-b)^2) or mean|a-b| times upstream gradient gscale[0]
+__global__ void __launch_bounds__(256) recon_bwd_kernel(int kind, const float* __restrict__ a,
+                                                        const float* __restrict__ b, const float* __restrict__ gscale,
+                                                        double mult, float* __restrict__ da, long long n) {
+  const float g = (float)(gscale[0] * mult);
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const float d = a[e] - b[e];
+    da[e] = kind == 1 ? g * 2.f * d : g * (float)((d > 0.f) - (d < 0.f));
+  }
+}
+
+static int egrid(long long n) { return (int)std::max<long long>(1, std::min<long long>((n + 255) / 256, 8192)); }
+
+}  // namespace mvae
+
+using namespace mvae;
+
+extern "C" {
+
+size_t mvae_reduce_workspace_bytes(void) { return RED_BLOCKS * sizeof(double); }
+
+int mvae_reparam_fwd(const float* mu, const float* logvar, long long ld, const float* eps, float* z, long long npix,
+                     int zc, void* stream) {
+  if (npix <= 0 || zc <= 0 || ld < zc) { set_error("reparam: bad sizes"); return MVAE_EINVAL; }
+  hipLaunchKernelGGL(reparam_fwd_kernel, dim3(egrid(npix * zc)), dim3(256), 0, (hipStream_t)stream, mu, logvar, ld,
+                     eps, z, npix, zc);
+  return launch_status();
+}
+
+int mvae_reparam_bwd(const float* dz, const float* eps, const float* logvar, long long ld, float* dlogvar,
+                     long long npix, int zc, void* stream) {
+  if (npix <= 0 || zc <= 0 || ld < zc) { set_error("reparam_bwd: bad sizes"); return MVAE_EINVAL; }
+  hipLaunchKernelGGL(reparam_bwd_kernel, dim3(egrid(npix * zc)), dim3(256), 0, (hipStream_t)stream, dz, eps,
+                     logvar, ld, dlogvar, npix, zc);
+  return launch_status();
+}
+
+// out[0] = scale * sum_e term(e); kind as in reduce_partial_kernel. For kinds 1/2, a and b are
+// dense [n] (npix = n, zc = 1, ld unused).
+int mvae_loss_reduce(int kind, const float* a, const float* b, long long ld, long long npix, int zc, double scale,
+                     float* out, void* workspace, size_t workspace_bytes, void* stream) {
+  if (kind < 0 || kind > 3 || npix <= 0 || zc <= 0) { set_error("loss_reduce: bad args"); return MVAE_EINVAL; }
+  if (workspace_bytes < RED_BLOCKS * sizeof(double)) { set_error("loss_reduce: workspace"); return MVAE_EWORKSPACE; }
+  hipStream_t st = (hipStream_t)stream;
+  const long long n = npix * zc;
+  const int blocks = (int)std::min<long long>(RED_BLOCKS, (n + 255) / 256);
+  hipLaunchKernelGGL(reduce_partial_kernel, dim3(blocks), dim3(256), 0, st, kind, a, b, ld, npix, zc,
+                     (double*)workspace);
+  hipLaunchKernelGGL(reduce_final_kernel, dim3(1), dim3(256), 0, st, (const double*)workspace, blocks, scale, out);
+  return launch_status();
+}
+
+int mvae_kl_bwd(const float* mu, const float* logvar, long long ld, const float* gscale, double mult, float* dmu,
+                float* dlogvar, long long npix, int zc, void* stream) {
+  if (npix <= 0 || zc <= 0) { set_error("kl_bwd: bad sizes"); return MVAE_EINVAL; }
+  hipLaunchKernelGGL(kl_bwd_kernel, dim3(egrid(npix * zc)), dim3(256), 0, (hipStream_t)stream, mu, logvar, ld, gscale,
+                     mult, dmu, dlogvar, npix, zc);
+  return launch_status();
+}
+
+int mvae_recon_bwd(int kind, const float* a, const float* b, const float* gscale, double mult, float* da, long long n,
+                   void* stream) {
+  if ((kind != 1 && kind != 2) || n <= 0) { set_error("recon_bwd: bad args"); return MVAE_EINVAL; }
+  hipLaunchKernelGGL(recon_bwd_kernel, dim3(egrid(n)), dim3(256), 0, (hipStream_t)stream, kind, a, b, gscale, mult, da,
+                     n);
+  return launch_status();
+}
+
+}  // extern "C"

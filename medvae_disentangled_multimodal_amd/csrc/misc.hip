@@ -1,0 +1,123 @@
+// Small helpers of the convolution backward pass.
+//   * weight re-layout for dgrad: KRSC [Cout][R][S][Cin] -> [Cin][R][S][Cout]
+//   * dgrad weights of Upsample's conv (nearest x2 then 3x3, encoder_decoder.py:205-209): the
+//     gradient w.r.t. the LOW-resolution input is a stride-2, pad-1 4x4 convolution of dY with the
+//     tap-summed kernel Weff[t] = sum{ W[r] : 2-r == t or 3-r == t } per spatial axis, which skips
+//     the 4x-upsampled intermediate gradient entirely (16 taps on H*W instead of 9 on 4*H*W).
+//   * bias gradient: fixed-order column sums of dY [pixels][Cout].
+#include "common.h"
+#include <algorithm>
+
+namespace mvae {
+
+__global__ void w_transpose_kernel(const float* __restrict__ w, float* __restrict__ wt, int cout, int rs, int cin) {
+  const long long n = (long long)cout * rs * cin;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    // e indexes the destination [cin][rs][cout]
+    const int o = (int)(e % cout);
+    const long long q = e / cout;
+    const int t = (int)(q % rs);
+    const int c = (int)(q / rs);
+    wt[e] = w[((long long)o * rs + t) * cin + c];
+  }
+}
+
+__device__ __forceinline__ int tap_mask(int t) {
+  // bit r set when source tap r contributes to effective tap t
+  return t == 0 ? 0b100 : t == 1 ? 0b110 : t == 2 ? 0b011 : 0b001;
+}
+
+__global__ void w_ups_dgrad_kernel(const float* __restrict__ w, float* __restrict__ wt, int cout, int cin) {
+  const long long n = (long long)cin * 16 * cout;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int o = (int)(e % cout);
+    const long long q = e / cout;
+    const int tu = (int)(q % 16);
+    const int c = (int)(q / 16);
+    const int mt = tap_mask(tu >> 2), mu = tap_mask(tu & 3);
+    float s = 0.f;
+    for (int r = 0; r < 3; ++r) {
+      if (!((mt >> r) & 1)) continue;
+      for (int u = 0; u < 3; ++u)
+        if ((mu >> u) & 1) s += w[(((long long)o * 3 + r) * 3 + u) * cin + c];
+    }
+    wt[e] = s;
+  }
+}
+
+// column sums: part[chunk][n] = sum over rows in chunk ; then out[n] += sum_chunks (fixed order)
+__global__ void __launch_bounds__(256) colsum_partial_kernel(const float* __restrict__ x, long long rows, int n,
+                                                             long long ld, int rows_per_chunk,
+                                                             double* __restrict__ part) {
+  __shared__ double sh[256];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const long long r0 = (long long)blockIdx.y * rows_per_chunk;
+  const long long r1 = std::min<long long>(rows, r0 + rows_per_chunk);
+  double acc = 0;
+  if (col < n)
+    for (long long r = r0 + rg; r < r1; r += 4) acc += x[r * ld + col];
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  if (rg == 0 && col < n) part[(long long)blockIdx.y * n + col] = sh[threadIdx.x] + sh[threadIdx.x + 64] +
+                                                                 sh[threadIdx.x + 128] + sh[threadIdx.x + 192];
+}
+
+__global__ void colsum_final_kernel(const double* __restrict__ part, int chunks, int n, float* out, float beta) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= n) return;
+  double s = 0;
+  for (int c = 0; c < chunks; ++c) s += part[(long long)c * n + col];
+  out[col] = (beta != 0.f ? beta * out[col] : 0.f) + (float)s;
+}
+
+static int colsum_chunks(long long rows, int n) {
+  const int colblocks = (n + 63) / 64;
+  long long chunks = std::max<long long>(1, 1024 / colblocks);
+  chunks = std::min<long long>(chunks, std::max<long long>(1, rows / 64));
+  return (int)chunks;
+}
+
+static int egrid(long long n) { return (int)std::max<long long>(1, std::min<long long>((n + 255) / 256, 8192)); }
+
+}  // namespace mvae
+
+using namespace mvae;
+
+extern "C" {
+
+int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int kw, int cin, void* stream) {
+  if (cout <= 0 || kh <= 0 || kw <= 0 || cin <= 0) { set_error("w_transpose: bad sizes"); return MVAE_EINVAL; }
+  hipLaunchKernelGGL(w_transpose_kernel, dim3(egrid((long long)cout * kh * kw * cin)), dim3(256), 0,
+                     (hipStream_t)stream, w, wt, cout, kh * kw, cin);
+  return launch_status();
+}
+
+// wt [cin][4][4][cout] for the dgrad of "nearest-x2 upsample then 3x3 conv"
+int mvae_conv_weight_upsample_dgrad(const float* w, float* wt, int cout, int cin, void* stream) {
+  if (cout <= 0 || cin <= 0) { set_error("w_ups: bad sizes"); return MVAE_EINVAL; }
+  hipLaunchKernelGGL(w_ups_dgrad_kernel, dim3(egrid((long long)cin * 16 * cout)), dim3(256), 0, (hipStream_t)stream,
+                     w, wt, cout, cin);
+  return launch_status();
+}
+
+size_t mvae_bias_grad_workspace_bytes(long long rows, int n) {
+  return (size_t)colsum_chunks(rows, n) * n * sizeof(double);
+}
+
+// out[n] = beta*out[n] + sum_rows x[row*ld + n]
+int mvae_bias_grad(const float* x, long long rows, int n, long long ld, float* out, float beta, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+  if (rows <= 0 || n <= 0) { set_error("bias_grad: bad sizes"); return MVAE_EINVAL; }
+  const int chunks = colsum_chunks(rows, n);
+  if (workspace_bytes < (size_t)chunks * n * sizeof(double)) { set_error("bias_grad: workspace"); return MVAE_EWORKSPACE; }
+  const int rpc = (int)((rows + chunks - 1) / chunks);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3((n + 63) / 64, chunks), dim3(256), 0, st, x, rows, n, ld, rpc,
+                     (double*)workspace);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((n + 255) / 256), dim3(256), 0, st, (const double*)workspace, chunks, n,
+                     out, beta);
+  return launch_status();
+}
+
+}  // extern "C"

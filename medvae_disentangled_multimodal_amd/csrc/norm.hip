@@ -1,0 +1,385 @@
+// GroupNorm (+ SiLU, + inverted dropout) forward/backward over NHWC activations, and the
+// attention row-softmax. Reference: Normalize = nn.GroupNorm(min(32,C), C, eps=1e-6, affine)
+// (encoder_decoder.py:28-33), nonlinearity = x*sigmoid(x) (:13-15), nn.Dropout in ResnetBlock
+// (:160-163), softmax(dim=2) in AttnBlock (:96-97).
+//
+// Layout: x is [nb][HW][C] (C contiguous). Statistics are per (sample, group) over HW x C/G.
+// Every reduction is two-stage and fixed-order (per-block partials in fp64 -> finalize), so the
+// results are bitwise reproducible run to run.
+#include "common.h"
+#include <algorithm>
+
+namespace mvae {
+
+// counter-based hash -> uniform [0,1) for the dropout mask (recomputed in backward, never stored)
+__device__ __forceinline__ float hash_uniform(unsigned long long seed, unsigned long long idx) {
+  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(unsigned)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// Per-channel partial sums over a chunk of rows of one sample.
+//   kind 0 (stats):  s0 = sum x,          s1 = sum x^2
+//   kind 1 (bwd):    s0 = sum dyn,        s1 = sum dyn * xhat
+// where dyn is the gradient w.r.t. the GroupNorm output (through SiLU / dropout if fused).
+struct GnArgs {
+  const float* x;
+  const float* dy;
+  const float* mean;   // [nb*G]
+  const float* rstd;   // [nb*G]
+  const float* gamma;
+  const float* beta;
+  int nb, hw, C, G, rows_per_chunk, chunks;
+  int silu;
+  float drop_p;
+  unsigned long long seed;
+  double* ws;  // [nb][chunks][C][2]
+};
+
+__device__ __forceinline__ float gn_dyn(const GnArgs& a, float xv, float dyv, float m, float rs, int c,
+                                        long long idx) {
+  float d = dyv;
+  if (a.drop_p > 0.f) {
+    const float u = hash_uniform(a.seed, (unsigned long long)idx);
+    d = (u >= a.drop_p) ? d / (1.f - a.drop_p) : 0.f;
+  }
+  if (a.silu) {
+    const float yn = (xv - m) * rs * a.gamma[c] + a.beta[c];
+    const float s = sigmoid_f(yn);
+    d = d * s * (1.f + yn * (1.f - s));
+  }
+  return d;
+}
+
+template <int KIND>
+__global__ void __launch_bounds__(256) gn_partial_kernel(GnArgs a) {
+  const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
+  const int C4 = a.C >> 2;
+  const int rpar = C4 >= 256 ? 1 : 256 / C4;  // rows processed in parallel
+  const int row_lo = chunk * a.rows_per_chunk;
+  const int row_hi = min(a.hw, row_lo + a.rows_per_chunk);
+  const int cpg = a.C / a.G;
+  __shared__ double red[256 * 8];
+  const long long sbase = (long long)b * a.hw * a.C;
+  // thread -> (column group, row phase); for C4 > 256 a thread owns several column groups
+  for (int cg0 = 0; cg0 < C4; cg0 += 256) {
+    const int c4 = (C4 >= 256) ? cg0 + tid : tid % C4;
+    const int rph = (C4 >= 256) ? 0 : tid / C4;
+    const bool act = (C4 >= 256) ? (c4 < C4) : (tid < rpar * C4);
+    double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
+    if (act) {
+      float m[4] = {0, 0, 0, 0}, rs[4] = {0, 0, 0, 0};
+      if (KIND == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int g = (c4 * 4 + e) / cpg;
+          m[e] = a.mean[b * a.G + g];
+          rs[e] = a.rstd[b * a.G + g];
+        }
+      }
+      for (int row = row_lo + rph; row < row_hi; row += rpar) {
+        const long long off = sbase + (long long)row * a.C + c4 * 4;
+        const float4 xv = *(const float4*)(a.x + off);
+        const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+        if (KIND == 0) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            s0[e] += xs[e];
+            s1[e] += (double)xs[e] * xs[e];
+          }
+        } else {
+          const float4 dv = *(const float4*)(a.dy + off);
+          const float ds[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = gn_dyn(a, xs[e], ds[e], m[e], rs[e], c4 * 4 + e, off + e);
+            s0[e] += d;
+            s1[e] += (double)d * ((xs[e] - m[e]) * rs[e]);
+          }
+        }
+      }
+    }
+    // reduce the rpar row phases that share a column group
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[tid * 8 + e] = s0[e];
+      red[tid * 8 + 4 + e] = s1[e];
+    }
+    __syncthreads();
+    if (act && rph == 0) {
+      for (int p = 1; p < rpar; ++p) {
+        const int t2 = tid + p * C4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s0[e] += red[t2 * 8 + e];
+          s1[e] += red[t2 * 8 + 4 + e];
+        }
+      }
+      double* w = a.ws + (((long long)b * a.chunks + chunk) * a.C + c4 * 4) * 2;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        w[2 * e] = s0[e];
+        w[2 * e + 1] = s1[e];
+      }
+    }
+    __syncthreads();
+    if (C4 < 256) break;
+  }
+}
+
+// stats finalize: one thread per (b, g) -> mean, rstd, and per-(b,c) scale/shift for the apply
+__global__ void gn_stats_finalize_kernel(GnArgs a, float* mean, float* rstd, float* scale, float* shift,
+                                         float eps) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.nb * a.G) return;
+  const int b = i / a.G, g = i - b * a.G;
+  const int cpg = a.C / a.G;
+  double s0 = 0, s1 = 0;
+  for (int ch = 0; ch < a.chunks; ++ch) {
+    const double* w = a.ws + (((long long)b * a.chunks + ch) * a.C + g * cpg) * 2;
+    for (int c = 0; c < cpg; ++c) {
+      s0 += w[2 * c];
+      s1 += w[2 * c + 1];
+    }
+  }
+  const double n = (double)a.hw * cpg;
+  const double mu = s0 / n;
+  double var = s1 / n - mu * mu;
+  if (var < 0) var = 0;
+  const float rs = (float)(1.0 / sqrt(var + (double)eps));
+  mean[i] = (float)mu;
+  rstd[i] = rs;
+  for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+    const float sc = rs * a.gamma[c];
+    scale[b * a.C + c] = sc;
+    shift[b * a.C + c] = a.beta[c] - (float)mu * sc;
+  }
+}
+
+__global__ void __launch_bounds__(256) gn_apply_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, int nb, int hw, int C,
+                                                       int silu, float drop_p, unsigned long long seed) {
+  const int C4 = C >> 2;
+  const long long total4 = (long long)nb * hw * C4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total4;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(e % C4);
+    const int b = (int)(e / ((long long)hw * C4));
+    const float4 sc = *(const float4*)(scale + (long long)b * C + c4 * 4);
+    const float4 sh = *(const float4*)(shift + (long long)b * C + c4 * 4);
+    const float4 xv = *(const float4*)(x + e * 4);
+    float o[4] = {xv.x * sc.x + sh.x, xv.y * sc.y + sh.y, xv.z * sc.z + sh.z, xv.w * sc.w + sh.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (silu) o[k] = o[k] * sigmoid_f(o[k]);
+      if (drop_p > 0.f) {
+        const float u = hash_uniform(seed, (unsigned long long)(e * 4 + k));
+        o[k] = (u >= drop_p) ? o[k] / (1.f - drop_p) : 0.f;
+      }
+    }
+    *(float4*)(y + e * 4) = float4{o[0], o[1], o[2], o[3]};
+  }
+}
+
+// backward finalize: per (b,g) coefficients so that dx = dyn*k1[b,c] + x*k2[b,g] + k3[b,g]
+__global__ void gn_bwd_finalize_kernel(GnArgs a, float* k1, float* k2, float* k3) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.nb * a.G) return;
+  const int b = i / a.G, g = i - b * a.G;
+  const int cpg = a.C / a.G;
+  double A1 = 0, A2 = 0;
+  for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+    double s0 = 0, s1 = 0;
+    for (int ch = 0; ch < a.chunks; ++ch) {
+      const double* w = a.ws + (((long long)b * a.chunks + ch) * a.C + c) * 2;
+      s0 += w[0];
+      s1 += w[1];
+    }
+    A1 += (double)a.gamma[c] * s0;
+    A2 += (double)a.gamma[c] * s1;
+    k1[b * a.C + c] = a.rstd[i] * a.gamma[c];
+  }
+  const double n = (double)a.hw * cpg;
+  const double rs = a.rstd[i], mu = a.mean[i];
+  k2[i] = (float)(-rs * rs * A2 / n);
+  k3[i] = (float)(-rs * A1 / n + mu * rs * rs * A2 / n);
+}
+
+// dgamma[c] += sum_{b,chunks} s1 ; dbeta[c] += sum s0  (fixed order)
+__global__ void gn_param_grad_kernel(GnArgs a, float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.C) return;
+  double s0 = 0, s1 = 0;
+  for (int b = 0; b < a.nb; ++b)
+    for (int ch = 0; ch < a.chunks; ++ch) {
+      const double* w = a.ws + (((long long)b * a.chunks + ch) * a.C + c) * 2;
+      s0 += w[0];
+      s1 += w[1];
+    }
+  if (dgamma) dgamma[c] += (float)s1;
+  if (dbeta) dbeta[c] += (float)s0;
+}
+
+__global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __restrict__ k1,
+                                                    const float* __restrict__ k2, const float* __restrict__ k3,
+                                                    float* __restrict__ dx) {
+  const int C4 = a.C >> 2;
+  const int cpg = a.C / a.G;
+  const long long total4 = (long long)a.nb * a.hw * C4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total4;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(e % C4);
+    const int b = (int)(e / ((long long)a.hw * C4));
+    const float4 xv = *(const float4*)(a.x + e * 4);
+    const float4 dv = *(const float4*)(a.dy + e * 4);
+    const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+    const float ds[4] = {dv.x, dv.y, dv.z, dv.w};
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = c4 * 4 + k;
+      const int bg = b * a.G + c / cpg;
+      const float d = gn_dyn(a, xs[k], ds[k], a.mean[bg], a.rstd[bg], c, e * 4 + k);
+      o[k] = d * k1[(long long)b * a.C + c] + xs[k] * k2[bg] + k3[bg];
+    }
+    *(float4*)(dx + e * 4) = float4{o[0], o[1], o[2], o[3]};
+  }
+}
+
+static int gn_chunks(int nb, int hw) {
+  int chunks = 1;
+  while ((long long)nb * chunks < 1024 && hw / (chunks * 2) >= 16) chunks *= 2;
+  return chunks;
+}
+
+static int grid_for(long long n4) { return (int)std::min<long long>((n4 + 255) / 256, 8192); }
+
+}  // namespace mvae
+
+using namespace mvae;
+
+extern "C" {
+
+size_t mvae_group_norm_workspace_bytes(int nb, int hw, int c) {
+  const int ch = gn_chunks(nb, hw);
+  // fp64 partials + 3 float arrays of nb*C (scale/shift or k1) + 2 of nb*C (k2/k3 upper bound)
+  return (size_t)nb * ch * c * 2 * sizeof(double) + (size_t)nb * c * 5 * sizeof(float) + 256;
+}
+
+// y = [dropout](silu?(GroupNorm(x)))  ; saves mean/rstd [nb*groups]
+int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* beta, float* y, float* mean,
+                             float* rstd, int nb, int hw, int c, int groups, float eps, int silu,
+                             float drop_p, unsigned long long seed, void* workspace, size_t workspace_bytes,
+                             void* stream) {
+  if (nb <= 0 || hw <= 0 || c <= 0 || (c & 3) || groups <= 0 || c % groups) {
+    set_error("group_norm: C must be a multiple of 4 and of groups");
+    return MVAE_EINVAL;
+  }
+  if (workspace_bytes < mvae_group_norm_workspace_bytes(nb, hw, c)) {
+    set_error("group_norm: workspace too small");
+    return MVAE_EWORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  GnArgs a{};
+  a.x = x; a.gamma = gamma; a.beta = beta; a.nb = nb; a.hw = hw; a.C = c; a.G = groups;
+  a.chunks = gn_chunks(nb, hw);
+  a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
+  a.ws = (double*)workspace;
+  float* scale = (float*)((char*)workspace + (size_t)nb * a.chunks * c * 2 * sizeof(double));
+  float* shift = scale + (size_t)nb * c;
+  hipLaunchKernelGGL(gn_partial_kernel<0>, dim3(a.chunks, nb), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(gn_stats_finalize_kernel, dim3(cdiv((long long)nb * groups, 256)), dim3(256), 0, st, a,
+                     mean, rstd, scale, shift, eps);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(grid_for((long long)nb * hw * c / 4)), dim3(256), 0, st, x, y, scale,
+                     shift, nb, hw, c, silu, drop_p, seed);
+  return launch_status();
+}
+
+// dx = d/dx of the fused forward; dgamma/dbeta are ACCUMULATED (+=) when non-null.
+int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
+                             const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta,
+                             int nb, int hw, int c, int groups, int silu, float drop_p,
+                             unsigned long long seed, void* workspace, size_t workspace_bytes, void* stream) {
+  if (nb <= 0 || hw <= 0 || c <= 0 || (c & 3) || groups <= 0 || c % groups) {
+    set_error("group_norm_bwd: bad geometry");
+    return MVAE_EINVAL;
+  }
+  if (workspace_bytes < mvae_group_norm_workspace_bytes(nb, hw, c)) {
+    set_error("group_norm_bwd: workspace too small");
+    return MVAE_EWORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  GnArgs a{};
+  a.x = x; a.dy = dy; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta;
+  a.nb = nb; a.hw = hw; a.C = c; a.G = groups; a.silu = silu; a.drop_p = drop_p; a.seed = seed;
+  a.chunks = gn_chunks(nb, hw);
+  a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
+  a.ws = (double*)workspace;
+  float* k1 = (float*)((char*)workspace + (size_t)nb * a.chunks * c * 2 * sizeof(double));
+  float* k2 = k1 + (size_t)nb * c;
+  float* k3 = k2 + (size_t)nb * c;
+  hipLaunchKernelGGL(gn_partial_kernel<1>, dim3(a.chunks, nb), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(cdiv((long long)nb * groups, 256)), dim3(256), 0, st, a, k1,
+                     k2, k3);
+  if (dgamma || dbeta)
+    hipLaunchKernelGGL(gn_param_grad_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st, a, dgamma, dbeta);
+  hipLaunchKernelGGL(gn_dx_kernel, dim3(grid_for((long long)nb * hw * c / 4)), dim3(256), 0, st, a, k1, k2, k3,
+                     dx);
+  return launch_status();
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// row softmax (attention probabilities): one wave per row
+// ------------------------------------------------------------------------------------------
+namespace mvae {
+__global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                           long long rows, int n) {
+  const long long row = blockIdx.x * 4LL + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* xr = x + row * n;
+  float* yr = y + row * n;
+  float m = -INFINITY;
+  for (int j = lane; j < n; j += 64) m = fmaxf(m, xr[j]);
+  m = wave_max_f(m);
+  float s = 0.f;
+  for (int j = lane; j < n; j += 64) s += __expf(xr[j] - m);
+  s = wave_sum_f(s);
+  const float inv = 1.f / s;
+  for (int j = lane; j < n; j += 64) yr[j] = __expf(xr[j] - m) * inv;
+}
+
+__global__ void __launch_bounds__(256) softmax_rows_bwd_kernel(const float* __restrict__ y,
+                                                               const float* __restrict__ dy,
+                                                               float* __restrict__ dx, long long rows, int n) {
+  const long long row = blockIdx.x * 4LL + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* yr = y + row * n;
+  const float* dr = dy + row * n;
+  float s = 0.f;
+  for (int j = lane; j < n; j += 64) s += yr[j] * dr[j];
+  s = wave_sum_f(s);
+  for (int j = lane; j < n; j += 64) dx[row * n + j] = yr[j] * (dr[j] - s);
+}
+}  // namespace mvae
+
+extern "C" {
+int mvae_softmax_rows(const float* x, float* y, long long rows, int n, void* stream) {
+  if (rows <= 0 || n <= 0) { set_error("softmax: bad sizes"); return MVAE_EINVAL; }
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x,
+                     y, rows, n);
+  return launch_status();
+}
+int mvae_softmax_rows_bwd(const float* y, const float* dy, float* dx, long long rows, int n, void* stream) {
+  if (rows <= 0 || n <= 0) { set_error("softmax_bwd: bad sizes"); return MVAE_EINVAL; }
+  hipLaunchKernelGGL(softmax_rows_bwd_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                     y, dy, dx, rows, n);
+  return launch_status();
+}
+}  // extern "C"

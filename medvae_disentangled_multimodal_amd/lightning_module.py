@@ -1,0 +1,164 @@
+"""Training module with the reference LightningModule contract (src/lightning_module.py:18-477).
+
+`VAELightningModule(model, optimizer_config, scheduler_config, loss_config)` keeps the reference's
+constructor, `forward`, `training_step(batch, batch_idx) -> loss`, `configure_optimizers`,
+loss-type switch and `train/<key>` logging keys. Dispatch is by capability (what the model's forward
+takes), not `isinstance` against the reference classes.
+
+The optimizer hooks of the reference -- zero non-finite grads per tensor (on_before_optimizer_step,
+:468-477), global-norm clipping (configure_gradient_clipping, :452-466) and Adam/AdamW (:390-408) --
+run as ONE fused device-side kernel chain (`FusedAdam.step`) over a flat parameter buffer, in that
+order and with the reference's per-tensor semantics. `fit_step` is the whole hot path of one
+Lightning optimisation step: zero_grad -> training_step -> backward -> [all-reduce] -> fused step.
+"""
+from __future__ import annotations
+
+import inspect
+from typing import Any, Dict, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .disentangled import DisentangledConditionalVAE
+from .losses import DisentangledVAELoss, LPIPSLoss, VAELoss
+from .optim import Adam, AdamW, FlatParameters, FusedAdam
+from .schedulers import get_scheduler
+
+try:  # Lightning is optional: the module works stand-alone
+    import lightning as L  # type: ignore
+    _Base = L.LightningModule
+except Exception:  # pragma: no cover - not installed in this image
+    _Base = nn.Module
+
+
+def _model_kind(model: nn.Module) -> str:
+    if isinstance(model, DisentangledConditionalVAE) or hasattr(model, "modality_decoders"):
+        return "indices"
+    params = list(inspect.signature(model.forward).parameters)
+    if len(params) >= 2 and params[1] in ("condition", "modality_indices"):
+        return "condition"
+    return "plain"
+
+
+class VAELightningModule(_Base):
+    def __init__(self, model: nn.Module, optimizer_config: Dict[str, Any], scheduler_config: Dict[str, Any],
+                 loss_config: Dict[str, Any], gradient_clip_val: Optional[float] = None, **kwargs):
+        super().__init__()
+        self.model = model
+        self.optimizer_config = dict(optimizer_config)
+        self.scheduler_config = dict(scheduler_config or {"type": "none"})
+        self.loss_config = dict(loss_config)
+        self.gradient_clip_val = gradient_clip_val
+        self._kind = _model_kind(model)
+        self._setup_loss()
+        self.automatic_optimization = True
+        self.flat: Optional[FlatParameters] = None
+        self.optimizer: Optional[FusedAdam] = None
+        self.scheduler = None
+        self.logged: Dict[str, torch.Tensor] = {}
+        self.process_group = None  # set by ddp.DataParallel
+        self._usage = None
+
+    def _setup_loss(self):
+        t = self.loss_config.get("type", "vae")
+        if t == "vae":
+            self.criterion = VAELoss(recon_loss_type=self.loss_config.get("recon_loss_type", "mse"),
+                                     kl_weight=self.loss_config.get("kl_weight", 1.0),
+                                     recon_weight=self.loss_config.get("recon_weight", 1.0))
+        elif t == "disentangled_vae":
+            self.criterion = DisentangledVAELoss(
+                recon_loss_type=self.loss_config.get("recon_loss_type", "mse"),
+                kl_weight=self.loss_config.get("kl_weight", 1.0),
+                recon_weight=self.loss_config.get("recon_weight", 1.0),
+                separation_weight=self.loss_config.get("separation_weight", 0.1),
+                contrastive_weight=self.loss_config.get("contrastive_weight", 0.05))
+        elif t == "lpips":
+            self.criterion = LPIPSLoss()
+        else:
+            raise ValueError(f"Unknown/unsupported loss type on the MI355X path: {t}")
+        self.use_discriminator = False
+
+    # ---------------------------------------------------------------------------------------
+    def forward(self, x, condition=None, **kw):
+        if self._kind != "plain" and condition is not None:
+            return self.model(x, condition, **kw)
+        return self.model(x, **kw)
+
+    def log(self, name, value, **kwargs):  # Lightning-compatible signature; keeps device tensors
+        self.logged[name] = value.detach() if torch.is_tensor(value) else value
+
+    def training_step(self, batch, batch_idx: int, eps: Optional[torch.Tensor] = None):
+        if len(batch) == 4:
+            x, labels, modality, modality_indices = batch
+        elif len(batch) == 3:
+            x, labels, modality = batch
+            modality_indices = None
+        else:
+            x, labels = batch[0], batch[1] if len(batch) > 1 else None
+            modality, modality_indices = None, None
+        kw = {} if eps is None else {"eps": eps}
+        if self._kind == "indices" and modality is not None:
+            if modality_indices is None:
+                modality_indices = torch.argmax(modality, dim=1)
+            self._usage = modality_indices
+            outputs = self.model(x, modality_indices, **kw)
+        elif self._kind == "condition" and modality is not None:
+            outputs = self.model(x, modality, **kw)
+        else:
+            outputs = self.model(x, **kw)
+        if isinstance(self.criterion, DisentangledVAELoss):
+            loss_dict = self.criterion(outputs, x)
+        else:
+            loss_dict = self.criterion(inputs=x, reconstructions=outputs["reconstruction"],
+                                       posteriors=outputs["posterior"], priors=outputs["prior"])
+        loss = loss_dict["loss"]
+        loss = torch.where(torch.isfinite(loss), loss, torch.full_like(loss, 1e6))
+        for k, v in loss_dict.items():
+            self.log(f"train/{k}", v, prog_bar=True, logger=True, on_step=True, on_epoch=True)
+        self._last_outputs = outputs
+        return loss
+
+    # ---------------------------------------------------------------------------------------
+    def configure_optimizers(self):
+        if self.flat is None:
+            self.flat = FlatParameters(self.model)
+        oc = self.optimizer_config
+        betas = tuple(oc.get("betas", (0.9, 0.999)))
+        if oc["type"] == "adam":
+            opt = Adam(self.flat, lr=oc["lr"], betas=betas, weight_decay=oc.get("weight_decay", 0))
+        elif oc["type"] == "adamw":
+            opt = AdamW(self.flat, lr=oc["lr"], betas=betas, weight_decay=oc.get("weight_decay", 1e-4))
+        else:
+            raise ValueError(f"Unknown optimizer: {oc['type']}")
+        opt.max_grad_norm = self.gradient_clip_val
+        self.optimizer = opt
+        self.scheduler = get_scheduler(opt, self.scheduler_config)
+        if self.scheduler is not None:
+            return [opt], [{"scheduler": self.scheduler, "monitor": "val/loss", "interval": "epoch",
+                            "frequency": 1}]
+        return [opt]
+
+    def _used_mask(self) -> Optional[torch.Tensor]:
+        if self._kind != "indices" or self._usage is None:
+            return None
+        f = self.flat
+        if not hasattr(self, "_param_mod"):
+            self._param_mod = torch.tensor([self.model.parameter_modality(n) for n in f.names],
+                                           dtype=torch.long, device=f.device)
+        present = self.model.modality_presence(self._usage.to(f.device))
+        pm = self._param_mod
+        used = (pm == -1) | ((pm >= 0) & present[pm.clamp_min(0)])
+        return used.to(torch.int32)
+
+    def fit_step(self, batch, batch_idx: int = 0, eps: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One automatic-optimisation step of Lightning's loop, fused."""
+        if self.optimizer is None:
+            self.configure_optimizers()
+        self.model.train()
+        self.optimizer.zero_grad()
+        loss = self.training_step(batch, batch_idx, eps=eps)
+        loss.backward()
+        if self.process_group is not None:
+            self.process_group.allreduce_gradients(self.flat)
+        self.optimizer.step(used=self._used_mask())
+        return loss

@@ -1,0 +1,488 @@
+"""Autograd functions over the C-ABI kernels (libmvae_hip.so).
+
+Activations are torch tensors with the reference's logical NCHW shapes stored channels_last
+(physical NHWC); conv weights are channels_last OIHW (physical KRSC). Weight / norm-affine
+gradients are written straight into the parameter's flat gradient slot (`p._mvae_main_grad`,
+attached by `FlatParameters`) and accumulated there (beta = 1), so autograd never materialises
+or adds them; without a flat slot the gradient is returned to autograd as usual.
+Every op requires CUDA(HIP) tensors: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+
+CL = torch.channels_last
+
+
+# ------------------------------------------------------------------------------------------
+# plumbing
+# ------------------------------------------------------------------------------------------
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _check(t: torch.Tensor, name: str = "tensor"):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name}: the MI355X path needs device tensors (got {t.device}); no CPU fallback")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name}: expected float32, got {t.dtype}")
+
+
+def nhwc(t: torch.Tensor) -> torch.Tensor:
+    """Return t with channels_last (NHWC) physical layout (no copy when it already is)."""
+    if t.dim() == 4:
+        return t if t.is_contiguous(memory_format=CL) else t.contiguous(memory_format=CL)
+    return t.contiguous()
+
+
+class _Arena:
+    """Per-device scratch buffers reused across launches (all work is ordered on one stream)."""
+
+    def __init__(self):
+        self.bufs = {}
+
+    def get(self, key: str, nbytes: int, device) -> torch.Tensor:
+        k = (key, str(device))
+        t = self.bufs.get(k)
+        if t is None or t.numel() < nbytes:
+            t = torch.empty(max(int(nbytes * 1.25) + 256, 256), dtype=torch.uint8, device=device)
+            self.bufs[k] = t
+        return t
+
+
+ARENA = _Arena()
+
+# Optional live kernel timing (bench.py): when PROFILE is a list, every implicit-GEMM launch is
+# bracketed by HIP events on the current stream and recorded as (tag, algorithmic_flops, start, end).
+PROFILE = None
+
+
+class _timed:
+    __slots__ = ("tag", "flops", "s")
+
+    def __init__(self, tag: str, flops: float):
+        self.tag, self.flops = tag, flops
+
+    def __enter__(self):
+        if PROFILE is not None:
+            self.s = torch.cuda.Event(enable_timing=True)
+            self.s.record()
+        return self
+
+    def __exit__(self, *exc):
+        if PROFILE is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            PROFILE.append((self.tag, self.flops, self.s, e))
+        return False
+
+
+def _main_grad(p: torch.Tensor):
+    return getattr(p, "_mvae_main_grad", None)
+
+
+# ------------------------------------------------------------------------------------------
+# convolution
+# ------------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class ConvGeom:
+    kh: int
+    kw: int
+    stride: int = 1
+    pad_t: int = 0
+    pad_l: int = 0
+    pad_b: int = 0
+    pad_r: int = 0
+    upsample: bool = False  # nearest x2 upsample fused into the gather (Upsample, :205-209)
+
+    def out_hw(self, h: int, w: int) -> Tuple[int, int]:
+        if self.upsample:
+            h, w = 2 * h, 2 * w
+        ho = (h + self.pad_t + self.pad_b - self.kh) // self.stride + 1
+        wo = (w + self.pad_l + self.pad_r - self.kw) // self.stride + 1
+        return ho, wo
+
+    @property
+    def pointwise(self) -> bool:
+        return self.kh == 1 and self.kw == 1 and self.stride == 1 and not self.upsample and \
+            self.pad_t == self.pad_l == self.pad_b == self.pad_r == 0
+
+
+def _krsc(w: torch.Tensor) -> torch.Tensor:
+    return w if w.is_contiguous(memory_format=CL) else w.contiguous(memory_format=CL)
+
+
+def conv2d_forward_raw(x, w, b, res, g: ConvGeom):
+    n, c, h, wd = x.shape
+    co = w.shape[0]
+    ho, wo = g.out_hw(h, wd)
+    y = torch.empty((n, co, ho, wo), device=x.device, dtype=torch.float32, memory_format=CL)
+    with _timed("conv_fwd", 2.0 * n * ho * wo * co * c * g.kh * g.kw):
+        _conv_fwd_launch(x, w, b, res, y, g, n, c, h, wd, co, ho, wo)
+    return y
+
+
+def _conv_fwd_launch(x, w, b, res, y, g, n, c, h, wd, co, ho, wo):
+    if g.pointwise:
+        # 1x1 conv = GEMM [pixels][cin] x [cout][cin]^T
+        _lib.call("mvae_gemm_strided_batched", 0, 1, n * h * wd, co, c, 1.0, x.data_ptr(), c, 0,
+                  w.data_ptr(), c, 0, 0.0, y.data_ptr(), co, 0, 1, _ptr(b), _ptr(res), co, 0, None, 0,
+                  _stream(x))
+    else:
+        _lib.call("mvae_conv2d_nhwc", x.data_ptr(), w.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n, h, wd, c,
+                  co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, 1 if g.upsample else 0, _stream(x))
+
+
+def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom):
+    n, c, h, wd = x_shape
+    co = w.shape[0]
+    _, _, ho, wo = dy.shape
+    dx = torch.empty((n, c, h, wd), device=dy.device, dtype=torch.float32, memory_format=CL)
+    st = _stream(dy)
+    flops = 2.0 * n * ho * wo * co * c * g.kh * g.kw  # algorithmic (reference) count
+    if g.pointwise:
+        # dx[m][c] = sum_n dy[m][n] W[n][c]  (W stored [K=cout][N=cin])
+        with _timed("conv_dgrad", flops):
+            _lib.call("mvae_gemm_strided_batched", 0, 0, n * h * wd, c, co, 1.0, dy.data_ptr(), co, 0, w.data_ptr(), c,
+                      0, 0.0, dx.data_ptr(), c, 0, 1, None, None, 0, 0, None, 0, st)
+        return dx
+    if g.upsample:
+        wt = ARENA.get("wt", c * 16 * co * 4, dy.device)
+        _lib.call("mvae_conv_weight_upsample_dgrad", w.data_ptr(), wt.data_ptr(), co, c, st)
+        # dX = stride-2, pad-1 4x4 conv of dY with the tap-summed kernel
+        with _timed("conv_dgrad", flops):
+            _lib.call("mvae_conv2d_nhwc", dy.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
+                      4, 4, 2, 1, 1, h, wd, 0, st)
+        return dx
+    wt = ARENA.get("wt", c * g.kh * g.kw * co * 4, dy.device)
+    _lib.call("mvae_conv_weight_transpose", w.data_ptr(), wt.data_ptr(), co, g.kh, g.kw, c, st)
+    with _timed("conv_dgrad", flops):
+        _lib.call("mvae_conv2d_nhwc", dy.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
+                  g.kh, g.kw, g.stride, g.pad_t, g.pad_l, h, wd, 2, st)
+    return dx
+
+
+def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom):
+    n, c, h, wd = x.shape
+    co = dy.shape[1]
+    _, _, ho, wo = dy.shape
+    with _timed("conv_wgrad", 2.0 * n * ho * wo * co * c * g.kh * g.kw):
+        _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo)
+
+
+def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo):
+    st = _stream(dy)
+    if g.pointwise:
+        m = n * h * wd
+        nbytes = _lib.query("mvae_gemm_workspace_bytes", co, c, m, 1)
+        ws = ARENA.get("ws", nbytes, dy.device)
+        # dW[n][c] = sum_m dy[m][n] x[m][c]: A = dy stored [K=m][M=cout], B = x stored [K=m][N=cin]
+        _lib.call("mvae_gemm_strided_batched", 1, 0, co, c, m, 1.0, dy.data_ptr(), co, 0, x.data_ptr(), c, 0,
+                  float(beta), dw.data_ptr(), c, 0, 1, None, None, 0, 0, ws.data_ptr(), ws.numel(), st)
+        return
+    nbytes = _lib.query("mvae_conv2d_wgrad_workspace_bytes", n, c, co, g.kh, g.kw, ho, wo)
+    ws = ARENA.get("ws", nbytes, dy.device)
+    _lib.call("mvae_conv2d_wgrad_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), float(beta), n, h, wd, c, co,
+              g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, 1 if g.upsample else 0, ws.data_ptr(), ws.numel(), st)
+
+
+def bias_grad_raw(dy2d_ptr, rows, n, out, beta, device, stream):
+    nbytes = _lib.query("mvae_bias_grad_workspace_bytes", rows, n)
+    ws = ARENA.get("bias", nbytes, device)
+    _lib.call("mvae_bias_grad", dy2d_ptr, rows, n, n, out.data_ptr(), float(beta), ws.data_ptr(), ws.numel(), stream)
+
+
+class Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, geom: ConvGeom):
+        _check(x, "conv input")
+        x = nhwc(x)
+        w = _krsc(weight)
+        res = nhwc(residual) if residual is not None else None
+        y = conv2d_forward_raw(x, w, bias, res, geom)
+        ctx.geom = geom
+        ctx.has_bias = bias is not None
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, w)
+        ctx.weight_ref = weight
+        ctx.bias_ref = bias
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        g = ctx.geom
+        dy = nhwc(dy)
+        dx = dw_ret = db_ret = dres = None
+        if ctx.needs_input_grad[0]:
+            dx = conv2d_dgrad_raw(dy, w, x.shape, g)
+        if ctx.needs_input_grad[1]:
+            tgt = _main_grad(ctx.weight_ref)
+            if tgt is not None:
+                conv2d_wgrad_raw(dy, x, tgt, 1.0, g)
+            else:
+                dw_ret = torch.empty_like(w, memory_format=CL)
+                conv2d_wgrad_raw(dy, x, dw_ret, 0.0, g)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            tgt = _main_grad(ctx.bias_ref)
+            n, co, ho, wo = dy.shape
+            if tgt is not None:
+                bias_grad_raw(dy.data_ptr(), n * ho * wo, co, tgt, 1.0, dy.device, _stream(dy))
+            else:
+                db_ret = torch.empty(co, device=dy.device, dtype=torch.float32)
+                bias_grad_raw(dy.data_ptr(), n * ho * wo, co, db_ret, 0.0, dy.device, _stream(dy))
+        if ctx.has_res and ctx.needs_input_grad[3]:
+            dres = dy
+        return dx, dw_ret, db_ret, dres, None
+
+
+def conv2d(x, weight, bias, geom: ConvGeom, residual=None):
+    return Conv2dFn.apply(x, weight, bias, residual, geom)
+
+
+# ------------------------------------------------------------------------------------------
+# GroupNorm (+SiLU, +dropout)
+# ------------------------------------------------------------------------------------------
+class GroupNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool, drop_p: float, seed: int):
+        _check(x, "group_norm input")
+        x = nhwc(x)
+        n, c, h, w = x.shape
+        y = torch.empty_like(x, memory_format=CL)
+        mean = torch.empty(n * groups, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        nbytes = _lib.query("mvae_group_norm_workspace_bytes", n, h * w, c)
+        ws = ARENA.get("gn", nbytes, x.device)
+        _lib.call("mvae_group_norm_fwd_nhwc", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
+                  mean.data_ptr(), rstd.data_ptr(), n, h * w, c, groups, float(eps), int(silu), float(drop_p),
+                  int(seed) & 0xFFFFFFFFFFFFFFFF, ws.data_ptr(), ws.numel(), _stream(x))
+        ctx.save_for_backward(x, gamma, beta, mean, rstd)
+        ctx.cfg = (groups, int(silu), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF)
+        ctx.gamma_ref, ctx.beta_ref = gamma, beta
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, beta, mean, rstd = ctx.saved_tensors
+        groups, silu, drop_p, seed = ctx.cfg
+        dy = nhwc(dy)
+        n, c, h, w = x.shape
+        dx = torch.empty_like(x, memory_format=CL)
+        dg_ret = db_ret = None
+        dg = _main_grad(ctx.gamma_ref) if ctx.needs_input_grad[1] else None
+        db = _main_grad(ctx.beta_ref) if ctx.needs_input_grad[2] else None
+        if ctx.needs_input_grad[1] and dg is None:
+            dg = dg_ret = torch.zeros(c, device=x.device, dtype=torch.float32)
+        if ctx.needs_input_grad[2] and db is None:
+            db = db_ret = torch.zeros(c, device=x.device, dtype=torch.float32)
+        nbytes = _lib.query("mvae_group_norm_workspace_bytes", n, h * w, c)
+        ws = ARENA.get("gn", nbytes, x.device)
+        _lib.call("mvae_group_norm_bwd_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                  mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(dg), _ptr(db), n, h * w, c, groups, silu,
+                  drop_p, seed, ws.data_ptr(), ws.numel(), _stream(x))
+        return dx, dg_ret, db_ret, None, None, None, None, None
+
+
+def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0):
+    return GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed)
+
+
+# ------------------------------------------------------------------------------------------
+# attention core: softmax(q k^T * C^-1/2) v over the h*w tokens of each image
+# ------------------------------------------------------------------------------------------
+def _gemm(ta, tb, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, st, residual=None):
+    with _timed("attn_gemm", 2.0 * m * n * k * batch):
+        _lib.call("mvae_gemm_strided_batched", ta, tb, m, n, k, float(alpha), A.data_ptr(), lda, sA, B.data_ptr(), ldb,
+                  sB, float(beta), C.data_ptr(), ldc, sC, batch, None, _ptr(residual), ldc, sC, None, 0, st)
+
+
+class AttnCoreFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v):
+        q, k, v = nhwc(q), nhwc(k), nhwc(v)
+        b, c, h, w = q.shape
+        n = h * w
+        st = _stream(q)
+        scale = float(c) ** -0.5
+        s = torch.empty((b, n, n), device=q.device, dtype=torch.float32)
+        _gemm(0, 1, n, n, c, scale, q, c, n * c, k, c, n * c, 0.0, s, n, n * n, b, st)
+        _lib.call("mvae_softmax_rows", s.data_ptr(), s.data_ptr(), b * n, n, st)
+        o = torch.empty_like(q, memory_format=CL)
+        _gemm(0, 0, n, c, n, 1.0, s, n, n * n, v, c, n * c, 0.0, o, c, n * c, b, st)
+        ctx.save_for_backward(q, k, v, s)
+        ctx.scale = scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, p = ctx.saved_tensors
+        do = nhwc(do)
+        b, c, h, w = q.shape
+        n = h * w
+        st = _stream(q)
+        dp = torch.empty((b, n, n), device=q.device, dtype=torch.float32)
+        _gemm(0, 1, n, n, c, 1.0, do, c, n * c, v, c, n * c, 0.0, dp, n, n * n, b, st)   # dP = dO V^T
+        dv = torch.empty_like(v, memory_format=CL)
+        _gemm(1, 0, n, c, n, 1.0, p, n, n * n, do, c, n * c, 0.0, dv, c, n * c, b, st)   # dV = P^T dO
+        _lib.call("mvae_softmax_rows_bwd", p.data_ptr(), dp.data_ptr(), dp.data_ptr(), b * n, n, st)  # dS
+        dq = torch.empty_like(q, memory_format=CL)
+        _gemm(0, 0, n, c, n, ctx.scale, dp, n, n * n, k, c, n * c, 0.0, dq, c, n * c, b, st)  # dQ = dS K
+        dk = torch.empty_like(k, memory_format=CL)
+        _gemm(1, 0, n, c, n, ctx.scale, dp, n, n * n, q, c, n * c, 0.0, dk, c, n * c, b, st)  # dK = dS^T Q
+        return dq, dk, dv
+
+
+def attention_core(q, k, v):
+    return AttnCoreFn.apply(q, k, v)
+
+
+# ------------------------------------------------------------------------------------------
+# reparameterization, KL, reconstruction
+# ------------------------------------------------------------------------------------------
+def _pixel_ld(t: torch.Tensor) -> Optional[int]:
+    """Row stride between consecutive pixels for a logical-NCHW tensor whose channels are
+    contiguous; None if the tensor is not laid out that way."""
+    n, c, h, w = t.shape
+    if t.stride(1) != 1 and c > 1:
+        return None
+    ld = t.stride(3) if w > 1 else (t.stride(2) if h > 1 else (t.stride(0) if n > 1 else c))
+    if w > 1 and t.stride(3) != ld:
+        return None
+    if h > 1 and t.stride(2) != w * ld:
+        return None
+    if n > 1 and t.stride(0) != h * w * ld:
+        return None
+    return ld
+
+
+def _pix(t):
+    ld = _pixel_ld(t)
+    if ld is None:
+        t = nhwc(t)
+        ld = t.shape[1]
+    return t, ld
+
+
+class ReparamFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mean, logvar, eps):
+        _check(mean, "mean")
+        mean, ldm = _pix(mean)
+        logvar, ldl = _pix(logvar)
+        eps = nhwc(eps)
+        n, zc, h, w = mean.shape
+        z = torch.empty((n, zc, h, w), device=mean.device, dtype=torch.float32, memory_format=CL)
+        if ldm == ldl:
+            _lib.call("mvae_reparam_fwd", mean.data_ptr(), logvar.data_ptr(), ldm, eps.data_ptr(), z.data_ptr(),
+                      n * h * w, zc, _stream(mean))
+        else:
+            mean, logvar = nhwc(mean.contiguous()), nhwc(logvar.contiguous())
+            ldm = ldl = zc
+            _lib.call("mvae_reparam_fwd", mean.data_ptr(), logvar.data_ptr(), zc, eps.data_ptr(), z.data_ptr(),
+                      n * h * w, zc, _stream(mean))
+        ctx.save_for_backward(logvar, eps)
+        ctx.ld = ldl
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        logvar, eps = ctx.saved_tensors
+        dz = nhwc(dz)
+        n, zc, h, w = dz.shape
+        dlv = None
+        if ctx.needs_input_grad[1]:
+            dlv = torch.empty((n, zc, h, w), device=dz.device, dtype=torch.float32, memory_format=CL)
+            _lib.call("mvae_reparam_bwd", dz.data_ptr(), eps.data_ptr(), logvar.data_ptr(), ctx.ld, dlv.data_ptr(),
+                      n * h * w, zc, _stream(dz))
+        return (dz if ctx.needs_input_grad[0] else None), dlv, None
+
+
+def reparameterize(mean, logvar, eps):
+    return ReparamFn.apply(mean, logvar, eps)
+
+
+class KLFn(torch.autograd.Function):
+    """kind 0: mean over elements of KL(N(mu, e^{lv/2}) || N(0,1));
+    kind 3: -0.5*sum(1+lv-mu^2-e^lv) / denom (DisentangledVAELoss)."""
+
+    @staticmethod
+    def forward(ctx, mean, logvar, kind: int, denom: float):
+        mean, ldm = _pix(mean)
+        logvar, ldl = _pix(logvar)
+        if ldm != ldl:
+            mean, logvar = nhwc(mean.contiguous()), nhwc(logvar.contiguous())
+            ldm = ldl = mean.shape[1]
+        n, zc, h, w = mean.shape
+        out = torch.empty((), device=mean.device, dtype=torch.float32)
+        ws = ARENA.get("red", _lib.query("mvae_reduce_workspace_bytes"), mean.device)
+        scale = (1.0 / denom) if kind == 0 else (-0.5 / denom)
+        _lib.call("mvae_loss_reduce", kind, mean.data_ptr(), logvar.data_ptr(), ldm, n * h * w, zc, scale,
+                  out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(mean))
+        ctx.save_for_backward(mean, logvar)
+        ctx.ld, ctx.denom = ldm, denom
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        mean, logvar = ctx.saved_tensors
+        g = g.contiguous().float()
+        n, zc, h, w = mean.shape
+        dmu = torch.empty((n, zc, h, w), device=mean.device, dtype=torch.float32, memory_format=CL)
+        dlv = torch.empty_like(dmu, memory_format=CL)
+        _lib.call("mvae_kl_bwd", mean.data_ptr(), logvar.data_ptr(), ctx.ld, g.data_ptr(), 1.0 / ctx.denom,
+                  dmu.data_ptr(), dlv.data_ptr(), n * h * w, zc, _stream(mean))
+        return dmu, dlv, None, None
+
+
+def kl_standard_normal_mean(mean, logvar):
+    return KLFn.apply(mean, logvar, 0, float(mean.numel()))
+
+
+def kl_closed_form_sum(mean, logvar, denom):
+    return KLFn.apply(mean, logvar, 3, float(denom))
+
+
+class ReconFn(torch.autograd.Function):
+    """mean((a-b)^2) (kind 1) or mean|a-b| (kind 2); gradient w.r.t. a only."""
+
+    @staticmethod
+    def forward(ctx, a, b, kind: int):
+        _check(a, "reconstruction")
+        a = nhwc(a)
+        b = nhwc(b.to(device=a.device, dtype=torch.float32))
+        out = torch.empty((), device=a.device, dtype=torch.float32)
+        ws = ARENA.get("red", _lib.query("mvae_reduce_workspace_bytes"), a.device)
+        n = a.numel()
+        _lib.call("mvae_loss_reduce", kind, a.data_ptr(), b.data_ptr(), 1, n, 1, 1.0 / n, out.data_ptr(),
+                  ws.data_ptr(), ws.numel(), _stream(a))
+        ctx.save_for_backward(a, b)
+        ctx.kind = kind
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.contiguous().float()
+        da = torch.empty_like(a, memory_format=CL) if a.dim() == 4 else torch.empty_like(a)
+        _lib.call("mvae_recon_bwd", ctx.kind, a.data_ptr(), b.data_ptr(), g.data_ptr(), 1.0 / a.numel(),
+                  da.data_ptr(), a.numel(), _stream(a))
+        return da, None, None
+
+
+def mse_mean(a, b):
+    return ReconFn.apply(a, b, 1)
+
+
+def l1_mean(a, b):
+    return ReconFn.apply(a, b, 2)
