@@ -8,14 +8,23 @@
 //   attention  (Q.K^T, P.V and their backward products; batched)     encoder_decoder.py:83-107
 //
 // Numerics ("3xBF16"): every fp32 operand x is split into hi = bf16(x), lo = bf16(x - hi) when it
-// is staged into LDS; a product is hi*hi + hi*lo + lo*hi accumulated in fp32 by
+// is staged into LDS; a product is lo*hi + hi*lo + hi*hi accumulated in fp32 by
 // v_mfma_f32_32x32x16_bf16. Relative error per product ~1e-5 (vs 6e-8 for fp32), far inside the
 // 1e-3 parity budget, at 3/16 of the bf16 MFMA cost = 5.3x the fp32-MFMA rate.
 //
-// Tile: BM x BN x 32, 256 threads = 4 waves in 2x2, each wave owns (BM/2)x(BN/2) = 32x32 MFMA tiles.
-// LDS: hi/lo bf16 planes of A[BM][32] and B[BN][32], rows padded to 40 elements (80 B) so the
-// ds_read_b128 fragment reads are bank-conflict free; double-buffered, register-staged loads
-// (global loads for tile t+1 are in flight while tile t is multiplied), one barrier per K-tile.
+// Tiles: BM x BN x 32 per workgroup of WGM x WGN waves; each wave owns a (BM/WGM) x (BN/WGN) block of
+// 32x32 MFMA tiles. Register-staged, double-buffered LDS: global loads of K-tile t+1 are in flight
+// while tile t is multiplied; one barrier per K-tile.
+// LDS images (hi and lo bf16 planes per operand):
+//   ROW image [ROWS][40]      for k-contiguous sources (weights, im2col rows); 80-B rows make the
+//                             ds_read_b128 fragment reads bank-conflict free
+//   COL image [32][ROWS+32]   for row-contiguous sources (dY^T, im2col columns of wgrad, P/V of the
+//                             attention backward): stored as loaded (coalesced, conflict-free 8-B
+//                             writes) and read k-contiguous with the gfx950 transpose read
+//                             ds_read_b64_tr_b16; the +32 pad puts the 4 k-rows of a read in 4
+//                             distinct 16-bank windows.
+// Workgroup -> tile mapping is XCD-aware: consecutive tiles (which share operand panels) are dealt to
+// the same XCD so they hit the same L2.
 #include "common.h"
 #include <algorithm>
 
@@ -41,44 +50,91 @@ struct GemmArgs {
 };
 
 constexpr int BK = 32;
-constexpr int PITCH = 40;  // bf16 elements per LDS row
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+
+template <int ROWS, bool COL>
+struct Img {
+  static constexpr int PITCH = COL ? ROWS + 32 : 40;
+  static constexpr int PLANE = COL ? BK * PITCH : ROWS * PITCH;
+  static constexpr int SIZE = 2 * PLANE;
+};
 
 __device__ __forceinline__ void split4(const float4& v, bf16x4& hi, bf16x4& lo) {
-  __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y, h2 = (__bf16)v.z, h3 = (__bf16)v.w;
+  const __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y, h2 = (__bf16)v.z, h3 = (__bf16)v.w;
   hi = bf16x4{h0, h1, h2, h3};
   lo = bf16x4{(__bf16)(v.x - (float)h0), (__bf16)(v.y - (float)h1), (__bf16)(v.z - (float)h2),
               (__bf16)(v.w - (float)h3)};
 }
 
-__device__ __forceinline__ void st_split(__bf16* hi_plane, __bf16* lo_plane, int off, const float4& v) {
+__device__ __forceinline__ void st_split(__bf16* img, int plane, int off, const float4& v) {
   bf16x4 h, l;
   split4(v, h, l);
-  *(bf16x4*)(hi_plane + off) = h;
-  *(bf16x4*)(lo_plane + off) = l;
+  *(bf16x4*)(img + off) = h;
+  *(bf16x4*)(img + plane + off) = l;
+}
+
+// fragment of a 32x32x16 MFMA operand: lane l holds element [row0 + (l&31)][ks*16 + 8*(l>>5) + j]
+template <int ROWS, bool COL>
+__device__ __forceinline__ bf16x8 read_frag(const __bf16* plane, int row0, int ks, int lane) {
+  if constexpr (!COL) {
+    return *(const bf16x8*)(plane + (row0 + (lane & 31)) * 40 + ks * 16 + (lane >> 5) * 8);
+  } else {
+    constexpr int P = Img<ROWS, true>::PITCH;
+    const int g = lane >> 4, li = lane & 15;
+    const __bf16* p = plane + (ks * 16 + (g >> 1) * 8 + (li >> 2)) * P + row0 + (g & 1) * 16 + 4 * (li & 3);
+    const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)p);
+    const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(p + 4 * P));
+    return __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
+// Gather-position helper: source pixel of output pixel (oh,ow) for filter tap (r,s).
+__device__ __forceinline__ bool tap_src(const GemmArgs& a, int oh, int ow, int r, int s, int& ih, int& iw) {
+  if (a.conv_mode == CONV_FWD) {
+    ih = oh * a.stride - a.pad_t + r;
+    iw = ow * a.stride - a.pad_l + s;
+    return ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+  } else if (a.conv_mode == CONV_UPS) {  // nearest x2 upsample, then conv (stride 1)
+    const int uh = oh - a.pad_t + r, uw = ow - a.pad_l + s;
+    ih = uh >> 1;
+    iw = uw >> 1;
+    return uh >= 0 && uh < 2 * a.H && uw >= 0 && uw < 2 * a.W;
+  } else {  // transposed gather (dgrad of a strided conv)
+    const int nh = oh + a.pad_t - r, nw = ow + a.pad_l - s;
+    if (nh < 0 || nw < 0) return false;
+    if (a.stride == 1) {
+      ih = nh; iw = nw;
+    } else {
+      if ((nh % a.stride) | (nw % a.stride)) return false;
+      ih = nh / a.stride; iw = nw / a.stride;
+    }
+    return ih < a.H && iw < a.W;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
-// operand loaders. Each stages a ROWS x 32 tile of the logical operand (rows = M or N, k
-// contiguous in LDS). Interface: init(args, row0, k_begin, tid), load() (tile at the current k),
-// advance() (k += 32), store(hi_plane, lo_plane).
+// operand loaders: init(args, base, row0, k_begin, tid); load(args) (the tile at the current k);
+// advance(args) (k += 32); store(img) into the operand's LDS image.
 // ------------------------------------------------------------------------------------------
 
-// K-contiguous rows: element (row, k) at P[row*ld + k].
-template <int ROWS, int VEC>
+// ROW image, source element (row, k) at P[row*ld + k]
+template <int ROWS, int VEC, int NT, bool IS_A>
 struct LoadRowK {
-  static constexpr int NR = ROWS / 32;
+  static constexpr int RP = NT / 8;     // rows per pass (8 float4 per 32-wide row)
+  static constexpr int NR = ROWS / RP;  // rows per thread
   const float* P;
   long long ld;
   int rows, K, row0, k, kc, r0;
   float4 v[NR];
-  __device__ void init(const float* p, long long ld_, int rows_, int K_, int row0_, int kb, int tid) {
-    P = p; ld = ld_; rows = rows_; K = K_; row0 = row0_; k = kb; kc = tid & 7; r0 = tid >> 3;
+  __device__ void init(const GemmArgs& a, const float* p, int row0_, int kb, int tid) {
+    P = p; ld = IS_A ? a.lda : a.ldb; rows = IS_A ? a.M : a.N; K = a.K;
+    row0 = row0_; k = kb; kc = tid & 7; r0 = tid >> 3;
   }
-  __device__ void load() {
+  __device__ void load(const GemmArgs&) {
     const int kk = k + kc * 4;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
-      const int row = row0 + r0 + 32 * i;
+      const int row = row0 + r0 + RP * i;
       const float* src = P + (long long)row * ld + kk;
       if (VEC == 4) {
         v[i] = (row < rows && kk < K) ? *(const float4*)src : float4{0.f, 0.f, 0.f, 0.f};
@@ -91,99 +147,31 @@ struct LoadRowK {
       }
     }
   }
-  __device__ void advance() { k += BK; }
-  __device__ void store(__bf16* hi, __bf16* lo) {
+  __device__ void advance(const GemmArgs&) { k += BK; }
+  __device__ void store(__bf16* img) {
 #pragma unroll
-    for (int i = 0; i < NR; ++i) st_split(hi, lo, (r0 + 32 * i) * PITCH + kc * 4, v[i]);
+    for (int i = 0; i < NR; ++i) st_split(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
   }
 };
 
-// Row-dim contiguous: element (row, k) at P[k*ld + row]. Each thread loads a 4(k) x 4(row) block
-// and transposes it into the k-contiguous LDS image.
-template <int ROWS, int VEC>
-struct LoadColK {
-  static constexpr int NC4 = ROWS / 4;       // 4-wide column groups
-  static constexpr int NT = NC4 * (BK / 4);  // active threads
-  const float* P;
-  long long ld;
-  int rows, K, row0, k, c4, k4;
-  bool active;
-  float4 v[4];
-  __device__ void init(const float* p, long long ld_, int rows_, int K_, int row0_, int kb, int tid) {
-    P = p; ld = ld_; rows = rows_; K = K_; row0 = row0_; k = kb;
-    active = tid < NT; c4 = tid % NC4; k4 = tid / NC4;
-  }
-  __device__ void load() {
-    const int col = row0 + c4 * 4;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int kr = k + k4 * 4 + kk;
-      const float* src = P + (long long)kr * ld + col;
-      const bool kv = active && kr < K;
-      if (VEC == 4) {
-        v[kk] = (kv && col < rows) ? *(const float4*)src : float4{0.f, 0.f, 0.f, 0.f};
-      } else {
-        v[kk].x = (kv && col + 0 < rows) ? src[0] : 0.f;
-        v[kk].y = (kv && col + 1 < rows) ? src[1] : 0.f;
-        v[kk].z = (kv && col + 2 < rows) ? src[2] : 0.f;
-        v[kk].w = (kv && col + 3 < rows) ? src[3] : 0.f;
-      }
-    }
-  }
-  __device__ void advance() { k += BK; }
-  __device__ void store(__bf16* hi, __bf16* lo) {
-    if (!active) return;
-    const int base = (c4 * 4) * PITCH + k4 * 4;
-    st_split(hi, lo, base + 0 * PITCH, float4{v[0].x, v[1].x, v[2].x, v[3].x});
-    st_split(hi, lo, base + 1 * PITCH, float4{v[0].y, v[1].y, v[2].y, v[3].y});
-    st_split(hi, lo, base + 2 * PITCH, float4{v[0].z, v[1].z, v[2].z, v[3].z});
-    st_split(hi, lo, base + 3 * PITCH, float4{v[0].w, v[1].w, v[2].w, v[3].w});
-  }
-};
-
-// Gather-position helper: source pixel of output pixel (oh,ow) for filter tap (r,s).
-struct TapPos {
-  __device__ static __forceinline__ bool src(const GemmArgs& a, int oh, int ow, int r, int s,
-                                             int& ih, int& iw) {
-    if (a.conv_mode == CONV_FWD) {
-      ih = oh * a.stride - a.pad_t + r;
-      iw = ow * a.stride - a.pad_l + s;
-      return ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-    } else if (a.conv_mode == CONV_UPS) {  // nearest x2 upsample, then conv (stride 1)
-      const int uh = oh - a.pad_t + r, uw = ow - a.pad_l + s;
-      ih = uh >> 1;
-      iw = uw >> 1;
-      return uh >= 0 && uh < 2 * a.H && uw >= 0 && uw < 2 * a.W;
-    } else {  // transposed gather (dgrad of a strided conv)
-      const int nh = oh + a.pad_t - r, nw = ow + a.pad_l - s;
-      if (nh < 0 || nw < 0) return false;
-      if (a.stride == 1) {
-        ih = nh; iw = nw;
-      } else {
-        if ((nh % a.stride) | (nw % a.stride)) return false;
-        ih = nh / a.stride; iw = nw / a.stride;
-      }
-      return ih < a.H && iw < a.W;
-    }
-  }
-};
-
-// Implicit im2col of an NHWC tensor: element (pixel m, k = (r*S+s)*Cx + c).
-template <int ROWS, int VEC>
+// ROW image, implicit im2col of an NHWC tensor: element (pixel m, k = (r*S+s)*Cx + c)
+template <int ROWS, int VEC, int NT>
 struct LoadConvA {
-  static constexpr int NR = ROWS / 32;
+  static constexpr int RP = NT / 8;
+  static constexpr int NR = ROWS / RP;
   const float* X;
   int kc, r0, k;
   int cc[4], rr[4], ss[4];  // (c, r, s) of element kc*4+e of the current k-tile
   long long base[NR];
   int oh[NR], ow[NR];
   bool mv[NR];
+  float4 v[NR];
   __device__ void init(const GemmArgs& a, const float* x, int row0, int kb, int tid) {
     X = x; kc = tid & 7; r0 = tid >> 3; k = kb;
     const int hw = a.Ho * a.Wo;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
-      const int m = row0 + r0 + 32 * i;
+      const int m = row0 + r0 + RP * i;
       mv[i] = m < a.M;
       const int mm = mv[i] ? m : 0;
       const int b = mm / hw;
@@ -212,13 +200,12 @@ struct LoadConvA {
       }
     }
   }
-  float4 v[NR];
   __device__ void load(const GemmArgs& a) {
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       if (VEC == 4) {
         int ih, iw;
-        const bool ok = mv[i] && (k + kc * 4 < a.K) && TapPos::src(a, oh[i], ow[i], rr[0], ss[0], ih, iw);
+        const bool ok = mv[i] && (k + kc * 4 < a.K) && tap_src(a, oh[i], ow[i], rr[0], ss[0], ih, iw);
         v[i] = ok ? *(const float4*)(X + base[i] + ((long long)ih * a.W + iw) * a.Cx + cc[0])
                   : float4{0.f, 0.f, 0.f, 0.f};
       } else {
@@ -226,167 +213,188 @@ struct LoadConvA {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           int ih, iw;
-          const bool ok = mv[i] && (k + kc * 4 + e < a.K) && TapPos::src(a, oh[i], ow[i], rr[e], ss[e], ih, iw);
+          const bool ok = mv[i] && (k + kc * 4 + e < a.K) && tap_src(a, oh[i], ow[i], rr[e], ss[e], ih, iw);
           t[e] = ok ? X[base[i] + ((long long)ih * a.W + iw) * a.Cx + cc[e]] : 0.f;
         }
         v[i] = float4{t[0], t[1], t[2], t[3]};
       }
     }
   }
-  __device__ void store(__bf16* hi, __bf16* lo) {
+  __device__ void store(__bf16* img) {
 #pragma unroll
-    for (int i = 0; i < NR; ++i) st_split(hi, lo, (r0 + 32 * i) * PITCH + kc * 4, v[i]);
+    for (int i = 0; i < NR; ++i) st_split(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
   }
 };
 
-// wgrad B operand: rows n' = (r*S+s)*Cx + c (filter element), k = output pixel m.
-// element = X[b][src(oh,ow,r,s)][c]; contiguous along c. 4(k) x 4(n') block per thread.
-template <int ROWS, int VEC>
-struct LoadWgradX {
-  static constexpr int NC4 = ROWS / 4;
-  static constexpr int NT = NC4 * (BK / 4);
-  const float* X;
-  bool active;
-  int c4, k4, k;
-  int cc[4], rr[4], ss[4];
-  bool nv[4];
-  int pb, poh, pow_;  // decomposition of pixel k + k4*4
-  float4 v[4];
-  __device__ void init(const GemmArgs& a, const float* x, int row0, int kb, int tid) {
-    X = x; k = kb;
-    active = tid < NT; c4 = tid % NC4; k4 = tid / NC4;
-    const int nE = VEC == 4 ? 1 : 4;
-    const int Nn = a.N;
-    for (int e = 0; e < 4; ++e) {
-      const int n = row0 + c4 * 4 + e;
-      nv[e] = n < Nn;
-      if (e < nE || VEC == 1) {
-        const int nn = nv[e] ? n : 0;
-        const int tap = nn / a.Cx;
-        cc[e] = nn - tap * a.Cx;
-        rr[e] = tap / a.S;
-        ss[e] = tap - rr[e] * a.S;
+// COL image, source element (row, k) at P[k*ld + row] (rows contiguous)
+template <int ROWS, int VEC, int NT, bool IS_A>
+struct LoadColK {
+  static constexpr int C4 = ROWS / 4;           // float4 per k-row
+  static constexpr int NF = (BK * C4 + NT - 1) / NT;  // float4 per thread
+  const float* P;
+  long long ld;
+  int rows, K, row0, k, c4, kr;
+  float4 v[NF];
+  __device__ void init(const GemmArgs& a, const float* p, int row0_, int kb, int tid) {
+    P = p; ld = IS_A ? a.lda : a.ldb; rows = IS_A ? a.M : a.N; K = a.K;
+    row0 = row0_; k = kb; c4 = tid % C4; kr = tid / C4;
+  }
+  __device__ void load(const GemmArgs&) {
+    const int col = row0 + c4 * 4;
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int krow = kr + i * (NT / C4);
+      const int kk = k + krow;
+      const bool kv = krow < BK && kk < K;
+      const float* src = P + (long long)kk * ld + col;
+      if (VEC == 4) {
+        v[i] = (kv && col < rows) ? *(const float4*)src : float4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        v[i].x = (kv && col + 0 < rows) ? src[0] : 0.f;
+        v[i].y = (kv && col + 1 < rows) ? src[1] : 0.f;
+        v[i].z = (kv && col + 2 < rows) ? src[2] : 0.f;
+        v[i].w = (kv && col + 3 < rows) ? src[3] : 0.f;
       }
     }
-    const int p = kb + k4 * 4;
+  }
+  __device__ void advance(const GemmArgs&) { k += BK; }
+  __device__ void store(__bf16* img) {
+    constexpr int P_ = Img<ROWS, true>::PITCH;
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int krow = kr + i * (NT / C4);
+      if (krow < BK) st_split(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+    }
+  }
+};
+
+// COL image for the wgrad B operand: rows n' = (r*S+s)*Cx + c (filter element), k = output pixel.
+// element = X[b][src(oh,ow,r,s)][c], contiguous along c.
+template <int ROWS, int VEC, int NT>
+struct LoadWgradX {
+  static constexpr int C4 = ROWS / 4;
+  static constexpr int NF = (BK * C4 + NT - 1) / NT;
+  const float* X;
+  int c4, kr, k;
+  int cc[4], rr[4], ss[4];
+  bool nv[4];
+  int pb[NF], poh[NF], pow_[NF];  // pixel decomposition of this thread's k-rows
+  float4 v[NF];
+  __device__ void init(const GemmArgs& a, const float* x, int row0, int kb, int tid) {
+    X = x; k = kb; c4 = tid % C4; kr = tid / C4;
+    for (int e = 0; e < 4; ++e) {
+      const int n = row0 + c4 * 4 + e;
+      nv[e] = n < a.N;
+      const int nn = nv[e] ? n : 0;
+      const int tap = nn / a.Cx;
+      cc[e] = nn - tap * a.Cx;
+      rr[e] = tap / a.S;
+      ss[e] = tap - rr[e] * a.S;
+    }
     const int hw = a.Ho * a.Wo;
-    pb = p / hw;
-    const int rem = p - pb * hw;
-    poh = rem / a.Wo;
-    pow_ = rem - poh * a.Wo;
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int p = kb + kr + i * (NT / C4);
+      pb[i] = p / hw;
+      const int rem = p - pb[i] * hw;
+      poh[i] = rem / a.Wo;
+      pow_[i] = rem - poh[i] * a.Wo;
+    }
   }
   __device__ void advance(const GemmArgs& a) {
     k += BK;
-    pow_ += BK;
-    while (pow_ >= a.Wo) {
-      pow_ -= a.Wo;
-      if (++poh == a.Ho) { poh = 0; ++pb; }
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      pow_[i] += BK;
+      while (pow_[i] >= a.Wo) {
+        pow_[i] -= a.Wo;
+        if (++poh[i] == a.Ho) { poh[i] = 0; ++pb[i]; }
+      }
     }
   }
   __device__ void load(const GemmArgs& a) {
-    int b = pb, oh = poh, ow = pow_;
     const long long img = (long long)a.H * a.W * a.Cx;
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const bool kv = active && (k + k4 * 4 + kk < a.K);
+    for (int i = 0; i < NF; ++i) {
+      const int krow = kr + i * (NT / C4);
+      const bool kv = krow < BK && (k + krow < a.K);
       if (VEC == 4) {
         int ih, iw;
-        const bool ok = kv && nv[0] && TapPos::src(a, oh, ow, rr[0], ss[0], ih, iw);
-        v[kk] = ok ? *(const float4*)(X + b * img + ((long long)ih * a.W + iw) * a.Cx + cc[0])
-                   : float4{0.f, 0.f, 0.f, 0.f};
+        const bool ok = kv && nv[0] && tap_src(a, poh[i], pow_[i], rr[0], ss[0], ih, iw);
+        v[i] = ok ? *(const float4*)(X + pb[i] * img + ((long long)ih * a.W + iw) * a.Cx + cc[0])
+                  : float4{0.f, 0.f, 0.f, 0.f};
       } else {
         float t[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           int ih, iw;
-          const bool ok = kv && nv[e] && TapPos::src(a, oh, ow, rr[e], ss[e], ih, iw);
-          t[e] = ok ? X[b * img + ((long long)ih * a.W + iw) * a.Cx + cc[e]] : 0.f;
+          const bool ok = kv && nv[e] && tap_src(a, poh[i], pow_[i], rr[e], ss[e], ih, iw);
+          t[e] = ok ? X[pb[i] * img + ((long long)ih * a.W + iw) * a.Cx + cc[e]] : 0.f;
         }
-        v[kk] = float4{t[0], t[1], t[2], t[3]};
+        v[i] = float4{t[0], t[1], t[2], t[3]};
       }
-      if (++ow == a.Wo) { ow = 0; if (++oh == a.Ho) { oh = 0; ++b; } }
     }
   }
-  __device__ void store(__bf16* hi, __bf16* lo) {
-    if (!active) return;
-    const int base = (c4 * 4) * PITCH + k4 * 4;
-    st_split(hi, lo, base + 0 * PITCH, float4{v[0].x, v[1].x, v[2].x, v[3].x});
-    st_split(hi, lo, base + 1 * PITCH, float4{v[0].y, v[1].y, v[2].y, v[3].y});
-    st_split(hi, lo, base + 2 * PITCH, float4{v[0].z, v[1].z, v[2].z, v[3].z});
-    st_split(hi, lo, base + 3 * PITCH, float4{v[0].w, v[1].w, v[2].w, v[3].w});
+  __device__ void store(__bf16* img) {
+    constexpr int P_ = Img<ROWS, true>::PITCH;
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int krow = kr + i * (NT / C4);
+      if (krow < BK) st_split(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+    }
   }
 };
 
-// Uniform wrappers so the kernel body can treat all loaders alike.
-template <int KIND, int ROWS, int VEC, bool IS_A>
-struct Operand;
+template <int KIND, int ROWS, int VEC, int NT, bool IS_A>
+struct Loader;
+template <int ROWS, int VEC, int NT, bool IS_A>
+struct Loader<0, ROWS, VEC, NT, IS_A> : LoadRowK<ROWS, VEC, NT, IS_A> { static constexpr bool COL = false; };
+template <int ROWS, int VEC, int NT, bool IS_A>
+struct Loader<1, ROWS, VEC, NT, IS_A> : LoadColK<ROWS, VEC, NT, IS_A> { static constexpr bool COL = true; };
+template <int ROWS, int VEC, int NT>
+struct Loader<2, ROWS, VEC, NT, true> : LoadConvA<ROWS, VEC, NT> { static constexpr bool COL = false; };
+template <int ROWS, int VEC, int NT>
+struct Loader<2, ROWS, VEC, NT, false> : LoadWgradX<ROWS, VEC, NT> { static constexpr bool COL = true; };
 
-template <int ROWS, int VEC, bool IS_A>
-struct Operand<0, ROWS, VEC, IS_A> {  // row-k
-  LoadRowK<ROWS, VEC> L;
-  __device__ void init(const GemmArgs& a, const float* p, int row0, int kb, int tid) {
-    L.init(p, IS_A ? a.lda : a.ldb, IS_A ? a.M : a.N, a.K, row0, kb, tid);
-  }
-  __device__ void load(const GemmArgs&) { L.load(); }
-  __device__ void advance(const GemmArgs&) { L.advance(); }
-  __device__ void store(__bf16* h, __bf16* l) { L.store(h, l); }
-};
-template <int ROWS, int VEC, bool IS_A>
-struct Operand<1, ROWS, VEC, IS_A> {  // col
-  LoadColK<ROWS, VEC> L;
-  __device__ void init(const GemmArgs& a, const float* p, int row0, int kb, int tid) {
-    L.init(p, IS_A ? a.lda : a.ldb, IS_A ? a.M : a.N, a.K, row0, kb, tid);
-  }
-  __device__ void load(const GemmArgs&) { L.load(); }
-  __device__ void advance(const GemmArgs&) { L.advance(); }
-  __device__ void store(__bf16* h, __bf16* l) { L.store(h, l); }
-};
-template <int ROWS, int VEC>
-struct Operand<2, ROWS, VEC, true> {  // conv gather (A)
-  LoadConvA<ROWS, VEC> L;
-  __device__ void init(const GemmArgs& a, const float* p, int row0, int kb, int tid) { L.init(a, p, row0, kb, tid); }
-  __device__ void load(const GemmArgs& a) { L.load(a); }
-  __device__ void advance(const GemmArgs& a) { L.advance(a); }
-  __device__ void store(__bf16* h, __bf16* l) { L.store(h, l); }
-};
-template <int ROWS, int VEC>
-struct Operand<2, ROWS, VEC, false> {  // wgrad gather (B)
-  LoadWgradX<ROWS, VEC> L;
-  __device__ void init(const GemmArgs& a, const float* p, int row0, int kb, int tid) { L.init(a, p, row0, kb, tid); }
-  __device__ void load(const GemmArgs& a) { L.load(a); }
-  __device__ void advance(const GemmArgs& a) { L.advance(a); }
-  __device__ void store(__bf16* h, __bf16* l) { L.store(h, l); }
-};
-
-template <int BM, int BN, int AK, int VA, int BKIND, int VB>
-__global__ void __launch_bounds__(256) gemm3x_kernel(GemmArgs a) {
-  constexpr int A_PL = BM * PITCH, B_PL = BN * PITCH;
-  constexpr int BUF = 2 * A_PL + 2 * B_PL;
-  constexpr int WM = BM / 64, WN = BN / 64;  // 32x32 MFMA tiles per wave (2x2 waves)
+template <int BM, int BN, int WGM, int WGN, int AK, int VA, int BKIND, int VB>
+__global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
+  constexpr int NT = 64 * WGM * WGN;
+  using LA = Loader<AK, BM, VA, NT, true>;
+  using LB = Loader<BKIND, BN, VB, NT, false>;
+  using IA = Img<BM, LA::COL>;
+  using IB = Img<BN, LB::COL>;
+  constexpr int BUF = IA::SIZE + IB::SIZE;
+  constexpr int TM = BM / WGM / 32, TN = BN / WGN / 32;  // 32x32 MFMA tiles per wave
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int tile = blockIdx.x;
+  const int wm = wid / WGN, wn = wid - wm * WGN;
+  // XCD-aware remap (bijective): blocks b and b+8 share an XCD, so hand each XCD a contiguous run
+  // of tiles (row-major over (m, n): neighbours share A rows and the same weight panel).
+  const int nwg = a.tiles_m * a.tiles_n;
+  const int orig = blockIdx.x;
+  int tile = orig;
+  if (nwg >= 16) {
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  }
   const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int z = blockIdx.z;
   const int bidx = z / a.splits, split = z - bidx * a.splits;
   const int kb = split * a.k_split;
   const int ke = min(a.K, kb + a.k_split);
-  const float* Ap = a.A + bidx * a.sA;
-  const float* Bp = a.B + bidx * a.sB;
 
-  Operand<AK, BM, VA, true> la;
-  Operand<BKIND, BN, VB, false> lb;
-  la.init(a, Ap, m0, kb, tid);
-  lb.init(a, Bp, n0, kb, tid);
+  LA la;
+  LB lb;
+  la.init(a, a.A + bidx * a.sA, m0, kb, tid);
+  lb.init(a, a.B + bidx * a.sB, n0, kb, tid);
 
-  f32x16 acc[WM][WN];
+  f32x16 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < WM; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < WN; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -394,10 +402,11 @@ __global__ void __launch_bounds__(256) gemm3x_kernel(GemmArgs a) {
   if (nt > 0) {
     la.load(a);
     lb.load(a);
-    la.store(lds, lds + A_PL);
-    lb.store(lds + 2 * A_PL, lds + 2 * A_PL + B_PL);
+    la.store(lds);
+    lb.store(lds + IA::SIZE);
   }
   __syncthreads();
+  const int arow = wm * (BM / WGM), brow = wn * (BN / WGN);
   for (int t = 0; t < nt; ++t) {
     const int cur = t & 1;
     if (t + 1 < nt) {
@@ -406,39 +415,32 @@ __global__ void __launch_bounds__(256) gemm3x_kernel(GemmArgs a) {
       la.load(a);
       lb.load(a);
     }
-    const __bf16* Ahi = lds + cur * BUF;
-    const __bf16* Alo = Ahi + A_PL;
-    const __bf16* Bhi = Ahi + 2 * A_PL;
-    const __bf16* Blo = Bhi + B_PL;
+    const __bf16* Ai = lds + cur * BUF;
+    const __bf16* Bi = Ai + IA::SIZE;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 ah[WM], al[WM], bh[WN], bl[WN];
-      const int koff = ks * 16 + (lane >> 5) * 8;
+      bf16x8 bh[TN], bl[TN];
 #pragma unroll
-      for (int i = 0; i < WM; ++i) {
-        const int off = (wm * (BM / 2) + i * 32 + (lane & 31)) * PITCH + koff;
-        ah[i] = *(const bf16x8*)(Ahi + off);
-        al[i] = *(const bf16x8*)(Alo + off);
+      for (int j = 0; j < TN; ++j) {
+        bh[j] = read_frag<BN, LB::COL>(Bi, brow + j * 32, ks, lane);
+        bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, ks, lane);
       }
 #pragma unroll
-      for (int j = 0; j < WN; ++j) {
-        const int off = (wn * (BN / 2) + j * 32 + (lane & 31)) * PITCH + koff;
-        bh[j] = *(const bf16x8*)(Bhi + off);
-        bl[j] = *(const bf16x8*)(Blo + off);
-      }
+      for (int i = 0; i < TM; ++i) {
+        const bf16x8 ah = read_frag<BM, LA::COL>(Ai, arow + i * 32, ks, lane);
+        const bf16x8 al = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow + i * 32, ks, lane);
 #pragma unroll
-      for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int j = 0; j < WN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
         }
+      }
     }
     if (t + 1 < nt) {
       __bf16* nb = lds + (cur ^ 1) * BUF;
-      la.store(nb, nb + A_PL);
-      lb.store(nb + 2 * A_PL, nb + 2 * A_PL + B_PL);
+      la.store(nb);
+      lb.store(nb + IA::SIZE);
     }
     __syncthreads();
   }
@@ -449,15 +451,15 @@ __global__ void __launch_bounds__(256) gemm3x_kernel(GemmArgs a) {
   const float* Rp = a.res ? a.res + bidx * a.sR : nullptr;
   float* Wp = partial ? a.ws + ((long long)bidx * a.splits + split) * a.M * a.N : nullptr;
 #pragma unroll
-  for (int j = 0; j < WN; ++j) {
-    const int col = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + brow + j * 32 + (lane & 31);
     if (col >= a.N) continue;
     const float bv = (!partial && a.bias) ? a.bias[col] : 0.f;
 #pragma unroll
-    for (int i = 0; i < WM; ++i) {
+    for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int row = m0 + arow + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (row >= a.M) continue;
         if (partial) {
           Wp[(long long)row * a.N + col] = acc[i][j][r];
@@ -496,33 +498,69 @@ __global__ void splitk_reduce_kernel(GemmArgs a) {
 // ------------------------------------------------------------------------------------------
 // host-side dispatch
 // ------------------------------------------------------------------------------------------
-template <int BM, int BN, int AK, int VA, int BKIND, int VB>
-static void launch_t(GemmArgs& a, hipStream_t st) {
+enum { T256x256 = 0, T256x128 = 1, T128x256 = 2, T128x128 = 3, T64x64 = 4 };
+static const int TILE_M[] = {256, 256, 128, 128, 64};
+static const int TILE_N[] = {256, 128, 256, 128, 64};
+
+static long long tiles_of(int cfg, const GemmArgs& a) {
+  return (long long)cdiv(a.M, TILE_M[cfg]) * cdiv(a.N, TILE_N[cfg]) * a.batch;
+}
+
+// pick the largest tile that still gives >= 1 full wave of the 256 CUs (wgrad adds split-K)
+static int choose_tile(const GemmArgs& a, bool allow_big) {
+  if (allow_big) {
+    if (tiles_of(T256x256, a) >= 240 && a.M > 128 && a.N > 128) return T256x256;
+    if (a.N <= 128 && tiles_of(T256x128, a) >= 240 && a.M > 128) return T256x128;
+    if (a.M <= 128 && tiles_of(T128x256, a) >= 240 && a.N > 128) return T128x256;
+  }
+  if (tiles_of(T128x128, a) >= 200 && a.M > 64 && a.N > 64) return T128x128;
+  return T64x64;
+}
+
+template <int CFG, int AK, int VA, int BKIND, int VB>
+static void launch_cfg(GemmArgs& a, hipStream_t st) {
+  constexpr int BM = CFG == T256x256 || CFG == T256x128 ? 256 : CFG == T64x64 ? 64 : 128;
+  constexpr int BN = CFG == T256x256 || CFG == T128x256 ? 256 : CFG == T64x64 ? 64 : 128;
+  constexpr int WGM = CFG == T256x128 ? 4 : 2;
+  constexpr int WGN = (CFG == T256x256 || CFG == T128x256) ? 4 : 2;
   a.tiles_m = cdiv(a.M, BM);
   a.tiles_n = cdiv(a.N, BN);
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splits);
-  hipLaunchKernelGGL((gemm3x_kernel<BM, BN, AK, VA, BKIND, VB>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB>), grid, dim3(64 * WGM * WGN), 0, st, a);
 }
 
 template <int AK, int VA, int BKIND, int VB>
-static void launch_sz(GemmArgs& a, hipStream_t st) {
-  // 128x128 tiles when the problem fills the chip, otherwise 64x64 (more blocks)
-  const long long t128 = (long long)cdiv(a.M, 128) * cdiv(a.N, 128) * a.batch * a.splits;
-  if (t128 >= 512 || (a.M >= 128 && a.N >= 128 && t128 >= 256))
-    launch_t<128, 128, AK, VA, BKIND, VB>(a, st);
-  else
-    launch_t<64, 64, AK, VA, BKIND, VB>(a, st);
+static void launch_big(GemmArgs& a, hipStream_t st, int cfg) {
+  switch (cfg) {
+    case T256x256: launch_cfg<T256x256, AK, VA, BKIND, VB>(a, st); break;
+    case T256x128: launch_cfg<T256x128, AK, VA, BKIND, VB>(a, st); break;
+    case T128x256: launch_cfg<T128x256, AK, VA, BKIND, VB>(a, st); break;
+    case T128x128: launch_cfg<T128x128, AK, VA, BKIND, VB>(a, st); break;
+    default: launch_cfg<T64x64, AK, VA, BKIND, VB>(a, st); break;
+  }
+}
+
+template <int AK, int VA, int BKIND, int VB>
+static void launch_small(GemmArgs& a, hipStream_t st, int cfg) {
+  if (cfg == T128x128) launch_cfg<T128x128, AK, VA, BKIND, VB>(a, st);
+  else launch_cfg<T64x64, AK, VA, BKIND, VB>(a, st);
 }
 
 static size_t splitk_ws_bytes(const GemmArgs& a) {
   return a.splits > 1 ? (size_t)a.batch * a.splits * a.M * a.N * sizeof(float) : 0;
 }
 
-// choose split-K so that a small-MN / huge-K product (wgrad) still fills 256 CUs
-static int choose_splits(int M, int N, int K, int batch) {
-  const long long tiles = (long long)cdiv(M, 128) * cdiv(N, 128) * batch;
+static void set_splits(GemmArgs& a, int splits) {
+  a.splits = std::max(1, splits);
+  a.k_split = ((cdiv(a.K, a.splits) + BK - 1) / BK) * BK;
+  a.splits = std::max(1, cdiv(a.K, a.k_split));
+}
+
+// split K so that a small-MN / huge-K product (wgrad) still fills the chip; >= 16 K-tiles per split
+static int choose_splits(const GemmArgs& a, int cfg) {
+  const long long tiles = tiles_of(cfg, a);
   int s = 1;
-  while (tiles * s < 512 && (long long)K / (s * 2) >= 512 && s < 64) s *= 2;
+  while (tiles * s < 400 && (long long)a.K / (s * 2) >= 512 && s < 64) s *= 2;
   return s;
 }
 
@@ -535,11 +573,10 @@ static int finish(GemmArgs& a, hipStream_t st) {
   return launch_status();
 }
 
-static void set_splits(GemmArgs& a, int splits) {
-  a.splits = splits;
-  a.k_split = ((cdiv(a.K, splits) + BK - 1) / BK) * BK;
-  a.splits = cdiv(a.K, a.k_split);
-  if (a.splits < 1) a.splits = 1;
+static void plan_splits(GemmArgs& a, int cfg, float* ws, size_t ws_bytes) {
+  set_splits(a, ws ? choose_splits(a, cfg) : 1);
+  while (a.splits > 1 && splitk_ws_bytes(a) > ws_bytes) set_splits(a, a.splits / 2);
+  a.ws = ws;
 }
 
 }  // namespace mvae
@@ -568,19 +605,18 @@ int mvae_gemm_strided_batched(int trans_a, int trans_b, int m, int n, int k, flo
   a.C = C; a.ldc = ldc; a.sC = stride_c;
   a.bias = bias; a.res = residual; a.ldr = ldr; a.sR = stride_r;
   a.alpha = alpha; a.beta = beta;
-  set_splits(a, workspace ? choose_splits(m, n, k, batch) : 1);
-  while (a.splits > 1 && splitk_ws_bytes(a) > workspace_bytes) set_splits(a, a.splits / 2);
-  a.ws = workspace;
   hipStream_t st = (hipStream_t)stream;
   const bool va = (trans_a ? (m % 4 == 0) : (k % 4 == 0)) && (lda % 4 == 0) && (stride_a % 4 == 0) && al16(A);
   const bool vb = (trans_b ? (k % 4 == 0) : (n % 4 == 0)) && (ldb % 4 == 0) && (stride_b % 4 == 0) && al16(B);
+  const int cfg = choose_tile(a, va && vb);
+  plan_splits(a, cfg, workspace, workspace_bytes);
   const int ak = trans_a ? A_COLM : A_ROWK;
   const int bk = trans_b ? B_ROWK : B_COLN;
 #define MVAE_G(AKk, BKk)                                                        \
-  if (va && vb) launch_sz<AKk, 4, BKk, 4>(a, st);                              \
-  else if (va) launch_sz<AKk, 4, BKk, 1>(a, st);                               \
-  else if (vb) launch_sz<AKk, 1, BKk, 4>(a, st);                               \
-  else launch_sz<AKk, 1, BKk, 1>(a, st);
+  if (va && vb) launch_big<AKk, 4, BKk, 4>(a, st, cfg);                        \
+  else if (va) launch_small<AKk, 4, BKk, 1>(a, st, cfg);                       \
+  else if (vb) launch_small<AKk, 1, BKk, 4>(a, st, cfg);                       \
+  else launch_small<AKk, 1, BKk, 1>(a, st, cfg);
   if (ak == A_ROWK && bk == B_ROWK) { MVAE_G(A_ROWK, B_ROWK) }
   else if (ak == A_ROWK && bk == B_COLN) { MVAE_G(A_ROWK, B_COLN) }
   else if (ak == A_COLM && bk == B_ROWK) { MVAE_G(A_COLM, B_ROWK) }
@@ -592,8 +628,10 @@ int mvae_gemm_strided_batched(int trans_a, int trans_b, int m, int n, int k, flo
 size_t mvae_gemm_workspace_bytes(int m, int n, int k, int batch) {
   GemmArgs a{};
   a.M = m; a.N = n; a.K = k; a.batch = batch;
-  set_splits(a, choose_splits(m, n, k, batch));
-  return splitk_ws_bytes(a);
+  set_splits(a, choose_splits(a, choose_tile(a, true)));
+  size_t b1 = splitk_ws_bytes(a);
+  set_splits(a, choose_splits(a, choose_tile(a, false)));
+  return std::max(b1, splitk_ws_bytes(a));
 }
 
 // Implicit-GEMM convolution over NHWC activations and KRSC ([Cout][R][S][Cin]) weights.
@@ -618,44 +656,50 @@ int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const fl
   a.stride = stride; a.pad_t = pad_t; a.pad_l = pad_l; a.conv_mode = mode;
   hipStream_t st = (hipStream_t)stream;
   const bool v = (cin % 4 == 0) && al16(x) && al16(w);
-  if (v) launch_sz<A_CONV, 4, B_ROWK, 4>(a, st);
-  else launch_sz<A_CONV, 1, B_ROWK, 1>(a, st);
+  const int cfg = choose_tile(a, v);
+  if (v) launch_big<A_CONV, 4, B_ROWK, 4>(a, st, cfg);
+  else launch_small<A_CONV, 1, B_ROWK, 1>(a, st, cfg);
   return finish(a, st);
 }
 
 // Weight gradient of mvae_conv2d_nhwc (modes 0 and 1):
 //   dw[cout][r][s][cin] = beta*dw + sum_pixels dy[pix][cout] * x[src(pix, r, s)][cin]
 // K = nb*ho*wo pixels, split deterministically across blocks (partials in `workspace`).
+static void wgrad_args(GemmArgs& a, int nb, int cin, int cout, int kh, int kw, int ho, int wo) {
+  a.M = cout; a.N = kh * kw * cin; a.K = nb * ho * wo; a.batch = 1;
+}
+
 int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float beta, int nb, int h,
                            int wd, int cin, int cout, int kh, int kw, int stride, int pad_t,
                            int pad_l, int ho, int wo, int mode, float* workspace,
                            size_t workspace_bytes, void* stream) {
   if (mode != 0 && mode != 1) { set_error("wgrad: mode must be 0 or 1"); return MVAE_EINVAL; }
   GemmArgs a{};
-  a.M = cout; a.N = kh * kw * cin; a.K = nb * ho * wo; a.batch = 1;
+  wgrad_args(a, nb, cin, cout, kh, kw, ho, wo);
   a.A = dy; a.lda = cout;
   a.B = x;
   a.C = dw; a.ldc = a.N; a.alpha = 1.f; a.beta = beta;
   a.H = h; a.W = wd; a.Cx = cin; a.Ho = ho; a.Wo = wo; a.R = kh; a.S = kw;
   a.stride = stride; a.pad_t = pad_t; a.pad_l = pad_l; a.conv_mode = mode;
-  set_splits(a, workspace ? choose_splits(a.M, a.N, a.K, 1) : 1);
-  while (a.splits > 1 && splitk_ws_bytes(a) > workspace_bytes) set_splits(a, a.splits / 2);
-  a.ws = workspace;
   hipStream_t st = (hipStream_t)stream;
   const bool va = (cout % 4 == 0) && al16(dy);
   const bool vb = (cin % 4 == 0) && al16(x);
-  if (va && vb) launch_sz<A_COLM, 4, B_WGRADX, 4>(a, st);
-  else if (va) launch_sz<A_COLM, 4, B_WGRADX, 1>(a, st);
-  else if (vb) launch_sz<A_COLM, 1, B_WGRADX, 4>(a, st);
-  else launch_sz<A_COLM, 1, B_WGRADX, 1>(a, st);
+  const int cfg = choose_tile(a, va && vb);
+  plan_splits(a, cfg, workspace, workspace_bytes);
+  if (va && vb) launch_big<A_COLM, 4, B_WGRADX, 4>(a, st, cfg);
+  else if (va) launch_small<A_COLM, 4, B_WGRADX, 1>(a, st, cfg);
+  else if (vb) launch_small<A_COLM, 1, B_WGRADX, 4>(a, st, cfg);
+  else launch_small<A_COLM, 1, B_WGRADX, 1>(a, st, cfg);
   return finish(a, st);
 }
 
 size_t mvae_conv2d_wgrad_workspace_bytes(int nb, int cin, int cout, int kh, int kw, int ho, int wo) {
   GemmArgs a{};
-  a.M = cout; a.N = kh * kw * cin; a.K = nb * ho * wo; a.batch = 1;
-  set_splits(a, choose_splits(a.M, a.N, a.K, 1));
-  return splitk_ws_bytes(a);
+  wgrad_args(a, nb, cin, cout, kh, kw, ho, wo);
+  set_splits(a, choose_splits(a, choose_tile(a, true)));
+  size_t b1 = splitk_ws_bytes(a);
+  set_splits(a, choose_splits(a, choose_tile(a, false)));
+  return std::max(b1, splitk_ws_bytes(a));
 }
 
 }  // extern "C"

@@ -82,29 +82,52 @@ def test_training_step_matches_reference(name):
     for k in FULL_GRADS[name]:
         g = mod.flat.params[names.index(k)]._mvae_main_grad.cpu()
         assert rel_err(g, data[f"grad.{k}"]) < TOL, k
-    mod.optimizer.step(used=mod._used_mask())
+    p_before = mod.flat.data.detach().clone().cpu()
+    g_before = mod.flat.grad.detach().clone().cpu()
+    used = mod._used_mask()
+    mod.optimizer.step(used=used)
     torch.cuda.synchronize()
     tn = float(mod.optimizer.last_total_norm)
     assert abs(tn - float(data["clip.total_norm"])) < TOL * float(data["clip.total_norm"])
-    # Post-step parameters. Adam's first step moves every element by ~lr*sign(g), so parameters
-    # whose reference gradient is pure rounding noise (e.g. a conv bias feeding a 1-channel-per-group
-    # GroupNorm, whose exact gradient is 0) take an arbitrary +-lr step on ANY platform; those are
-    # excluded (their gradient magnitude was already checked above).
-    total_sq = sum(float(data[f"gradsum.{k}"][1]) for k in has)
-    total_n = sum(mod.flat.params[names.index(k)].numel() for k in has)
-    glob_rms = (total_sq / total_n) ** 0.5
-    worst = 0.0
-    for k, p in zip(names, mod.flat.params):
-        if k in has and (float(data[f"gradsum.{k}"][1]) / p.numel()) ** 0.5 < 1e-4 * glob_rms:
+    # (a) the fused step equals torch.optim applied to OUR gradients (per-tensor non-finite zeroing,
+    #     global clip, Adam/AdamW, params without a gradient skipped)
+    used_l = used.tolist() if used is not None else [1] * len(names)
+    ref_params, ref_grads = [], []
+    for i, (k, p) in enumerate(zip(names, mod.flat.params)):
+        if not used_l[i]:
             continue
-        v = p.detach().double().cpu()
-        ref = float(data[f"stepsum.{k}"][1])
-        worst = max(worst, abs(float((v * v).sum()) - ref) / max(ref, 1e-30))
-        assert abs(float((v * v).sum()) - ref) <= 1e-4 * ref + 1e-12, k
-    report["step.sumsq_worst"] = worst
+        off, n = mod.flat.offsets[i], p.numel()
+        ref_params.append(p_before[off:off + n].clone().requires_grad_())
+        ref_grads.append(g_before[off:off + n].clone())
+    for rp, rg in zip(ref_params, ref_grads):
+        rp.grad = rg if torch.isfinite(rg).all() else torch.zeros_like(rg)
+    torch.nn.utils.clip_grad_norm_(ref_params, case["clip"])
+    oc = case["optimizer"]
+    O = torch.optim.AdamW if oc["type"] == "adamw" else torch.optim.Adam
+    O(ref_params, lr=oc["lr"], betas=tuple(oc["betas"]), weight_decay=oc["weight_decay"]).step()
+    after = mod.flat.data.detach().cpu()
+    j = 0
+    worst = 0.0
+    for i, (k, p) in enumerate(zip(names, mod.flat.params)):
+        off, n = mod.flat.offsets[i], p.numel()
+        if not used_l[i]:
+            assert torch.equal(after[off:off + n], p_before[off:off + n]), f"unused {k} changed"
+            continue
+        d = float((after[off:off + n] - ref_params[j].detach()).abs().max())
+        worst = max(worst, d)
+        assert d <= 1e-6 * float(ref_params[j].detach().abs().max()) + 1e-9, k
+        j += 1
+    report["step.vs_torch_optim_maxabs"] = worst
+    # (b) against the reference's own post-step values: Adam's first step moves each element by
+    #     ~lr*sign(g), so an element whose reference gradient is rounding noise (e.g. a conv bias in
+    #     front of a 1-channel-per-group GroupNorm: exact gradient 0) may step the other way on ANY
+    #     platform. Bound: |dp| <= 2*lr everywhere and < 0.01*lr for >= 98% of the elements.
+    lr = oc["lr"]
     for k in FULL_GRADS[name]:
         p = mod.flat.params[names.index(k)].detach().cpu()
-        assert rel_err(p, data[f"step.{k}"]) < TOL, k
+        d = (p - torch.from_numpy(data[f"step.{k}"])).abs()
+        assert float(d.max()) <= 2.0 * lr * 1.001 + 1e-7, k
+        assert float((d > 0.01 * lr).float().mean()) < 0.02, k
     out_dir = os.environ.get("MVAE_PARITY_REPORT")
     if out_dir:
         os.makedirs(out_dir, exist_ok=True)
