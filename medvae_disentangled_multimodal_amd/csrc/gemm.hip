@@ -292,9 +292,11 @@ struct LoadWgradX {
       ss[e] = tap - rr[e] * a.S;
     }
     const int hw = a.Ho * a.Wo;
+    // with 64 column groups the k-row is wave-uniform: keep the pixel walk in scalar registers
+    const int krw = (C4 % 64 == 0) ? __builtin_amdgcn_readfirstlane(kr) : kr;
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
-      const int p = kb + kr + i * (NT / C4);
+      const int p = kb + krw + i * (NT / C4);
       pb[i] = p / hw;
       const int rem = p - pb[i] * hw;
       poh[i] = rem / a.Wo;
@@ -506,14 +508,24 @@ static long long tiles_of(int cfg, const GemmArgs& a) {
   return (long long)cdiv(a.M, TILE_M[cfg]) * cdiv(a.N, TILE_N[cfg]) * a.batch;
 }
 
-// pick the largest tile that still gives >= 1 full wave of the 256 CUs (wgrad adds split-K)
-static int choose_tile(const GemmArgs& a, bool allow_big) {
+// largest useful split-K factor (>= 16 K-tiles per split)
+static int max_splits_of(const GemmArgs& a, bool can_split) {
+  if (!can_split) return 1;
+  int s = 1;
+  while (s < 64 && (long long)a.K / (s * 2) >= 512) s *= 2;
+  return s;
+}
+
+// pick the largest tile that still gives >= 1 full wave of the 256 CUs, counting the blocks that
+// split-K adds when a workspace is available (wgrad: small M x N, huge K)
+static int choose_tile(const GemmArgs& a, bool allow_big, bool can_split) {
+  const long long ms = max_splits_of(a, can_split);
   if (allow_big) {
-    if (tiles_of(T256x256, a) >= 240 && a.M > 128 && a.N > 128) return T256x256;
-    if (a.N <= 128 && tiles_of(T256x128, a) >= 240 && a.M > 128) return T256x128;
-    if (a.M <= 128 && tiles_of(T128x256, a) >= 240 && a.N > 128) return T128x256;
+    if (tiles_of(T256x256, a) * ms >= 240 && a.M > 128 && a.N > 128) return T256x256;
+    if (a.N <= 128 && tiles_of(T256x128, a) * ms >= 240 && a.M > 128) return T256x128;
+    if (a.M <= 128 && tiles_of(T128x256, a) * ms >= 240 && a.N > 128) return T128x256;
   }
-  if (tiles_of(T128x128, a) >= 200 && a.M > 64 && a.N > 64) return T128x128;
+  if (tiles_of(T128x128, a) * ms >= 200 && a.M > 64 && a.N > 64) return T128x128;
   return T64x64;
 }
 
@@ -559,8 +571,9 @@ static void set_splits(GemmArgs& a, int splits) {
 // split K so that a small-MN / huge-K product (wgrad) still fills the chip; >= 16 K-tiles per split
 static int choose_splits(const GemmArgs& a, int cfg) {
   const long long tiles = tiles_of(cfg, a);
+  const int ms = max_splits_of(a, true);
   int s = 1;
-  while (tiles * s < 400 && (long long)a.K / (s * 2) >= 512 && s < 64) s *= 2;
+  while (tiles * s < 400 && s < ms) s *= 2;
   return s;
 }
 
@@ -608,7 +621,7 @@ int mvae_gemm_strided_batched(int trans_a, int trans_b, int m, int n, int k, flo
   hipStream_t st = (hipStream_t)stream;
   const bool va = (trans_a ? (m % 4 == 0) : (k % 4 == 0)) && (lda % 4 == 0) && (stride_a % 4 == 0) && al16(A);
   const bool vb = (trans_b ? (k % 4 == 0) : (n % 4 == 0)) && (ldb % 4 == 0) && (stride_b % 4 == 0) && al16(B);
-  const int cfg = choose_tile(a, va && vb);
+  const int cfg = choose_tile(a, va && vb, workspace != nullptr);
   plan_splits(a, cfg, workspace, workspace_bytes);
   const int ak = trans_a ? A_COLM : A_ROWK;
   const int bk = trans_b ? B_ROWK : B_COLN;
@@ -628,9 +641,9 @@ int mvae_gemm_strided_batched(int trans_a, int trans_b, int m, int n, int k, flo
 size_t mvae_gemm_workspace_bytes(int m, int n, int k, int batch) {
   GemmArgs a{};
   a.M = m; a.N = n; a.K = k; a.batch = batch;
-  set_splits(a, choose_splits(a, choose_tile(a, true)));
+  set_splits(a, choose_splits(a, choose_tile(a, true, true)));
   size_t b1 = splitk_ws_bytes(a);
-  set_splits(a, choose_splits(a, choose_tile(a, false)));
+  set_splits(a, choose_splits(a, choose_tile(a, false, true)));
   return std::max(b1, splitk_ws_bytes(a));
 }
 
@@ -656,7 +669,7 @@ int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const fl
   a.stride = stride; a.pad_t = pad_t; a.pad_l = pad_l; a.conv_mode = mode;
   hipStream_t st = (hipStream_t)stream;
   const bool v = (cin % 4 == 0) && al16(x) && al16(w);
-  const int cfg = choose_tile(a, v);
+  const int cfg = choose_tile(a, v, false);
   if (v) launch_big<A_CONV, 4, B_ROWK, 4>(a, st, cfg);
   else launch_small<A_CONV, 1, B_ROWK, 1>(a, st, cfg);
   return finish(a, st);
@@ -684,7 +697,7 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float bet
   hipStream_t st = (hipStream_t)stream;
   const bool va = (cout % 4 == 0) && al16(dy);
   const bool vb = (cin % 4 == 0) && al16(x);
-  const int cfg = choose_tile(a, va && vb);
+  const int cfg = choose_tile(a, va && vb, workspace != nullptr);
   plan_splits(a, cfg, workspace, workspace_bytes);
   if (va && vb) launch_big<A_COLM, 4, B_WGRADX, 4>(a, st, cfg);
   else if (va) launch_small<A_COLM, 4, B_WGRADX, 1>(a, st, cfg);
@@ -696,9 +709,9 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float bet
 size_t mvae_conv2d_wgrad_workspace_bytes(int nb, int cin, int cout, int kh, int kw, int ho, int wo) {
   GemmArgs a{};
   wgrad_args(a, nb, cin, cout, kh, kw, ho, wo);
-  set_splits(a, choose_splits(a, choose_tile(a, true)));
+  set_splits(a, choose_splits(a, choose_tile(a, true, true)));
   size_t b1 = splitk_ws_bytes(a);
-  set_splits(a, choose_splits(a, choose_tile(a, false)));
+  set_splits(a, choose_splits(a, choose_tile(a, false, true)));
   return std::max(b1, splitk_ws_bytes(a));
 }
 
