@@ -10,7 +10,7 @@ CXXFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-functi
 
 all: $(PKG)/libmvae_hip.so
 
-build/%.o: $(PKG)/csrc/% $(PKG)/csrc/common.h
+build/%.o: $(PKG)/csrc/% $(PKG)/csrc/common.h $(PKG)/csrc/gemm_core.h
 	@mkdir -p build
 	$(HIPCC) $(CXXFLAGS) -c $< -o $@
 
