@@ -1,0 +1,72 @@
+"""Data-parallel plumbing on CPU (gloo, world_size 2): initial-parameter broadcast, the bucketed
+all-reduce of the ONE flat gradient buffer, and the 1/world average folded into the optimizer's
+grad_scale. The averaged gradient must equal the gradient of the concatenated global batch (the DDP
+parity argument of SURVEY.md section 8(e): every op of the VAE is per-sample and the loss is a mean)."""
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class _Mod:
+    """Stand-in for VAELightningModule: only the attributes ddp.DataParallel touches."""
+
+    def __init__(self, model):
+        from medvae_disentangled_multimodal_amd.optim import FlatParameters
+
+        class _Opt:
+            grad_scale = 1.0
+        self.model = model
+        self.flat = FlatParameters(model, torch.device("cpu"))
+        self.optimizer = _Opt()
+        self.process_group = None
+
+    def configure_optimizers(self):
+        pass
+
+
+def _worker(rank, world, init_file, out_file):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    from medvae_disentangled_multimodal_amd import ddp
+    torch.manual_seed(100 + rank)  # different init on each rank: broadcast must fix it
+    model = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.Tanh(), torch.nn.Linear(5, 3))
+    mod = _Mod(model)
+    dp = ddp.DataParallel(mod, bucket_bytes=64)  # tiny buckets: exercise the slicing
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(8, 7, generator=g)
+    y = torch.randn(8, 3, generator=g)
+    xs, ys = x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4]
+    mod.flat.zero_grad()
+    loss = torch.nn.functional.mse_loss(model(xs), ys)
+    loss.backward()
+    dp.allreduce_gradients(mod.flat)
+    avg = mod.flat.grad * mod.optimizer.grad_scale
+    if rank == 0:
+        torch.save({"params": mod.flat.data.clone(), "grad": avg.clone()}, out_file)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_flat_gradient_allreduce_matches_global_batch():
+    with tempfile.TemporaryDirectory() as d:
+        init_file = os.path.join(d, "init")
+        out_file = os.path.join(d, "out.pt")
+        mp.spawn(_worker, args=(2, init_file, out_file), nprocs=2, join=True)
+        res = torch.load(out_file, weights_only=True)
+    # reference: rank-0 initial weights (broadcast), the full batch of 8, one process
+    torch.manual_seed(100)
+    ref = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.Tanh(), torch.nn.Linear(5, 3))
+    flat_ref = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
+    from medvae_disentangled_multimodal_amd.optim import FlatParameters
+    f = FlatParameters(ref, torch.device("cpu"))
+    assert torch.allclose(res["params"], f.data)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(8, 7, generator=g)
+    y = torch.randn(8, 3, generator=g)
+    f.zero_grad()
+    torch.nn.functional.mse_loss(ref(x), y).backward()
+    assert torch.allclose(res["grad"], f.grad, rtol=1e-5, atol=1e-7)
+    assert flat_ref.numel() <= f.numel
