@@ -31,6 +31,7 @@
 #pragma once
 #include "common.h"
 #include <algorithm>
+#include <stdlib.h>
 
 namespace mvae {
 
@@ -434,17 +435,34 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int nt = ke > kb ? (ke - kb + BK - 1) / BK : 0;
+  // Prologue: tile 0 -> LDS buffer 0, tile 1 -> registers.
   if (nt > 0) {
     la.load(a);
     lb.load(a);
     la.store(lds);
     lb.store(lds + IA::SIZE);
   }
+  if (nt > 1) {
+    la.advance(a);
+    lb.advance(a);
+    la.load(a);
+    lb.load(a);
+  }
   __syncthreads();
   const int arow = wm * (BM / WGM), brow = wn * (BN / WGN);
+  // Steady state ("write after barrier"): at iteration t the registers hold tile t+1 (loaded one
+  // full compute phase earlier). Right after the barrier each wave splits/writes them into the
+  // free buffer, immediately re-issues the global loads of tile t+2 into the same registers, and
+  // multiplies tile t -- whose buffer was completed before the barrier -- so the LDS writes and the
+  // VALU split overlap the wave's own MFMAs and the global loads have a whole phase to land.
   for (int t = 0; t < nt; ++t) {
     const int cur = t & 1;
     if (t + 1 < nt) {
+      __bf16* nb = lds + (cur ^ 1) * BUF;
+      la.store(nb);
+      lb.store(nb + IA::SIZE);
+    }
+    if (t + 2 < nt) {
       la.advance(a);
       lb.advance(a);
       la.load(a);
@@ -471,11 +489,6 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
         }
       }
-    }
-    if (t + 1 < nt) {
-      __bf16* nb = lds + (cur ^ 1) * BUF;
-      la.store(nb);
-      lb.store(nb + IA::SIZE);
     }
     __syncthreads();
   }
@@ -547,7 +560,17 @@ inline int max_splits_of(const GemmArgs& a, bool can_split) {
 
 // pick the largest tile that still gives >= 1 full wave of the 256 CUs, counting the blocks that
 // split-K adds when a workspace is available (wgrad: small M x N, huge K)
+inline int tile_override() {
+  static int v = [] {
+    const char* e = getenv("MVAE_GEMM_TILE");  // experiment knob: force a tile config (0..4)
+    return e ? atoi(e) : -1;
+  }();
+  return v;
+}
+
 inline int choose_tile(const GemmArgs& a, bool allow_big, bool can_split) {
+  const int ov = tile_override();
+  if (ov >= 0 && ov <= 4 && (allow_big || ov >= T128x128)) return ov;
   const long long ms = max_splits_of(a, can_split);
   if (allow_big) {
     if (tiles_of(T256x256, a) * ms >= 240 && a.M > 128 && a.N > 128) return T256x256;
