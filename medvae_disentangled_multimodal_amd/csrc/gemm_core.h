@@ -455,20 +455,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   // free buffer, immediately re-issues the global loads of tile t+2 into the same registers, and
   // multiplies tile t -- whose buffer was completed before the barrier -- so the LDS writes and the
   // VALU split overlap the wave's own MFMAs and the global loads have a whole phase to land.
-  for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nt) {
-      __bf16* nb = lds + (cur ^ 1) * BUF;
-      la.store(nb);
-      lb.store(nb + IA::SIZE);
-    }
-    if (t + 2 < nt) {
-      la.advance(a);
-      lb.advance(a);
-      la.load(a);
-      lb.load(a);
-    }
-    const __bf16* Ai = lds + cur * BUF;
+  auto compute = [&](const __bf16* Ai) {
     const __bf16* Bi = Ai + IA::SIZE;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -490,8 +477,38 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
         }
       }
     }
+  };
+  // steady state: branch-free body (one scheduling region), so the split/ds_write of tile t+1 and
+  // the address math of tile t+2 can interleave with the MFMAs of tile t
+  int t = 0;
+  for (; t + 2 < nt; ++t) {
+    __bf16* nb = lds + ((t & 1) ^ 1) * BUF;
+    la.store(nb);
+    lb.store(nb + IA::SIZE);
+    la.advance(a);
+    lb.advance(a);
+    la.load(a);
+    lb.load(a);
+    compute(lds + (t & 1) * BUF);
+#ifdef MVAE_SCHED_INTERLEAVE
+#pragma unroll
+    for (int q = 0; q < 6 * TM * TN; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // 3 VALU
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+    }
+#endif
     __syncthreads();
   }
+  if (t + 1 < nt) {  // last staged tile: write it, nothing left to load
+    __bf16* nb = lds + ((t & 1) ^ 1) * BUF;
+    la.store(nb);
+    lb.store(nb + IA::SIZE);
+    compute(lds + (t & 1) * BUF);
+    __syncthreads();
+    ++t;
+  }
+  if (t < nt) compute(lds + (t & 1) * BUF);
 
   // epilogue: C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
   // Stores go through buffer descriptors: rows/cols outside the matrix are dropped by the hardware.
@@ -620,12 +637,24 @@ inline void set_splits(GemmArgs& a, int splits) {
   a.splits = std::max(1, cdiv(a.K, a.k_split));
 }
 
+// Split-K factor: fill the chip AND avoid wave quantisation (a last round of blocks that leaves
+// most CUs idle): the smallest s whose tiles*s blocks make >= 1 round of 256 CUs at >= 95 % round
+// efficiency (fewer splits = less partial-sum traffic); otherwise the most efficient s.
 inline int choose_splits(const GemmArgs& a, int cfg) {
   const long long tiles = tiles_of(cfg, a);
-  const int ms = max_splits_of(a, true);
-  int s = 1;
-  while (tiles * s < 400 && s < ms) s *= 2;
-  return s;
+  const int ms = std::max(1, (int)std::min<long long>(64, a.K / 512));
+  if (tiles >= 1024) return 1;
+  int best = 1;
+  double best_eff = -1.0;
+  for (int s = 1; s <= ms; ++s) {
+    const long long blocks = tiles * s;
+    const long long rounds = (blocks + 255) / 256;
+    const double eff = (double)blocks / (double)(rounds * 256);
+    if (blocks >= 240 && eff >= 0.95) return s;
+    const double score = eff - (blocks < 240 ? 0.5 : 0.0);
+    if (score > best_eff + 1e-9) { best_eff = score; best = s; }
+  }
+  return best;
 }
 
 inline void plan_splits(GemmArgs& a, int cfg, float* ws, size_t ws_bytes) {
