@@ -38,86 +38,107 @@ struct GnArgs {
   double* ws;  // [nb][chunks][C][2]
 };
 
-__device__ __forceinline__ float gn_dyn(const GnArgs& a, float xv, float dyv, float m, float rs, int c,
-                                        long long idx) {
-  float d = dyv;
-  if (a.drop_p > 0.f) {
-    const float u = hash_uniform(a.seed, (unsigned long long)idx);
-    d = (u >= a.drop_p) ? d / (1.f - a.drop_p) : 0.f;
+// Thread mapping shared by the NHWC GroupNorm kernels: a block owns (sample b, chunk of rows); a
+// thread owns one 4-channel column group c4 and walks rows row_lo + rph, + rpar, ... (rpar rows in
+// flight per block), unrolled 4x so every thread keeps 4 independent 16-B loads in flight.
+struct GnMap {
+  int C4, rpar, c4, rph, row_lo, row_hi;
+  bool act;
+  __device__ GnMap(const GnArgs& a, int cg0) {
+    C4 = a.C >> 2;
+    const int tid = threadIdx.x;
+    rpar = C4 >= 256 ? 1 : 256 / C4;
+    c4 = C4 >= 256 ? cg0 + tid : tid % C4;
+    rph = C4 >= 256 ? 0 : tid / C4;
+    act = C4 >= 256 ? (c4 < C4) : (tid < rpar * C4);
+    row_lo = blockIdx.x * a.rows_per_chunk;
+    row_hi = min(a.hw, row_lo + a.rows_per_chunk);
   }
-  if (a.silu) {
-    const float yn = (xv - m) * rs * a.gamma[c] + a.beta[c];
-    const float s = sigmoid_f(yn);
-    d = d * s * (1.f + yn * (1.f - s));
-  }
-  return d;
-}
+};
 
 template <int KIND>
 __global__ void __launch_bounds__(256) gn_partial_kernel(GnArgs a) {
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
-  const int C4 = a.C >> 2;
-  const int rpar = C4 >= 256 ? 1 : 256 / C4;  // rows processed in parallel
-  const int row_lo = chunk * a.rows_per_chunk;
-  const int row_hi = min(a.hw, row_lo + a.rows_per_chunk);
   const int cpg = a.C / a.G;
   __shared__ double red[256 * 8];
   const long long sbase = (long long)b * a.hw * a.C;
-  // thread -> (column group, row phase); for C4 > 256 a thread owns several column groups
-  for (int cg0 = 0; cg0 < C4; cg0 += 256) {
-    const int c4 = (C4 >= 256) ? cg0 + tid : tid % C4;
-    const int rph = (C4 >= 256) ? 0 : tid / C4;
-    const bool act = (C4 >= 256) ? (c4 < C4) : (tid < rpar * C4);
+  for (int cg0 = 0; cg0 < (a.C >> 2); cg0 += 256) {
+    GnMap mp(a, cg0);
     double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
-    if (act) {
-      float m[4] = {0, 0, 0, 0}, rs[4] = {0, 0, 0, 0};
+    if (mp.act) {
+      float m[4] = {0, 0, 0, 0}, rs[4] = {0, 0, 0, 0}, gm[4] = {0, 0, 0, 0}, bt[4] = {0, 0, 0, 0};
       if (KIND == 1) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int g = (c4 * 4 + e) / cpg;
+          const int c = mp.c4 * 4 + e, g = c / cpg;
           m[e] = a.mean[b * a.G + g];
           rs[e] = a.rstd[b * a.G + g];
+          gm[e] = a.gamma[c];
+          bt[e] = a.beta[c];
         }
       }
-      for (int row = row_lo + rph; row < row_hi; row += rpar) {
-        const long long off = sbase + (long long)row * a.C + c4 * 4;
-        const float4 xv = *(const float4*)(a.x + off);
-        const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
-        if (KIND == 0) {
+      const float* xp = a.x + sbase + mp.c4 * 4;
+      const float* dp = a.dy + sbase + mp.c4 * 4;
+      int row = mp.row_lo + mp.rph;
+      for (; row < mp.row_hi; row += 4 * mp.rpar) {
+        float4 xv[4], dv[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            s0[e] += xs[e];
-            s1[e] += (double)xs[e] * xs[e];
-          }
-        } else {
-          const float4 dv = *(const float4*)(a.dy + off);
-          const float ds[4] = {dv.x, dv.y, dv.z, dv.w};
+        for (int u = 0; u < 4; ++u) {
+          const int r = row + u * mp.rpar;
+          const bool ok = r < mp.row_hi;
+          xv[u] = ok ? *(const float4*)(xp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+          if (KIND == 1) dv[u] = ok ? *(const float4*)(dp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+        }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float d = gn_dyn(a, xs[e], ds[e], m[e], rs[e], c4 * 4 + e, off + e);
-            s0[e] += d;
-            s1[e] += (double)d * ((xs[e] - m[e]) * rs[e]);
+        for (int u = 0; u < 4; ++u) {
+          const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+          if (KIND == 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              s0[e] += xs[e];
+              s1[e] += (double)xs[e] * xs[e];
+            }
+          } else {
+            const int r = row + u * mp.rpar;
+            if (r >= mp.row_hi) continue;
+            const float ds[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
+            const long long off = sbase + (long long)r * a.C + mp.c4 * 4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float d = ds[e];
+              if (a.drop_p > 0.f) {
+                const float uu = hash_uniform(a.seed, (unsigned long long)(off + e));
+                d = (uu >= a.drop_p) ? d / (1.f - a.drop_p) : 0.f;
+              }
+              const float xh = (xs[e] - m[e]) * rs[e];
+              if (a.silu) {
+                const float yn = xh * gm[e] + bt[e];
+                const float sg = sigmoid_f(yn);
+                d = d * sg * (1.f + yn * (1.f - sg));
+              }
+              s0[e] += d;
+              s1[e] += (double)d * xh;
+            }
           }
         }
       }
     }
-    // reduce the rpar row phases that share a column group
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       red[tid * 8 + e] = s0[e];
       red[tid * 8 + 4 + e] = s1[e];
     }
     __syncthreads();
-    if (act && rph == 0) {
-      for (int p = 1; p < rpar; ++p) {
-        const int t2 = tid + p * C4;
+    if (mp.act && mp.rph == 0) {
+      for (int p = 1; p < mp.rpar; ++p) {  // fixed order: deterministic
+        const int t2 = tid + p * mp.C4;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           s0[e] += red[t2 * 8 + e];
           s1[e] += red[t2 * 8 + 4 + e];
         }
       }
-      double* w = a.ws + (((long long)b * a.chunks + chunk) * a.C + c4 * 4) * 2;
+      double* w = a.ws + (((long long)b * a.chunks + chunk) * a.C + mp.c4 * 4) * 2;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         w[2 * e] = s0[e];
@@ -125,127 +146,199 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(GnArgs a) {
       }
     }
     __syncthreads();
-    if (C4 < 256) break;
+    if ((a.C >> 2) < 256) break;
   }
 }
 
-// stats finalize: one thread per (b, g) -> mean, rstd, and per-(b,c) scale/shift for the apply
-__global__ void gn_stats_finalize_kernel(GnArgs a, float* mean, float* rstd, float* scale, float* shift,
-                                         float eps) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// one wave per (b, g): fixed-order wave reduction of the chunk x channel partials
+__device__ __forceinline__ void gn_group_sums(const GnArgs& a, int b, int g, double& S0, double& S1) {
+  const int lane = threadIdx.x & 63, cpg = a.C / a.G;
+  double s0 = 0, s1 = 0;
+  for (int i = lane; i < a.chunks * cpg; i += 64) {
+    const int ch = i / cpg, c = g * cpg + (i - ch * cpg);
+    const double* w = a.ws + (((long long)b * a.chunks + ch) * a.C + c) * 2;
+    s0 += w[0];
+    s1 += w[1];
+  }
+  S0 = wave_sum_d(s0);
+  S1 = wave_sum_d(s1);
+}
+
+__global__ void __launch_bounds__(256) gn_stats_finalize_kernel(GnArgs a, float* mean, float* rstd, float* scale,
+                                                                float* shift, float eps) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= a.nb * a.G) return;
   const int b = i / a.G, g = i - b * a.G;
   const int cpg = a.C / a.G;
-  double s0 = 0, s1 = 0;
-  for (int ch = 0; ch < a.chunks; ++ch) {
-    const double* w = a.ws + (((long long)b * a.chunks + ch) * a.C + g * cpg) * 2;
-    for (int c = 0; c < cpg; ++c) {
-      s0 += w[2 * c];
-      s1 += w[2 * c + 1];
-    }
-  }
+  double s0, s1;
+  gn_group_sums(a, b, g, s0, s1);
   const double n = (double)a.hw * cpg;
   const double mu = s0 / n;
   double var = s1 / n - mu * mu;
   if (var < 0) var = 0;
   const float rs = (float)(1.0 / sqrt(var + (double)eps));
-  mean[i] = (float)mu;
-  rstd[i] = rs;
-  for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+  if (lane == 0) {
+    mean[i] = (float)mu;
+    rstd[i] = rs;
+  }
+  for (int c = g * cpg + lane; c < (g + 1) * cpg; c += 64) {
     const float sc = rs * a.gamma[c];
     scale[b * a.C + c] = sc;
     shift[b * a.C + c] = a.beta[c] - (float)mu * sc;
   }
 }
 
-__global__ void __launch_bounds__(256) gn_apply_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                       const float* __restrict__ scale,
-                                                       const float* __restrict__ shift, int nb, int hw, int C,
-                                                       int silu, float drop_p, unsigned long long seed) {
-  const int C4 = C >> 2;
-  const long long total4 = (long long)nb * hw * C4;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total4;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int c4 = (int)(e % C4);
-    const int b = (int)(e / ((long long)hw * C4));
-    const float4 sc = *(const float4*)(scale + (long long)b * C + c4 * 4);
-    const float4 sh = *(const float4*)(shift + (long long)b * C + c4 * 4);
-    const float4 xv = *(const float4*)(x + e * 4);
-    float o[4] = {xv.x * sc.x + sh.x, xv.y * sc.y + sh.y, xv.z * sc.z + sh.z, xv.w * sc.w + sh.w};
+// y = [dropout](silu?(x*scale + shift))
+__global__ void __launch_bounds__(256) gn_apply_kernel(GnArgs a, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, float* __restrict__ y) {
+  const int b = blockIdx.y;
+  const long long sbase = (long long)b * a.hw * a.C;
+  for (int cg0 = 0; cg0 < (a.C >> 2); cg0 += 256) {
+    GnMap mp(a, cg0);
+    if (mp.act) {
+      const float4 sc = *(const float4*)(scale + (long long)b * a.C + mp.c4 * 4);
+      const float4 sh = *(const float4*)(shift + (long long)b * a.C + mp.c4 * 4);
+      const float* xp = a.x + sbase + mp.c4 * 4;
+      float* yp = y + sbase + mp.c4 * 4;
+      for (int row = mp.row_lo + mp.rph; row < mp.row_hi; row += 4 * mp.rpar) {
+        float4 xv[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (silu) o[k] = o[k] * sigmoid_f(o[k]);
-      if (drop_p > 0.f) {
-        const float u = hash_uniform(seed, (unsigned long long)(e * 4 + k));
-        o[k] = (u >= drop_p) ? o[k] / (1.f - drop_p) : 0.f;
+        for (int u = 0; u < 4; ++u) {
+          const int r = row + u * mp.rpar;
+          xv[u] = r < mp.row_hi ? *(const float4*)(xp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = row + u * mp.rpar;
+          if (r >= mp.row_hi) continue;
+          float o[4] = {xv[u].x * sc.x + sh.x, xv[u].y * sc.y + sh.y, xv[u].z * sc.z + sh.z, xv[u].w * sc.w + sh.w};
+          const long long off = sbase + (long long)r * a.C + mp.c4 * 4;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (a.silu) o[k] = o[k] * sigmoid_f(o[k]);
+            if (a.drop_p > 0.f) {
+              const float uu = hash_uniform(a.seed, (unsigned long long)(off + k));
+              o[k] = (uu >= a.drop_p) ? o[k] / (1.f - a.drop_p) : 0.f;
+            }
+          }
+          *(float4*)(yp + (long long)r * a.C) = float4{o[0], o[1], o[2], o[3]};
+        }
       }
     }
-    *(float4*)(y + e * 4) = float4{o[0], o[1], o[2], o[3]};
+    if ((a.C >> 2) < 256) break;
   }
 }
 
 // backward finalize: per (b,g) coefficients so that dx = dyn*k1[b,c] + x*k2[b,g] + k3[b,g]
-__global__ void gn_bwd_finalize_kernel(GnArgs a, float* k1, float* k2, float* k3) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(256) gn_bwd_finalize_kernel(GnArgs a, float* k1, float* k2, float* k3) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= a.nb * a.G) return;
   const int b = i / a.G, g = i - b * a.G;
   const int cpg = a.C / a.G;
   double A1 = 0, A2 = 0;
-  for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
-    double s0 = 0, s1 = 0;
-    for (int ch = 0; ch < a.chunks; ++ch) {
-      const double* w = a.ws + (((long long)b * a.chunks + ch) * a.C + c) * 2;
-      s0 += w[0];
-      s1 += w[1];
-    }
-    A1 += (double)a.gamma[c] * s0;
-    A2 += (double)a.gamma[c] * s1;
-    k1[b * a.C + c] = a.rstd[i] * a.gamma[c];
+  for (int j = lane; j < a.chunks * cpg; j += 64) {
+    const int ch = j / cpg, c = g * cpg + (j - ch * cpg);
+    const double* w = a.ws + (((long long)b * a.chunks + ch) * a.C + c) * 2;
+    A1 += (double)a.gamma[c] * w[0];
+    A2 += (double)a.gamma[c] * w[1];
   }
-  const double n = (double)a.hw * cpg;
-  const double rs = a.rstd[i], mu = a.mean[i];
-  k2[i] = (float)(-rs * rs * A2 / n);
-  k3[i] = (float)(-rs * A1 / n + mu * rs * rs * A2 / n);
+  A1 = wave_sum_d(A1);
+  A2 = wave_sum_d(A2);
+  const float rsf = a.rstd[i];
+  for (int c = g * cpg + lane; c < (g + 1) * cpg; c += 64) k1[b * a.C + c] = rsf * a.gamma[c];
+  if (lane == 0) {
+    const double n = (double)a.hw * cpg;
+    const double rs = rsf, mu = a.mean[i];
+    k2[i] = (float)(-rs * rs * A2 / n);
+    k3[i] = (float)(-rs * A1 / n + mu * rs * rs * A2 / n);
+  }
 }
 
-// dgamma[c] += sum_{b,chunks} s1 ; dbeta[c] += sum s0  (fixed order)
-__global__ void gn_param_grad_kernel(GnArgs a, float* dgamma, float* dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.C) return;
+// dgamma[c] += sum_{b,chunks} s1 ; dbeta[c] += sum s0   (64 channels x 4 partial lanes per block)
+__global__ void __launch_bounds__(256) gn_param_grad_kernel(GnArgs a, float* dgamma, float* dbeta) {
+  __shared__ double sh[2][256];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   double s0 = 0, s1 = 0;
-  for (int b = 0; b < a.nb; ++b)
-    for (int ch = 0; ch < a.chunks; ++ch) {
-      const double* w = a.ws + (((long long)b * a.chunks + ch) * a.C + c) * 2;
+  if (c < a.C) {
+    const int n = a.nb * a.chunks;
+    for (int i = rg; i < n; i += 4) {
+      const double* w = a.ws + ((long long)i * a.C + c) * 2;
       s0 += w[0];
       s1 += w[1];
     }
-  if (dgamma) dgamma[c] += (float)s1;
-  if (dbeta) dbeta[c] += (float)s0;
+  }
+  sh[0][threadIdx.x] = s0;
+  sh[1][threadIdx.x] = s1;
+  __syncthreads();
+  if (rg == 0 && c < a.C) {
+    s0 = sh[0][cl] + sh[0][cl + 64] + sh[0][cl + 128] + sh[0][cl + 192];
+    s1 = sh[1][cl] + sh[1][cl + 64] + sh[1][cl + 128] + sh[1][cl + 192];
+    if (dgamma) dgamma[c] += (float)s1;
+    if (dbeta) dbeta[c] += (float)s0;
+  }
 }
 
 __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __restrict__ k1,
                                                     const float* __restrict__ k2, const float* __restrict__ k3,
                                                     float* __restrict__ dx) {
-  const int C4 = a.C >> 2;
+  const int b = blockIdx.y;
   const int cpg = a.C / a.G;
-  const long long total4 = (long long)a.nb * a.hw * C4;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total4;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int c4 = (int)(e % C4);
-    const int b = (int)(e / ((long long)a.hw * C4));
-    const float4 xv = *(const float4*)(a.x + e * 4);
-    const float4 dv = *(const float4*)(a.dy + e * 4);
-    const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
-    const float ds[4] = {dv.x, dv.y, dv.z, dv.w};
-    float o[4];
+  const long long sbase = (long long)b * a.hw * a.C;
+  for (int cg0 = 0; cg0 < (a.C >> 2); cg0 += 256) {
+    GnMap mp(a, cg0);
+    if (mp.act) {
+      float m[4], rs[4], gm[4], bt[4], q1[4], q2[4], q3[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int c = c4 * 4 + k;
-      const int bg = b * a.G + c / cpg;
-      const float d = gn_dyn(a, xs[k], ds[k], a.mean[bg], a.rstd[bg], c, e * 4 + k);
-      o[k] = d * k1[(long long)b * a.C + c] + xs[k] * k2[bg] + k3[bg];
+      for (int e = 0; e < 4; ++e) {
+        const int c = mp.c4 * 4 + e, bg = b * a.G + c / cpg;
+        m[e] = a.mean[bg];
+        rs[e] = a.rstd[bg];
+        gm[e] = a.gamma[c];
+        bt[e] = a.beta[c];
+        q1[e] = k1[(long long)b * a.C + c];
+        q2[e] = k2[bg];
+        q3[e] = k3[bg];
+      }
+      const float* xp = a.x + sbase + mp.c4 * 4;
+      const float* dp = a.dy + sbase + mp.c4 * 4;
+      float* op = dx + sbase + mp.c4 * 4;
+      for (int row = mp.row_lo + mp.rph; row < mp.row_hi; row += 4 * mp.rpar) {
+        float4 xv[4], dv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = row + u * mp.rpar;
+          const bool ok = r < mp.row_hi;
+          xv[u] = ok ? *(const float4*)(xp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+          dv[u] = ok ? *(const float4*)(dp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = row + u * mp.rpar;
+          if (r >= mp.row_hi) continue;
+          const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+          const float ds[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
+          const long long off = sbase + (long long)r * a.C + mp.c4 * 4;
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float d = ds[e];
+            if (a.drop_p > 0.f) {
+              const float uu = hash_uniform(a.seed, (unsigned long long)(off + e));
+              d = (uu >= a.drop_p) ? d / (1.f - a.drop_p) : 0.f;
+            }
+            if (a.silu) {
+              const float yn = (xs[e] - m[e]) * rs[e] * gm[e] + bt[e];
+              const float sg = sigmoid_f(yn);
+              d = d * sg * (1.f + yn * (1.f - sg));
+            }
+            o[e] = d * q1[e] + xs[e] * q2[e] + q3[e];
+          }
+          *(float4*)(op + (long long)r * a.C) = float4{o[0], o[1], o[2], o[3]};
+        }
+      }
     }
-    *(float4*)(dx + e * 4) = float4{o[0], o[1], o[2], o[3]};
+    if ((a.C >> 2) < 256) break;
   }
 }
 
@@ -254,8 +347,6 @@ static int gn_chunks(int nb, int hw) {
   while ((long long)nb * chunks < 1024 && hw / (chunks * 2) >= 16) chunks *= 2;
   return chunks;
 }
-
-static int grid_for(long long n4) { return (int)std::min<long long>((n4 + 255) / 256, 8192); }
 
 }  // namespace mvae
 
@@ -291,10 +382,10 @@ int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* be
   float* scale = (float*)((char*)workspace + (size_t)nb * a.chunks * c * 2 * sizeof(double));
   float* shift = scale + (size_t)nb * c;
   hipLaunchKernelGGL(gn_partial_kernel<0>, dim3(a.chunks, nb), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(gn_stats_finalize_kernel, dim3(cdiv((long long)nb * groups, 256)), dim3(256), 0, st, a,
+  hipLaunchKernelGGL(gn_stats_finalize_kernel, dim3(cdiv((long long)nb * groups, 4)), dim3(256), 0, st, a,
                      mean, rstd, scale, shift, eps);
-  hipLaunchKernelGGL(gn_apply_kernel, dim3(grid_for((long long)nb * hw * c / 4)), dim3(256), 0, st, x, y, scale,
-                     shift, nb, hw, c, silu, drop_p, seed);
+  a.silu = silu; a.drop_p = drop_p; a.seed = seed;
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(a.chunks, nb), dim3(256), 0, st, a, scale, shift, y);
   return launch_status();
 }
 
@@ -322,12 +413,11 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
   float* k2 = k1 + (size_t)nb * c;
   float* k3 = k2 + (size_t)nb * c;
   hipLaunchKernelGGL(gn_partial_kernel<1>, dim3(a.chunks, nb), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(cdiv((long long)nb * groups, 256)), dim3(256), 0, st, a, k1,
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(cdiv((long long)nb * groups, 4)), dim3(256), 0, st, a, k1,
                      k2, k3);
   if (dgamma || dbeta)
-    hipLaunchKernelGGL(gn_param_grad_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st, a, dgamma, dbeta);
-  hipLaunchKernelGGL(gn_dx_kernel, dim3(grid_for((long long)nb * hw * c / 4)), dim3(256), 0, st, a, k1, k2, k3,
-                     dx);
+    hipLaunchKernelGGL(gn_param_grad_kernel, dim3(cdiv(c, 64)), dim3(256), 0, st, a, dgamma, dbeta);
+  hipLaunchKernelGGL(gn_dx_kernel, dim3(a.chunks, nb), dim3(256), 0, st, a, k1, k2, k3, dx);
   return launch_status();
 }
 
