@@ -41,9 +41,10 @@ int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const fl
                      int nb, int h, int w_, int cin, int cout, int kh, int kw, int stride, int pad_t,
                      int pad_l, int ho, int wo, int mode, void* stream);
 
-/* Weight gradient of mvae_conv2d_nhwc (modes 0/1): dw = beta*dw + sum_pixels dy (x) x.
- * Replaces the weight half of aten::convolution_backward for the convolutions above. */
-int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float beta, int nb, int h, int w_,
+/* Weight gradient of mvae_conv2d_nhwc (modes 0/1): dw = beta*dw + sum_pixels dy (x) x, and (if dbias
+ * is non-null) the bias gradient dbias = beta*dbias + sum_pixels dy, computed from the same staged dy.
+ * Replaces the weight/bias half of aten::convolution_backward for the convolutions above. */
+int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* dbias, float beta, int nb, int h, int w_,
                            int cin, int cout, int kh, int kw, int stride, int pad_t, int pad_l, int ho,
                            int wo, int mode, float* workspace, size_t workspace_bytes, void* stream);
 size_t mvae_conv2d_wgrad_workspace_bytes(int nb, int cin, int cout, int kh, int kw, int ho, int wo);

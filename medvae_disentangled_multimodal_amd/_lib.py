@@ -24,7 +24,7 @@ SIGNATURES = {
     "mvae_last_error": (ctypes.c_char_p, []),
     "mvae_abi_version": (I, []),
     "mvae_conv2d_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P]),
-    "mvae_conv2d_wgrad_nhwc": (I, [P, P, P, F, I, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),
+    "mvae_conv2d_wgrad_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),
     "mvae_conv2d_wgrad_workspace_bytes": (Z, [I, I, I, I, I, I, I]),
     "mvae_conv_weight_transpose": (I, [P, P, I, I, I, I, P]),
     "mvae_conv_weight_upsample_dgrad": (I, [P, P, I, I, P]),

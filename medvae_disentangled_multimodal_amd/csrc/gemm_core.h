@@ -50,6 +50,7 @@ struct GemmArgs {
   const float* res; long long ldr, sR;
   float alpha, beta;
   float* ws;  // split partials [batch][splits][M][N]
+  float* bias_ws;  // wgrad only: per-split row sums of A = dY^T (the conv bias gradient) [splits][M]
   unsigned a_bytes, b_bytes, c_bytes, r_bytes;  // descriptor ranges (per batch entry)
   // gather geometry: source X is [nb][H][W][Cx]; output pixels are [nb][Ho][Wo]
   int H, W, Cx, Ho, Wo, R, S, stride, stride_shift, pad_t, pad_l;
@@ -256,6 +257,7 @@ struct LoadColK {
   unsigned ld;
   int rows, K, row0, k, c4, kr;
   float4 v[NF];
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};  // A side: running row sums of every staged element
   __device__ void init(const GemmArgs& a, const float* p, int row0_, int kb, int tid) {
     rs = make_rsrc(p, IS_A ? a.a_bytes : a.b_bytes);
     ld = (unsigned)(IS_A ? a.lda : a.ldb); rows = IS_A ? a.M : a.N; K = a.K;
@@ -285,7 +287,12 @@ struct LoadColK {
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
       const int krow = kr + i * (NT / C4);
-      if (krow < BK) st_split(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+      if (krow < BK) {
+        st_split(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+        if constexpr (IS_A) {
+          bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
+        }
+      }
     }
   }
 };
@@ -509,6 +516,28 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
     ++t;
   }
   if (t < nt) compute(lds + (t & 1) * BUF);
+
+  // wgrad: the conv bias gradient (row sums of A = dY^T over this split's pixels) falls out of the
+  // A staging for free; one column of tiles (tn == 0) publishes it, fixed-order reduction in LDS.
+  if constexpr (AK == A_COLM) {
+    if (a.bias_ws != nullptr && tn == 0) {
+      constexpr int KRN = NT / (BM / 4);
+      float* red = (float*)lds;
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[la.kr * BM + la.c4 * 4 + e] = la.bs[e];
+      __syncthreads();
+      if (la.kr == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float sum = 0.f;
+          for (int q = 0; q < KRN; ++q) sum += red[q * BM + la.c4 * 4 + e];
+          const int row = m0 + la.c4 * 4 + e;
+          if (row < a.M) a.bias_ws[((long long)bidx * a.splits + split) * a.M + row] = sum;
+        }
+      }
+    }
+  }
 
   // epilogue: C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
   // Stores go through buffer descriptors: rows/cols outside the matrix are dropped by the hardware.

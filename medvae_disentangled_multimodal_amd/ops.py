@@ -172,15 +172,17 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom):
     return dx
 
 
-def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom):
+def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None):
+    """dw (+ db when given and the conv is not pointwise) accumulate with `beta`. Returns True when
+    the bias gradient was produced by the fused wgrad kernel."""
     n, c, h, wd = x.shape
     co = dy.shape[1]
     _, _, ho, wo = dy.shape
     with _timed("conv_wgrad", 2.0 * n * ho * wo * co * c * g.kh * g.kw):
-        _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo)
+        return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db)
 
 
-def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo):
+def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None):
     st = _stream(dy)
     if g.pointwise:
         m = n * h * wd
@@ -189,11 +191,13 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo):
         # dW[n][c] = sum_m dy[m][n] x[m][c]: A = dy stored [K=m][M=cout], B = x stored [K=m][N=cin]
         _lib.call("mvae_gemm_strided_batched", 1, 0, co, c, m, 1.0, dy.data_ptr(), co, 0, x.data_ptr(), c, 0,
                   float(beta), dw.data_ptr(), c, 0, 1, None, None, 0, 0, ws.data_ptr(), ws.numel(), st)
-        return
+        return False
     nbytes = _lib.query("mvae_conv2d_wgrad_workspace_bytes", n, c, co, g.kh, g.kw, ho, wo)
     ws = ARENA.get("ws", nbytes, dy.device)
-    _lib.call("mvae_conv2d_wgrad_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), float(beta), n, h, wd, c, co,
-              g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, 1 if g.upsample else 0, ws.data_ptr(), ws.numel(), st)
+    _lib.call("mvae_conv2d_wgrad_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db), float(beta), n, h, wd,
+              c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, 1 if g.upsample else 0, ws.data_ptr(),
+              ws.numel(), st)
+    return db is not None
 
 
 def bias_grad_raw(dy2d_ptr, rows, n, out, beta, device, stream):
@@ -226,14 +230,19 @@ class Conv2dFn(torch.autograd.Function):
         dx = dw_ret = db_ret = dres = None
         if ctx.needs_input_grad[0]:
             dx = conv2d_dgrad_raw(dy, w, x.shape, g)
+        bias_done = False
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             tgt = _main_grad(ctx.weight_ref)
-            if tgt is not None:
+            btgt = _main_grad(ctx.bias_ref) if want_b else None
+            if tgt is not None and (not want_b or btgt is not None):
+                bias_done = conv2d_wgrad_raw(dy, x, tgt, 1.0, g, btgt)
+            elif tgt is not None:
                 conv2d_wgrad_raw(dy, x, tgt, 1.0, g)
             else:
                 dw_ret = torch.empty_like(w, memory_format=CL)
                 conv2d_wgrad_raw(dy, x, dw_ret, 0.0, g)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        if ctx.has_bias and ctx.needs_input_grad[2] and not bias_done:
             tgt = _main_grad(ctx.bias_ref)
             n, co, ho, wo = dy.shape
             if tgt is not None:

@@ -83,6 +83,16 @@ def test_conv_fwd_dgrad_wgrad(dev, case):
     # bias grad = column sum of dY: absolute error relative to the size of dY
     scale = float(yr.numel()) ** 0.5 + float(br.grad.abs().max())
     assert float((bd.grad.cpu() - br.grad).abs().max()) < 1e-5 * scale
+    # flat-buffer path: weight + bias gradients accumulated in place by the fused wgrad kernel
+    wm = cl(wt, dev).requires_grad_()
+    bm = b.to(dev).requires_grad_()
+    wm._mvae_main_grad = torch.full_like(wm, 0.5, memory_format=torch.channels_last)
+    bm._mvae_main_grad = torch.full_like(bm, 0.25)
+    ym = ops.conv2d(cl(x, dev), wm, bm, geom, residual=cl(res, dev))
+    ym.mul(torch.linspace(-1, 1, ym.numel(), device=dev).view(ym.shape)).sum().backward()
+    assert wm.grad is None and bm.grad is None
+    assert rel(wm._mvae_main_grad - 0.5, wr.grad) < CONV_TOL
+    assert float((bm._mvae_main_grad.cpu() - 0.25 - br.grad).abs().max()) < 1e-5 * scale
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
