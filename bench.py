@@ -103,6 +103,7 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch override (default: config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--detail", action="store_true", help="per-shape GEMM launch timings on stderr")
     args = ap.parse_args()
 
     import medvae_disentangled_multimodal_amd as M
@@ -155,10 +156,20 @@ def main():
         step_ms = (time.perf_counter() - t1) * 1e3
         rec = ops.PROFILE
         ops.PROFILE = None
-        tot_ms = sum(s.elapsed_time(e) for _, _, s, e in rec)
-        tot_fl = sum(f for _, f, _, _ in rec)
+        tot_ms = sum(r[2].elapsed_time(r[3]) for r in rec)
+        tot_fl = sum(r[1] for r in rec)
+        if args.detail and rank == 0:
+            agg = {}
+            for tag, f, s, e, shp in rec:
+                d = agg.setdefault((tag, shp), [0, 0.0, 0.0])
+                d[0] += 1
+                d[1] += f
+                d[2] += s.elapsed_time(e)
+            for (tag, shp), (cnt, f, ms) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
+                print(f"[detail] {tag:10s} {str(shp):42s} x{cnt:3d} {ms:8.2f} ms {f / (ms * 1e-3) / 1e12:7.1f} TF/s",
+                      file=sys.stderr)
         by = {}
-        for tag, f, s, e in rec:
+        for tag, f, s, e, _ in rec:
             d = by.setdefault(tag, [0, 0.0, 0.0])
             d[0] += 1
             d[1] += f

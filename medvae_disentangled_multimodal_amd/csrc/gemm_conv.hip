@@ -3,6 +3,11 @@
 
 using namespace mvae;
 
+static bool kperm_enabled() {  // MVAE_NO_KPERM=1: reference K order (A/B experiments)
+  static const bool on = getenv("MVAE_NO_KPERM") == nullptr;
+  return on;
+}
+
 extern "C" {
 
 // Implicit-GEMM convolution over NHWC activations and KRSC ([Cout][R][S][Cin]) weights.
@@ -43,6 +48,8 @@ int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const fl
     a.a_bytes = (unsigned)(in_img * n); a.b_bytes = (unsigned)wbytes;
     a.c_bytes = (unsigned)(out_img * n); a.r_bytes = a.c_bytes;
     a.H = h; a.W = wd; a.Cx = cin; a.Ho = ho; a.Wo = wo; a.R = kh; a.S = kw;
+    a.perm_rs = (v && cin % BK == 0 && kh * kw > 1 && kperm_enabled()) ? kh * kw : 1;
+    set_gather_magic(a);
     a.stride = stride; a.stride_shift = shift; a.pad_t = pad_t; a.pad_l = pad_l;
     const int cfg = choose_tile(a, v, false);
     if (mode == 0) {

@@ -40,6 +40,23 @@ enum { A_ROWK = 0, A_COLM = 1, A_CONV_FWD = 2, A_CONV_UPS = 3, A_CONV_DGRAD = 4 
 enum { B_ROWK = 0, B_COLN = 1, B_WGRAD_FWD = 2, B_WGRAD_UPS = 3 };
 enum { MODE_FWD = 0, MODE_UPS = 1, MODE_DGRAD = 2 };
 
+constexpr int BK = 32;
+
+// Exact division by a runtime constant d for 0 <= n < 2^31 (Granlund-Montgomery, N = 31):
+// q = (n * m) >> (31 + l), l = ceil(log2 d), m = floor(2^(31+l) / d) + 1 (< 2^32).
+struct Magic {
+  unsigned m;
+  int sh;
+};
+inline Magic make_magic(int d) {
+  int l = 0;
+  while ((1LL << l) < d) ++l;
+  return Magic{(unsigned)(((1ULL << (31 + l)) / (unsigned long long)d) + 1ULL), 31 + l};
+}
+__device__ __forceinline__ int mdiv(int n, Magic mg) {
+  return (int)(((unsigned long long)(unsigned)n * mg.m) >> mg.sh);
+}
+
 struct GemmArgs {
   int M, N, K;
   int batch, splits, k_split;  // split z covers K range [z*k_split, min(K,(z+1)*k_split))
@@ -55,9 +72,32 @@ struct GemmArgs {
   // gather geometry: source X is [nb][H][W][Cx]; output pixels are [nb][Ho][Wo]
   int H, W, Cx, Ho, Wo, R, S, stride, stride_shift, pad_t, pad_l;
   int tiles_m, tiles_n;
+  Magic mg_cx, mg_s, mg_hw, mg_wo;  // divisions by Cx, S, Ho*Wo, Wo (gather index decomposition)
+  // conv K-order permutation (perm_rs = R*S, 1 = identity; needs Cx % 32 == 0): K-tile t covers channel
+  // chunk t / RS of tap t % RS, so while the 32 CUs of an XCD sweep K their gathered input
+  // footprint is one 32-channel slice of the image rows (L2-resident) instead of all channels of a
+  // tap (which overflows L2 and re-fetches the input once per tap)
+  int perm_rs = 1;
+  Magic mg_rs = {0x80000001u, 31};  // make_magic(1)
 };
 
-constexpr int BK = 32;
+// column of the reference K order where (permuted) K-tile starting at k begins; k % 32 == 0
+// (branch-free: perm_rs = 1 gives chunk = t, tap = 0, i.e. the identity)
+__device__ __forceinline__ int kperm(const GemmArgs& a, int k) {
+  const int t = k >> 5;
+  const int chunk = mdiv(t, a.mg_rs);
+  return (t - chunk * a.perm_rs) * a.Cx + chunk * BK;
+}
+
+inline void set_gather_magic(GemmArgs& a) {
+  a.perm_rs = std::max(1, a.perm_rs);
+  a.mg_rs = make_magic(a.perm_rs);
+  a.mg_cx = make_magic(a.Cx);
+  a.mg_s = make_magic(a.S);
+  a.mg_hw = make_magic(a.Ho * a.Wo);
+  a.mg_wo = make_magic(a.Wo);
+}
+
 constexpr unsigned OOB = 0xFFFFFFF0u;  // byte offset beyond every descriptor range
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
@@ -126,9 +166,27 @@ __device__ __forceinline__ bool tap_src(const GemmArgs& a, int oh, int ow, int r
   }
 }
 
+// Row of the ROW-image store pattern for thread tid: a wave stages 8 rows x 32 k (8 lanes per row).
+// ds_write_b64 serves 16 lanes (2 rows) per LDS cycle; with the 80-B row pitch rows r and r+1 overlap
+// in 4 banks, rows r and r+4 are 16 banks apart -- so lane groups pair rows (0,4),(1,5),(2,6),(3,7).
+__device__ __forceinline__ int row_of_tid(int tid) {
+#ifdef MVAE_NO_ROW_SWIZZLE
+  return tid >> 3;
+#else
+  const int g = (tid >> 3) & 7;
+  return (tid >> 6) * 8 + ((g >> 1) | ((g & 1) << 2));
+#endif
+}
+
 // ------------------------------------------------------------------------------------------
-// operand loaders: init(args, base, row0, k_begin, tid); load(args) (the tile at the current k);
-// advance(args) (k += 32); store(img) into the operand's LDS image.
+// operand loaders. Each thread stages NS float4 "slots" of a BK-deep K-tile:
+//   init(args, base, row0, k_begin, tid)
+//   prep(args)          per-tile index math for the tile at the current k (before load_slot)
+//   load_slot(args, i)  issue the global load of slot i
+//   store_slot(img, i)  split slot i into hi/lo bf16 and write it into the operand's LDS image
+//   advance()           k += BK
+// load() / store() run every slot. Slots let the main loop interleave the staging of tile t+1 with
+// the MFMAs of tile t, one slot at a time.
 // ------------------------------------------------------------------------------------------
 
 // ROW image, source element (row, k) at P[row*ld + k]
@@ -136,37 +194,42 @@ template <int ROWS, int VEC, int NT, bool IS_A>
 struct LoadRowK {
   static constexpr bool COL = false;
   static constexpr int RP = NT / 8;     // rows per pass (8 float4 per 32-wide row)
-  static constexpr int NR = ROWS / RP;  // rows per thread
+  static constexpr int NS = ROWS / RP;  // rows per thread
   __amdgpu_buffer_rsrc_t rs;
   unsigned ld;
-  int rows, K, row0, k, kc, r0;
-  float4 v[NR];
+  int rows, K, row0, k, kc, r0, kk;
+  float4 v[NS];
   __device__ void init(const GemmArgs& a, const float* p, int row0_, int kb, int tid) {
     rs = make_rsrc(p, IS_A ? a.a_bytes : a.b_bytes);
     ld = (unsigned)(IS_A ? a.lda : a.ldb); rows = IS_A ? a.M : a.N; K = a.K;
-    row0 = row0_; k = kb; kc = tid & 7; r0 = tid >> 3;
+    row0 = row0_; k = kb; kc = tid & 7; r0 = row_of_tid(tid);
   }
-  __device__ void load(const GemmArgs&) {
-    const int kk = k + kc * 4;
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int row = row0 + r0 + RP * i;
-      const unsigned base = ((unsigned)row * ld + (unsigned)kk) * 4u;
-      const bool rv = row < rows;
-      if (VEC == 4) {
-        v[i] = bload4(rs, (rv && kk < K) ? base : OOB);
-      } else {
-        v[i].x = bload1(rs, (rv && kk + 0 < K) ? base : OOB);
-        v[i].y = bload1(rs, (rv && kk + 1 < K) ? base + 4 : OOB);
-        v[i].z = bload1(rs, (rv && kk + 2 < K) ? base + 8 : OOB);
-        v[i].w = bload1(rs, (rv && kk + 3 < K) ? base + 12 : OOB);
-      }
+  __device__ void prep(const GemmArgs& a) { kk = kperm(a, k) + kc * 4; }
+  __device__ void load_slot(const GemmArgs&, int i) {
+    const int row = row0 + r0 + RP * i;
+    const unsigned base = ((unsigned)row * ld + (unsigned)kk) * 4u;
+    const bool rv = row < rows;
+    if (VEC == 4) {
+      v[i] = bload4(rs, (rv && kk < K) ? base : OOB);
+    } else {
+      v[i].x = bload1(rs, (rv && kk + 0 < K) ? base : OOB);
+      v[i].y = bload1(rs, (rv && kk + 1 < K) ? base + 4 : OOB);
+      v[i].z = bload1(rs, (rv && kk + 2 < K) ? base + 8 : OOB);
+      v[i].w = bload1(rs, (rv && kk + 3 < K) ? base + 12 : OOB);
     }
   }
-  __device__ void advance(const GemmArgs&) { k += BK; }
+  __device__ void store_slot(__bf16* img, int i) {
+    st_split(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+  }
+  __device__ void advance() { k += BK; }
+  __device__ void load(const GemmArgs& a) {
+    prep(a);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) load_slot(a, i);
+  }
   __device__ void store(__bf16* img) {
 #pragma unroll
-    for (int i = 0; i < NR; ++i) st_split(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+    for (int i = 0; i < NS; ++i) store_slot(img, i);
   }
 };
 
@@ -175,75 +238,77 @@ template <int ROWS, int VEC, int NT, int MODE>
 struct LoadConvA {
   static constexpr bool COL = false;
   static constexpr int RP = NT / 8;
-  static constexpr int NR = ROWS / RP;
+  static constexpr int NS = ROWS / RP;
+  static constexpr int NE = VEC == 4 ? 1 : 4;  // (c, r, s) decompositions per thread
   __amdgpu_buffer_rsrc_t rs;
   int kc, r0, k;
-  int cc[4], rr[4], ss[4];  // (c, r, s) of element kc*4+e of the current k-tile
-  unsigned base[NR];
-  int oh[NR], ow[NR];
-  bool mv[NR];
-  float4 v[NR];
+  unsigned base[NS];
+  int oh[NS], ow[NS];
+  bool mv[NS];
+  int cc[NE], rr[NE], ss[NE];
+  bool kv[NE];
+  float4 v[NS];
   __device__ void init(const GemmArgs& a, const float* x, int row0, int kb, int tid) {
     rs = make_rsrc(x, a.a_bytes);
-    kc = tid & 7; r0 = tid >> 3; k = kb;
-    const int hw = a.Ho * a.Wo;
+    kc = tid & 7; r0 = row_of_tid(tid); k = kb;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
+    for (int i = 0; i < NS; ++i) {
       const int m = row0 + r0 + RP * i;
       mv[i] = m < a.M;
       const int mm = mv[i] ? m : 0;
-      const int b = mm / hw;
-      const int rem = mm - b * hw;
-      oh[i] = rem / a.Wo;
+      const int b = mdiv(mm, a.mg_hw);
+      const int rem = mm - b * (a.Ho * a.Wo);
+      oh[i] = mdiv(rem, a.mg_wo);
       ow[i] = rem - oh[i] * a.Wo;
       base[i] = (unsigned)b * (unsigned)(a.H * a.W);
     }
-    const int nE = VEC == 4 ? 1 : 4;
-    for (int e = 0; e < nE; ++e) {
-      const int kk = k + kc * 4 + e;
-      const int tap = kk / a.Cx;
+  }
+  // (c, r, s) of this thread's k columns, by exact multiply-shift division: branch-free, so the
+  // steady-state loop stays one basic block
+  __device__ void prep(const GemmArgs& a) {
+    const int kp = kperm(a, k);
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int kk = kp + kc * 4 + e;
+      const int tap = mdiv(kk, a.mg_cx);
       cc[e] = kk - tap * a.Cx;
-      rr[e] = tap / a.S;
+      rr[e] = mdiv(tap, a.mg_s);
       ss[e] = tap - rr[e] * a.S;
+      kv[e] = kk < a.K;
     }
   }
-  __device__ void advance(const GemmArgs& a) {
-    k += BK;
-    const int nE = VEC == 4 ? 1 : 4;
-    for (int e = 0; e < nE; ++e) {
-      cc[e] += BK;
-      while (cc[e] >= a.Cx) {
-        cc[e] -= a.Cx;
-        if (++ss[e] == a.S) { ss[e] = 0; ++rr[e]; }
-      }
-    }
-  }
-  __device__ void load(const GemmArgs& a) {
+  __device__ void load_slot(const GemmArgs& a, int i) {
+    if (VEC == 4) {
+      int ih = 0, iw = 0;
+      const bool tv = tap_src<MODE>(a, oh[i], ow[i], rr[0], ss[0], ih, iw);
+      const bool ok = mv[i] & kv[0] & tv;
+      const unsigned off = ((base[i] + (unsigned)(ih * a.W + iw)) * (unsigned)a.Cx + (unsigned)cc[0]) * 4u;
+      v[i] = bload4(rs, ok ? off : OOB);
+    } else {
+      float t[4];
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      if (VEC == 4) {
+      for (int e = 0; e < 4; ++e) {
         int ih = 0, iw = 0;
-        const bool tv = tap_src<MODE>(a, oh[i], ow[i], rr[0], ss[0], ih, iw);
-        const bool ok = mv[i] & (k + kc * 4 < a.K) & tv;
-        const unsigned off = ((base[i] + (unsigned)(ih * a.W + iw)) * (unsigned)a.Cx + (unsigned)cc[0]) * 4u;
-        v[i] = bload4(rs, ok ? off : OOB);
-      } else {
-        float t[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          int ih = 0, iw = 0;
-          const bool tv = tap_src<MODE>(a, oh[i], ow[i], rr[e], ss[e], ih, iw);
-          const bool ok = mv[i] & (k + kc * 4 + e < a.K) & tv;
-          const unsigned off = ((base[i] + (unsigned)(ih * a.W + iw)) * (unsigned)a.Cx + (unsigned)cc[e]) * 4u;
-          t[e] = bload1(rs, ok ? off : OOB);
-        }
-        v[i] = float4{t[0], t[1], t[2], t[3]};
+        const bool tv = tap_src<MODE>(a, oh[i], ow[i], rr[e], ss[e], ih, iw);
+        const bool ok = mv[i] & kv[e] & tv;
+        const unsigned off = ((base[i] + (unsigned)(ih * a.W + iw)) * (unsigned)a.Cx + (unsigned)cc[e]) * 4u;
+        t[e] = bload1(rs, ok ? off : OOB);
       }
+      v[i] = float4{t[0], t[1], t[2], t[3]};
     }
+  }
+  __device__ void store_slot(__bf16* img, int i) {
+    st_split(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+  }
+  __device__ void advance() { k += BK; }
+  __device__ void load(const GemmArgs& a) {
+    prep(a);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) load_slot(a, i);
   }
   __device__ void store(__bf16* img) {
 #pragma unroll
-    for (int i = 0; i < NR; ++i) st_split(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+    for (int i = 0; i < NS; ++i) store_slot(img, i);
   }
 };
 
@@ -252,48 +317,51 @@ template <int ROWS, int VEC, int NT, bool IS_A>
 struct LoadColK {
   static constexpr bool COL = true;
   static constexpr int C4 = ROWS / 4;                 // float4 per k-row
-  static constexpr int NF = (BK * C4 + NT - 1) / NT;  // float4 per thread
+  static constexpr int NS = (BK * C4 + NT - 1) / NT;  // float4 per thread
   __amdgpu_buffer_rsrc_t rs;
   unsigned ld;
   int rows, K, row0, k, c4, kr;
-  float4 v[NF];
+  float4 v[NS];
   float bs[4] = {0.f, 0.f, 0.f, 0.f};  // A side: running row sums of every staged element
   __device__ void init(const GemmArgs& a, const float* p, int row0_, int kb, int tid) {
     rs = make_rsrc(p, IS_A ? a.a_bytes : a.b_bytes);
     ld = (unsigned)(IS_A ? a.lda : a.ldb); rows = IS_A ? a.M : a.N; K = a.K;
     row0 = row0_; k = kb; c4 = tid % C4; kr = tid / C4;
   }
-  __device__ void load(const GemmArgs&) {
+  __device__ void prep(const GemmArgs&) {}
+  __device__ void load_slot(const GemmArgs&, int i) {
     const int col = row0 + c4 * 4;
-#pragma unroll
-    for (int i = 0; i < NF; ++i) {
-      const int krow = kr + i * (NT / C4);
-      const int kk = k + krow;
-      const bool kv = krow < BK && kk < K;
-      const unsigned base = ((unsigned)kk * ld + (unsigned)col) * 4u;
-      if (VEC == 4) {
-        v[i] = bload4(rs, (kv && col < rows) ? base : OOB);
-      } else {
-        v[i].x = bload1(rs, (kv && col + 0 < rows) ? base : OOB);
-        v[i].y = bload1(rs, (kv && col + 1 < rows) ? base + 4 : OOB);
-        v[i].z = bload1(rs, (kv && col + 2 < rows) ? base + 8 : OOB);
-        v[i].w = bload1(rs, (kv && col + 3 < rows) ? base + 12 : OOB);
+    const int krow = kr + i * (NT / C4);
+    const int kk = k + krow;
+    const bool kv = krow < BK && kk < K;
+    const unsigned base = ((unsigned)kk * ld + (unsigned)col) * 4u;
+    if (VEC == 4) {
+      v[i] = bload4(rs, (kv && col < rows) ? base : OOB);
+    } else {
+      v[i].x = bload1(rs, (kv && col + 0 < rows) ? base : OOB);
+      v[i].y = bload1(rs, (kv && col + 1 < rows) ? base + 4 : OOB);
+      v[i].z = bload1(rs, (kv && col + 2 < rows) ? base + 8 : OOB);
+      v[i].w = bload1(rs, (kv && col + 3 < rows) ? base + 12 : OOB);
+    }
+  }
+  __device__ void store_slot(__bf16* img, int i) {
+    constexpr int P_ = Img<ROWS, true>::PITCH;
+    const int krow = kr + i * (NT / C4);
+    if (krow < BK) {
+      st_split(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+      if constexpr (IS_A) {
+        bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
       }
     }
   }
-  __device__ void advance(const GemmArgs&) { k += BK; }
-  __device__ void store(__bf16* img) {
-    constexpr int P_ = Img<ROWS, true>::PITCH;
+  __device__ void advance() { k += BK; }
+  __device__ void load(const GemmArgs& a) {
 #pragma unroll
-    for (int i = 0; i < NF; ++i) {
-      const int krow = kr + i * (NT / C4);
-      if (krow < BK) {
-        st_split(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
-        if constexpr (IS_A) {
-          bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
-        }
-      }
-    }
+    for (int i = 0; i < NS; ++i) load_slot(a, i);
+  }
+  __device__ void store(__bf16* img) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) store_slot(img, i);
   }
 };
 
@@ -303,13 +371,13 @@ template <int ROWS, int VEC, int NT, int MODE>
 struct LoadWgradX {
   static constexpr bool COL = true;
   static constexpr int C4 = ROWS / 4;
-  static constexpr int NF = (BK * C4 + NT - 1) / NT;
+  static constexpr int NS = (BK * C4 + NT - 1) / NT;
   __amdgpu_buffer_rsrc_t rs;
-  int c4, kr, k;
+  int c4, kr, krw, k;
   int cc[4], rr[4], ss[4];
   bool nv[4];
-  int pb[NF], poh[NF], pow_[NF];  // pixel decomposition of this thread's k-rows
-  float4 v[NF];
+  int pb[NS], poh[NS], pow_[NS];  // pixel decomposition of this thread's k-rows (current tile)
+  float4 v[NS];
   __device__ void init(const GemmArgs& a, const float* x, int row0, int kb, int tid) {
     rs = make_rsrc(x, a.b_bytes);
     k = kb; c4 = tid % C4; kr = tid / C4;
@@ -322,63 +390,57 @@ struct LoadWgradX {
       rr[e] = tap / a.S;
       ss[e] = tap - rr[e] * a.S;
     }
-    const int hw = a.Ho * a.Wo;
     // with 64 column groups the k-row is wave-uniform: keep the pixel walk in scalar registers
-    const int krw = (C4 % 64 == 0) ? __builtin_amdgcn_readfirstlane(kr) : kr;
+    krw = (C4 % 64 == 0) ? __builtin_amdgcn_readfirstlane(kr) : kr;
+  }
+  __device__ void prep(const GemmArgs& a) {
 #pragma unroll
-    for (int i = 0; i < NF; ++i) {
-      const int p = kb + krw + i * (NT / C4);
-      pb[i] = p / hw;
-      const int rem = p - pb[i] * hw;
-      poh[i] = rem / a.Wo;
+    for (int i = 0; i < NS; ++i) {
+      const int p = min(k + krw + i * (NT / C4), a.K - 1);  // clamp: rows past K are masked
+      pb[i] = mdiv(p, a.mg_hw);
+      const int rem = p - pb[i] * (a.Ho * a.Wo);
+      poh[i] = mdiv(rem, a.mg_wo);
       pow_[i] = rem - poh[i] * a.Wo;
     }
   }
-  __device__ void advance(const GemmArgs& a) {
-    k += BK;
+  __device__ void load_slot(const GemmArgs& a, int i) {
+    const unsigned img = (unsigned)(a.H * a.W);
+    const int krow = kr + i * (NT / C4);
+    const bool kv = krow < BK && (k + krow < a.K);
+    if (VEC == 4) {
+      int ih = 0, iw = 0;
+      const bool tv = tap_src<MODE>(a, poh[i], pow_[i], rr[0], ss[0], ih, iw);
+      const bool ok = kv & nv[0] & tv;
+      const unsigned off = (((unsigned)pb[i] * img + (unsigned)(ih * a.W + iw)) * (unsigned)a.Cx + (unsigned)cc[0]) * 4u;
+      v[i] = bload4(rs, ok ? off : OOB);
+    } else {
+      float t[4];
 #pragma unroll
-    for (int i = 0; i < NF; ++i) {
-      pow_[i] += BK;
-      while (pow_[i] >= a.Wo) {
-        pow_[i] -= a.Wo;
-        if (++poh[i] == a.Ho) { poh[i] = 0; ++pb[i]; }
+      for (int e = 0; e < 4; ++e) {
+        int ih = 0, iw = 0;
+        const bool tv = tap_src<MODE>(a, poh[i], pow_[i], rr[e], ss[e], ih, iw);
+        const bool ok = kv & nv[e] & tv;
+        const unsigned off =
+            (((unsigned)pb[i] * img + (unsigned)(ih * a.W + iw)) * (unsigned)a.Cx + (unsigned)cc[e]) * 4u;
+        t[e] = bload1(rs, ok ? off : OOB);
       }
+      v[i] = float4{t[0], t[1], t[2], t[3]};
     }
   }
+  __device__ void store_slot(__bf16* img, int i) {
+    constexpr int P_ = Img<ROWS, true>::PITCH;
+    const int krow = kr + i * (NT / C4);
+    if (krow < BK) st_split(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+  }
+  __device__ void advance() { k += BK; }
   __device__ void load(const GemmArgs& a) {
-    const unsigned img = (unsigned)(a.H * a.W);
+    prep(a);
 #pragma unroll
-    for (int i = 0; i < NF; ++i) {
-      const int krow = kr + i * (NT / C4);
-      const bool kv = krow < BK && (k + krow < a.K);
-      if (VEC == 4) {
-        int ih = 0, iw = 0;
-        const bool tv = tap_src<MODE>(a, poh[i], pow_[i], rr[0], ss[0], ih, iw);
-        const bool ok = kv & nv[0] & tv;
-        const unsigned off = (((unsigned)pb[i] * img + (unsigned)(ih * a.W + iw)) * (unsigned)a.Cx + (unsigned)cc[0]) * 4u;
-        v[i] = bload4(rs, ok ? off : OOB);
-      } else {
-        float t[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          int ih = 0, iw = 0;
-          const bool tv = tap_src<MODE>(a, poh[i], pow_[i], rr[e], ss[e], ih, iw);
-          const bool ok = kv & nv[e] & tv;
-          const unsigned off =
-              (((unsigned)pb[i] * img + (unsigned)(ih * a.W + iw)) * (unsigned)a.Cx + (unsigned)cc[e]) * 4u;
-          t[e] = bload1(rs, ok ? off : OOB);
-        }
-        v[i] = float4{t[0], t[1], t[2], t[3]};
-      }
-    }
+    for (int i = 0; i < NS; ++i) load_slot(a, i);
   }
   __device__ void store(__bf16* img) {
-    constexpr int P_ = Img<ROWS, true>::PITCH;
 #pragma unroll
-    for (int i = 0; i < NF; ++i) {
-      const int krow = kr + i * (NT / C4);
-      if (krow < BK) st_split(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
-    }
+    for (int i = 0; i < NS; ++i) store_slot(img, i);
   }
 };
 
@@ -414,16 +476,20 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   const int wm = wid / WGN, wn = wid - wm * WGN;
   // XCD-aware remap (bijective): blocks b and b+8 share an XCD, so hand each XCD a contiguous run
   // of tiles (row-major over (m, n): neighbours share A rows and the same weight panel).
-  const int nwg = a.tiles_m * a.tiles_n;
-  const int orig = blockIdx.x;
-  int tile = orig;
+  // The remap runs over the whole grid (tiles x batch x splits, split-major) since workgroups are
+  // dealt to XCDs round-robin by their linear id: the blocks of one split (same K range) share an L2.
+  const int ntile = a.tiles_m * a.tiles_n;
+  const int nwg = ntile * gridDim.z;
+  const int orig = blockIdx.x + ntile * blockIdx.z;
+  int lin = orig;
   if (nwg >= 16) {
     const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
   }
+  const int z = lin / ntile;
+  const int tile = lin - z * ntile;
   const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int z = blockIdx.z;
   const int bidx = z / a.splits, split = z - bidx * a.splits;
   const int kb = split * a.k_split;
   const int ke = min(a.K, kb + a.k_split);
@@ -450,8 +516,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
     lb.store(lds + IA::SIZE);
   }
   if (nt > 1) {
-    la.advance(a);
-    lb.advance(a);
+    la.advance();
+    lb.advance();
     la.load(a);
     lb.load(a);
   }
@@ -485,28 +551,87 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
       }
     }
   };
-  // steady state: branch-free body (one scheduling region), so the split/ds_write of tile t+1 and
-  // the address math of tile t+2 can interleave with the MFMAs of tile t
   int t = 0;
+#ifndef MVAE_BLOCK_STAGING
+  // steady state, software-pipelined by hand: the K-tile's 2*TM MFMA steps (one 32-row A fragment
+  // x TN B fragments x 3 split products each) each carry a share of the staging work -- split +
+  // LDS write of one slot of tile t+1, then the global load of the same slot of tile t+2 -- and
+  // prefetch the next step's A fragment. sched_barrier pins that order (the scheduler would
+  // otherwise hoist all staging VALU into one block ahead of the MFMAs, idling the MFMA pipe).
+  constexpr int STEPS = 2 * TM;
+  constexpr int NSL = LA::NS + LB::NS;
   for (; t + 2 < nt; ++t) {
+    __bf16* nb = lds + ((t & 1) ^ 1) * BUF;
+    const __bf16* Ai = lds + (t & 1) * BUF;
+    const __bf16* Bi = Ai + IA::SIZE;
+    la.advance();
+    lb.advance();
+    la.prep(a);
+    lb.prep(a);
+    bf16x8 bh[TN], bl[TN], ah[2], al[2];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bh[j] = read_frag<BN, LB::COL>(Bi, brow + j * 32, 0, lane);
+      bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, 0, lane);
+    }
+    ah[0] = read_frag<BM, LA::COL>(Ai, arow, 0, lane);
+    al[0] = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow, 0, lane);
+#pragma unroll
+    for (int st = 0; st < STEPS; ++st) {
+      const int i = st % TM, cur = st & 1;
+      if (st + 1 < STEPS) {
+        const int ks1 = (st + 1) / TM, i1 = (st + 1) % TM;
+        ah[cur ^ 1] = read_frag<BM, LA::COL>(Ai, arow + i1 * 32, ks1, lane);
+        al[cur ^ 1] = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow + i1 * 32, ks1, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[cur], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cur], bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cur], bh[j], acc[i][j], 0, 0, 0);
+      }
+      if (st == TM - 1) {  // B fragments of the second k-half
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          bh[j] = read_frag<BN, LB::COL>(Bi, brow + j * 32, 1, lane);
+          bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, 1, lane);
+        }
+      }
+#pragma unroll
+      for (int q = st * NSL / STEPS; q < (st + 1) * NSL / STEPS; ++q) {
+        if (q < LA::NS) {
+#ifndef MVAE_EXP_NOSTORE
+          la.store_slot(nb, q);
+#endif
+#ifndef MVAE_EXP_NOLOAD
+          la.load_slot(a, q);
+#endif
+        } else {
+#ifndef MVAE_EXP_NOSTORE
+          lb.store_slot(nb + IA::SIZE, q - LA::NS);
+#endif
+#ifndef MVAE_EXP_NOLOAD
+          lb.load_slot(a, q - LA::NS);
+#endif
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+  }
+#else
+  for (; t + 2 < nt; ++t) {  // block staging: all of tile t+1's staging, then tile t's MFMAs
     __bf16* nb = lds + ((t & 1) ^ 1) * BUF;
     la.store(nb);
     lb.store(nb + IA::SIZE);
-    la.advance(a);
-    lb.advance(a);
+    la.advance();
+    lb.advance();
     la.load(a);
     lb.load(a);
     compute(lds + (t & 1) * BUF);
-#ifdef MVAE_SCHED_INTERLEAVE
-#pragma unroll
-    for (int q = 0; q < 6 * TM * TN; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // 3 VALU
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
-    }
-#endif
     __syncthreads();
   }
+#endif
   if (t + 1 < nt) {  // last staged tile: write it, nothing left to load
     __bf16* nb = lds + ((t & 1) ^ 1) * BUF;
     la.store(nb);
@@ -632,7 +757,11 @@ void launch_cfg(GemmArgs& a, hipStream_t st) {
   constexpr int BM = CFG == T256x256 || CFG == T256x128 ? 256 : CFG == T64x64 ? 64 : 128;
   constexpr int BN = CFG == T256x256 || CFG == T128x256 ? 256 : CFG == T64x64 ? 64 : 128;
   constexpr int WGM = CFG == T256x128 ? 4 : 2;
+#ifdef MVAE_W4
+  constexpr int WGN = CFG == T128x256 ? 4 : 2;  // 256x256 on 4 waves (128x128 per wave)
+#else
   constexpr int WGN = (CFG == T256x256 || CFG == T128x256) ? 4 : 2;
+#endif
   a.tiles_m = cdiv(a.M, BM);
   a.tiles_n = cdiv(a.N, BN);
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splits);

@@ -46,6 +46,7 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
     a.a_bytes = (unsigned)(out_img * n); a.b_bytes = (unsigned)(in_img * n);
     a.c_bytes = (unsigned)((long long)a.M * a.N * 4);
     a.H = h; a.W = wd; a.Cx = cin; a.Ho = ho; a.Wo = wo; a.R = kh; a.S = kw;
+    set_gather_magic(a);
     a.stride = stride; a.pad_t = pad_t; a.pad_l = pad_l;
     const int cfg = choose_tile(a, va && vb, workspace != nullptr);
     const size_t bias_bytes = dbias ? ((size_t)64 * a.M * sizeof(float) + 256) : 0;

@@ -63,15 +63,16 @@ class _Arena:
 ARENA = _Arena()
 
 # Optional live kernel timing (bench.py): when PROFILE is a list, every implicit-GEMM launch is
-# bracketed by HIP events on the current stream and recorded as (tag, algorithmic_flops, start, end).
+# bracketed by HIP events on the current stream and recorded as
+# (tag, algorithmic_flops, start, end, shape) -- shape = the launch's problem tuple.
 PROFILE = None
 
 
 class _timed:
-    __slots__ = ("tag", "flops", "s")
+    __slots__ = ("tag", "flops", "s", "shape")
 
-    def __init__(self, tag: str, flops: float):
-        self.tag, self.flops = tag, flops
+    def __init__(self, tag: str, flops: float, shape=None):
+        self.tag, self.flops, self.shape = tag, flops, shape
 
     def __enter__(self):
         if PROFILE is not None:
@@ -83,7 +84,7 @@ class _timed:
         if PROFILE is not None:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
-            PROFILE.append((self.tag, self.flops, self.s, e))
+            PROFILE.append((self.tag, self.flops, self.s, e, self.shape))
         return False
 
 
@@ -127,7 +128,7 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom):
     co = w.shape[0]
     ho, wo = g.out_hw(h, wd)
     y = torch.empty((n, co, ho, wo), device=x.device, dtype=torch.float32, memory_format=CL)
-    with _timed("conv_fwd", 2.0 * n * ho * wo * co * c * g.kh * g.kw):
+    with _timed("conv_fwd", 2.0 * n * ho * wo * co * c * g.kh * g.kw, (n, c, h, wd, co, g.kh, g.stride, g.upsample)):
         _conv_fwd_launch(x, w, b, res, y, g, n, c, h, wd, co, ho, wo)
     return y
 
@@ -152,7 +153,7 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom):
     flops = 2.0 * n * ho * wo * co * c * g.kh * g.kw  # algorithmic (reference) count
     if g.pointwise:
         # dx[m][c] = sum_n dy[m][n] W[n][c]  (W stored [K=cout][N=cin])
-        with _timed("conv_dgrad", flops):
+        with _timed("conv_dgrad", flops, (n, c, h, wd, co, g.kh, g.stride, g.upsample)):
             _lib.call("mvae_gemm_strided_batched", 0, 0, n * h * wd, c, co, 1.0, dy.data_ptr(), co, 0, w.data_ptr(), c,
                       0, 0.0, dx.data_ptr(), c, 0, 1, None, None, 0, 0, None, 0, st)
         return dx
@@ -160,13 +161,13 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom):
         wt = ARENA.get("wt", c * 16 * co * 4, dy.device)
         _lib.call("mvae_conv_weight_upsample_dgrad", w.data_ptr(), wt.data_ptr(), co, c, st)
         # dX = stride-2, pad-1 4x4 conv of dY with the tap-summed kernel
-        with _timed("conv_dgrad", flops):
+        with _timed("conv_dgrad", flops, (n, c, h, wd, co, g.kh, g.stride, g.upsample)):
             _lib.call("mvae_conv2d_nhwc", dy.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
                       4, 4, 2, 1, 1, h, wd, 0, st)
         return dx
     wt = ARENA.get("wt", c * g.kh * g.kw * co * 4, dy.device)
     _lib.call("mvae_conv_weight_transpose", w.data_ptr(), wt.data_ptr(), co, g.kh, g.kw, c, st)
-    with _timed("conv_dgrad", flops):
+    with _timed("conv_dgrad", flops, (n, c, h, wd, co, g.kh, g.stride, g.upsample)):
         _lib.call("mvae_conv2d_nhwc", dy.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
                   g.kh, g.kw, g.stride, g.pad_t, g.pad_l, h, wd, 2, st)
     return dx
@@ -178,7 +179,7 @@ def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None):
     n, c, h, wd = x.shape
     co = dy.shape[1]
     _, _, ho, wo = dy.shape
-    with _timed("conv_wgrad", 2.0 * n * ho * wo * co * c * g.kh * g.kw):
+    with _timed("conv_wgrad", 2.0 * n * ho * wo * co * c * g.kh * g.kw, (n, c, h, wd, co, g.kh, g.stride, g.upsample)):
         return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db)
 
 
@@ -311,7 +312,7 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0)
 # attention core: softmax(q k^T * C^-1/2) v over the h*w tokens of each image
 # ------------------------------------------------------------------------------------------
 def _gemm(ta, tb, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, st, residual=None):
-    with _timed("attn_gemm", 2.0 * m * n * k * batch):
+    with _timed("attn_gemm", 2.0 * m * n * k * batch, (m, n, k, batch)):
         _lib.call("mvae_gemm_strided_batched", ta, tb, m, n, k, float(alpha), A.data_ptr(), lda, sA, B.data_ptr(), ldb,
                   sB, float(beta), C.data_ptr(), ldc, sC, batch, None, _ptr(residual), ldc, sC, None, 0, st)
 

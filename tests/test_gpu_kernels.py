@@ -46,6 +46,12 @@ CONV_CASES = [
     (2, 64, 3, 16, 16, 3, 1, (1, 1, 1, 1), False),    # conv_out, cout = 3
     (2, 32, 1, 12, 12, 3, 1, (1, 1, 1, 1), False),    # conv_out, cout = 1
     (4, 128, 64, 8, 8, 1, 1, (0, 0, 0, 0), False),    # nin_shortcut 1x1
+    (2, 96, 48, 9, 9, 3, 1, (1, 1, 1, 1), False),     # K-permuted order with 3 chunks per tap
+    (2, 48, 96, 9, 9, 3, 1, (1, 1, 1, 1), False),     # Cin % 32 != 0: reference K order
+    # production-size launches: 256x256 / 256x128 tiles, XCD remap, split-K wgrad over many splits
+    (64, 256, 256, 32, 32, 3, 1, (1, 1, 1, 1), False),
+    (64, 256, 128, 16, 16, 3, 1, (1, 1, 1, 1), True),  # Upsample 16 -> 32
+    (64, 128, 128, 64, 64, 3, 2, (0, 0, 1, 1), False),  # Downsample 64 -> 32
 ]
 
 
@@ -80,9 +86,11 @@ def test_conv_fwd_dgrad_wgrad(dev, case):
     yd.mul(torch.linspace(-1, 1, yd.numel(), device=dev).view(yd.shape)).sum().backward()
     assert rel(xd.grad, xr.grad) < CONV_TOL
     assert rel(wd.grad, wr.grad) < CONV_TOL
-    # bias grad = column sum of dY: absolute error relative to the size of dY
-    scale = float(yr.numel()) ** 0.5 + float(br.grad.abs().max())
-    assert float((bd.grad.cpu() - br.grad).abs().max()) < 1e-5 * scale
+    # bias grad = column sum of dY, referenced in float64 (the fp32 CPU conv backward itself drifts
+    # by ~1e-3 relative at 65k pixels); absolute error relative to the size of dY
+    db_ref = torch.linspace(-1, 1, yr.numel()).view(yr.shape).double().sum((0, 2, 3))
+    scale = float(yr.numel()) ** 0.5 + float(db_ref.abs().max())
+    assert float((bd.grad.cpu().double() - db_ref).abs().max()) < 1e-5 * scale
     # flat-buffer path: weight + bias gradients accumulated in place by the fused wgrad kernel
     wm = cl(wt, dev).requires_grad_()
     bm = b.to(dev).requires_grad_()
@@ -92,7 +100,7 @@ def test_conv_fwd_dgrad_wgrad(dev, case):
     ym.mul(torch.linspace(-1, 1, ym.numel(), device=dev).view(ym.shape)).sum().backward()
     assert wm.grad is None and bm.grad is None
     assert rel(wm._mvae_main_grad - 0.5, wr.grad) < CONV_TOL
-    assert float((bm._mvae_main_grad.cpu() - 0.25 - br.grad).abs().max()) < 1e-5 * scale
+    assert float((bm._mvae_main_grad.cpu().double() - 0.25 - db_ref).abs().max()) < 1e-5 * scale
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])

@@ -1,15 +1,15 @@
 #!/bin/bash
-# Collect PMC counter sets (one rocprofv3 pass each, no tracing domains) for one conv pass.
-# usage: tools/pmc.sh <shape> <pass> <outprefix>
+# Collect PMC counter sets (one rocprofv3 pass each, kernel-trace only, no tracing domains) for one
+# conv pass of tools/one_conv.py.   usage: tools/pmc.sh <shape> <pass> <outprefix>
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 SHAPE=$1; PASS=$2; OUT=$3
 SETS=(
- "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA"
- "SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE"
- "TCC_HIT_sum TCC_MISS_sum"
- "FETCH_SIZE"
- "WRITE_SIZE"
+ "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_MFMA"
+ "SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_RD"
+ "TA_TA_BUSY TD_TD_BUSY TCP_PENDING_STALL_CYCLES TCP_TCR_TCP_STALL_CYCLES"
+ "TCC_HIT TCC_MISS TCC_EA0_RDREQ TCC_EA0_RDREQ_DRAM"
+ "TCP_TCC_READ_REQ_LATENCY TCP_TCC_READ_REQ TCP_TOTAL_CACHE_ACCESSES TCP_CACHE_MISS"
 )
 i=0
 for P in "${SETS[@]}"; do
