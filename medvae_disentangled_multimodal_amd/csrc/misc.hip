@@ -10,15 +10,24 @@
 
 namespace mvae {
 
-__global__ void w_transpose_kernel(const float* __restrict__ w, float* __restrict__ wt, int cout, int rs, int cin) {
-  const long long n = (long long)cout * rs * cin;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-    // e indexes the destination [cin][rs][cout]
-    const int o = (int)(e % cout);
-    const long long q = e / cout;
-    const int t = (int)(q % rs);
-    const int c = (int)(q / rs);
-    wt[e] = w[((long long)o * rs + t) * cin + c];
+// per tap t: [cout][cin] (row stride rs*cin) -> [cin][cout] (row stride rs*cout), 64x64 tiles through
+// LDS so both the reads (along cin) and the writes (along cout) are coalesced
+__global__ void __launch_bounds__(256) w_transpose_kernel(const float* __restrict__ w, float* __restrict__ wt,
+                                                          int cout, int rs, int cin) {
+  __shared__ float tile[64][65];
+  const int t = blockIdx.z;
+  const int c0 = blockIdx.x * 64, o0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int o = o0 + ty + 4 * i, c = c0 + tx;
+    tile[ty + 4 * i][tx] = (o < cout && c < cin) ? w[((long long)o * rs + t) * cin + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = c0 + ty + 4 * i, o = o0 + tx;
+    if (o < cout && c < cin) wt[((long long)c * rs + t) * cout + o] = tile[tx][ty + 4 * i];
   }
 }
 
@@ -27,21 +36,33 @@ __device__ __forceinline__ int tap_mask(int t) {
   return t == 0 ? 0b100 : t == 1 ? 0b110 : t == 2 ? 0b011 : 0b001;
 }
 
-__global__ void w_ups_dgrad_kernel(const float* __restrict__ w, float* __restrict__ wt, int cout, int cin) {
-  const long long n = (long long)cin * 16 * cout;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-    const int o = (int)(e % cout);
-    const long long q = e / cout;
-    const int tu = (int)(q % 16);
-    const int c = (int)(q / 16);
-    const int mt = tap_mask(tu >> 2), mu = tap_mask(tu & 3);
+// grid (cin/64, cout/64, 16 effective taps): sum the <= 4 contributing source taps of a 64x64
+// [cout][cin] tile (coalesced along cin), transpose through LDS, write along cout
+__global__ void __launch_bounds__(256) w_ups_dgrad_kernel(const float* __restrict__ w, float* __restrict__ wt,
+                                                          int cout, int cin) {
+  __shared__ float tile[64][65];
+  const int tu = blockIdx.z;
+  const int mt = tap_mask(tu >> 2), mu = tap_mask(tu & 3);
+  const int c0 = blockIdx.x * 64, o0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int o = o0 + ty + 4 * i, c = c0 + tx;
     float s = 0.f;
-    for (int r = 0; r < 3; ++r) {
-      if (!((mt >> r) & 1)) continue;
-      for (int u = 0; u < 3; ++u)
-        if ((mu >> u) & 1) s += w[(((long long)o * 3 + r) * 3 + u) * cin + c];
+    if (o < cout && c < cin) {
+      for (int r = 0; r < 3; ++r) {
+        if (!((mt >> r) & 1)) continue;
+        for (int u = 0; u < 3; ++u)
+          if ((mu >> u) & 1) s += w[(((long long)o * 3 + r) * 3 + u) * cin + c];
+      }
     }
-    wt[e] = s;
+    tile[ty + 4 * i][tx] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = c0 + ty + 4 * i, o = o0 + tx;
+    if (o < cout && c < cin) wt[((long long)c * 16 + tu) * cout + o] = tile[tx][ty + 4 * i];
   }
 }
 
@@ -88,7 +109,7 @@ extern "C" {
 
 int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int kw, int cin, void* stream) {
   if (cout <= 0 || kh <= 0 || kw <= 0 || cin <= 0) { set_error("w_transpose: bad sizes"); return MVAE_EINVAL; }
-  hipLaunchKernelGGL(w_transpose_kernel, dim3(egrid((long long)cout * kh * kw * cin)), dim3(256), 0,
+  hipLaunchKernelGGL(w_transpose_kernel, dim3((cin + 63) / 64, (cout + 63) / 64, kh * kw), dim3(256), 0,
                      (hipStream_t)stream, w, wt, cout, kh * kw, cin);
   return launch_status();
 }
@@ -96,8 +117,8 @@ int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int 
 // wt [cin][4][4][cout] for the dgrad of "nearest-x2 upsample then 3x3 conv"
 int mvae_conv_weight_upsample_dgrad(const float* w, float* wt, int cout, int cin, void* stream) {
   if (cout <= 0 || cin <= 0) { set_error("w_ups: bad sizes"); return MVAE_EINVAL; }
-  hipLaunchKernelGGL(w_ups_dgrad_kernel, dim3(egrid((long long)cin * 16 * cout)), dim3(256), 0, (hipStream_t)stream,
-                     w, wt, cout, cin);
+  hipLaunchKernelGGL(w_ups_dgrad_kernel, dim3((cin + 63) / 64, (cout + 63) / 64, 16), dim3(256), 0,
+                     (hipStream_t)stream, w, wt, cout, cin);
   return launch_status();
 }
 

@@ -185,7 +185,7 @@ def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None):
 
 def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None):
     st = _stream(dy)
-    if g.pointwise:
+    if g.pointwise and db is None:
         m = n * h * wd
         nbytes = _lib.query("mvae_gemm_workspace_bytes", co, c, m, 1)
         ws = ARENA.get("ws", nbytes, dy.device)
