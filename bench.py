@@ -43,6 +43,14 @@ CONFIGS = {
                            modalities=MODALITIES, condition_method="concat"),
                opt=dict(type="adamw", lr=1e-4, weight_decay=1e-5, betas=[0.5, 0.999]), clip=1.0,
                loss=dict(type="vae", recon_loss_type="mse", kl_weight=1.0, recon_weight=1.0)),
+    # BASELINE config 5: config 4 + bf16-mixed + LPIPS(VGG) generator objective (LPIPS + 1e-5 * KL.sum()/B)
+    "c5": dict(cls="ConditionalVAE", res=64, batch=256, precision="bf16-mixed",
+               kwargs=dict(input_channels=3, latent_dim=256, hidden_channels=256, ch_mult=(1, 2, 4, 8),
+                           num_res_blocks=2, attn_resolutions=[16], dropout=0.0, resolution=64,
+                           modalities=MODALITIES, condition_method="concat"),
+               opt=dict(type="adamw", lr=1e-4, weight_decay=1e-5, betas=[0.5, 0.999]), clip=1.0,
+               loss=dict(type="lpips_discriminator", perceptual_factor=1.0, kl_factor=1e-5,
+                         discriminator_iter_start=10000, allow_synthetic_lpips=True, lpips_net="vgg")),
     # BASELINE config 2: path_beta_vae at 28x28x3 with the 3-level ch_mult, bs 256
     "c2": dict(cls="BetaVAE", res=28, batch=256,
                kwargs=dict(input_channels=3, latent_dim=128, hidden_channels=128, ch_mult=(1, 2, 4),
@@ -118,7 +126,8 @@ def main():
 
     torch.manual_seed(42)
     model = getattr(M, cfg["cls"])(**cfg["kwargs"]).to(dev)
-    mod = M.VAELightningModule(model, cfg["opt"], {"type": "none"}, cfg["loss"], gradient_clip_val=cfg["clip"])
+    mod = M.VAELightningModule(model, cfg["opt"], {"type": "none"}, cfg["loss"], gradient_clip_val=cfg["clip"],
+                               precision=cfg.get("precision", "32"))
     mod.configure_optimizers()
     if world > 1:
         ddp.DataParallel(mod)
@@ -147,6 +156,7 @@ def main():
     loss_v = float(loss)
 
     roofline = None
+    bf16 = cfg.get("precision", "32") == "bf16-mixed"
     if not args.no_kernel_timing:
         ops.PROFILE = []
         torch.cuda.synchronize()
@@ -175,11 +185,13 @@ def main():
             d[1] += f
             d[2] += s.elapsed_time(e)
         ach = tot_fl / (tot_ms * 1e-3) / 1e12
+        peak = BF16_DENSE_PEAK_TF if bf16 else PEAK_3XBF16_TF
         roofline = {"bound": "mfma", "kernel": "gemm3x_kernel (implicit-GEMM conv + attention bmm, all launches)",
-                    "achieved": round(ach, 2), "peak": round(PEAK_3XBF16_TF, 1), "unit": "TFLOP/s",
-                    "frac": round(ach / PEAK_3XBF16_TF, 4), "traffic": None,
-                    "peak_note": "3xBF16 fp32-emulation ceiling = bf16 dense MFMA 2.5 PF/s / 3; "
-                                 "native fp32 MFMA peak is 157.3 TF/s",
+                    "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                    "frac": round(ach / peak, 4), "traffic": None,
+                    "peak_note": ("bf16 dense MFMA peak 2.5 PF/s (bf16 operands, fp32 accumulate)" if bf16 else
+                                  "3xBF16 fp32-emulation ceiling = bf16 dense MFMA 2.5 PF/s / 3; "
+                                  "native fp32 MFMA peak is 157.3 TF/s"),
                     "launches_per_step": len(rec), "avg_launch_us": round(tot_ms * 1e3 / len(rec), 2),
                     "gemm_ms_per_step": round(tot_ms, 2), "instrumented_step_ms": round(step_ms, 2),
                     "gemm_share_of_step": round(tot_ms / step_ms, 3),
@@ -187,7 +199,7 @@ def main():
                                     "TFLOP/s": round(v[1] / (v[2] * 1e-3) / 1e12, 1)} for k, v in by.items()}}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg["loss"]["type"] == "vae":
         cpu = cpu_baseline(cfg)
 
     if rank == 0:
@@ -196,7 +208,8 @@ def main():
                if args.config == "c4" else f"training images/sec, config {args.config}",
                "value": round(imgs / dt, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (3xBF16 MFMA, fp32 accumulate)",
+               "scaling": "weak", "vs_baseline": None, "dtype": ("bf16 (bf16-mixed: bf16 MFMA operands, fp32 accumulate/activations)" if bf16
+                                                     else "fp32 (3xBF16 MFMA, fp32 accumulate)"),
                "data": "synthetic (MedMNIST-shaped, resident in HBM; random-init weights)",
                "config": {"workload": f"{cfg['cls']} {cfg['res']}x{cfg['res']}x{cfg['kwargs']['input_channels']} "
                                       f"train step (fwd+loss+bwd+clip+AdamW)", "model": cfg["cls"],

@@ -31,6 +31,13 @@ extern "C" {
 const char* mvae_last_error(void);
 int mvae_abi_version(void);
 
+/* Process-wide GEMM arithmetic for all convolution / GEMM entry points below:
+ * 0 = 3xBF16 fp32 emulation (default; the reference's precision=32 training),
+ * 1 = bf16 operands, fp32 accumulation and fp32 outputs (the reference's precision="bf16-mixed"
+ *     autocast runs these convolutions/bmm in bf16; main.py trainer precision flag). */
+int mvae_set_math_mode(int mode);
+int mvae_get_math_mode(void);
+
 /* ---- convolutions (implicit GEMM on MFMA, 3xBF16 split arithmetic, fp32 accumulate) ------------
  * Replaces nn.Conv2d forward in ResnetBlock/AttnBlock/Encoder/Decoder
  * (src/models/encoder_decoder.py:123-146,76-81,250-299,356-418), Downsample's F.pad + stride-2 conv
@@ -117,6 +124,29 @@ int mvae_multi_tensor_adam(float* params, float* grads, float* exp_avg, float* e
                            float beta2, float eps, float weight_decay, int decoupled, void* workspace,
                            size_t workspace_bytes, float* scalars, void* stream);
 size_t mvae_multi_tensor_adam_workspace_bytes(int nchunks, int ntensors);
+
+/* ---- perceptual loss (LPIPSLoss, src/losses/vae_losses.py:67-94; lpips 0.1.4 net="alex"/"vgg") ----
+ * y = (a*x + b - shift[c]) * inv_scale[c]: `inputs*2-1` (a=2, b=-1) then lpips' ScalingLayer. */
+int mvae_lpips_scale(const float* x, float* y, long long n, int c, float a, float b, const float* shift,
+                     const float* inv_scale, void* stream);
+int mvae_lpips_scale_bwd(const float* dy, float* dx, long long n, int c, float a, const float* inv_scale,
+                         void* stream);
+/* ReLU of the AlexNet feature slices (torchvision alexnet.features) and its gradient (from the output). */
+int mvae_relu_fwd(const float* x, float* y, long long n, void* stream);
+int mvae_relu_bwd(const float* y, const float* dy, float* dx, long long n, void* stream);
+/* MaxPool2d(k, stride) over NHWC (AlexNet 3/2, VGG16 2/2); argmax = window index per output element
+ * (first max wins, as in torch). */
+int mvae_maxpool_fwd(const float* x, float* y, unsigned char* argmax, int nb, int h, int w, int c, int k, int stride,
+                     void* stream);
+int mvae_maxpool_bwd(const float* dy, const unsigned char* argmax, float* dx, int nb, int h, int w, int c, int k,
+                     int stride, void* stream);
+/* One LPIPS layer: score[b] = beta*score[b] + mean_p sum_c w[c] (f0/(|f0|+1e-10) - f1/(|f1|+1e-10))^2
+ * (normalize_tensor + NetLinLayer 1x1 conv + spatial_average); c <= 512. Gradient w.r.t. f0 and (if
+ * df1 != NULL) f1, scaled by gscore[b]. */
+int mvae_lpips_dist(const float* f0, const float* f1, const float* w, float* score, int nb, int npix, int c,
+                    float beta, void* stream);
+int mvae_lpips_dist_bwd(const float* f0, const float* f1, const float* w, const float* gscore, float* df0, float* df1,
+                        int nb, int npix, int c, void* stream);
 
 #ifdef __cplusplus
 }

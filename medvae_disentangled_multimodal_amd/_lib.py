@@ -23,6 +23,8 @@ Z = c_size_t
 SIGNATURES = {
     "mvae_last_error": (ctypes.c_char_p, []),
     "mvae_abi_version": (I, []),
+    "mvae_set_math_mode": (I, [I]),
+    "mvae_get_math_mode": (I, []),
     "mvae_conv2d_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P]),
     "mvae_conv2d_wgrad_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),
     "mvae_conv2d_wgrad_workspace_bytes": (Z, [I, I, I, I, I, I, I]),
@@ -45,6 +47,14 @@ SIGNATURES = {
     "mvae_recon_bwd": (I, [I, P, P, P, D, P, L, P]),
     "mvae_multi_tensor_adam": (I, [P, P, P, P, P, P, P, I, P, I, P, P, F, F, I, F, F, F, F, F, I, P, Z, P, P]),
     "mvae_multi_tensor_adam_workspace_bytes": (Z, [I, I]),
+    "mvae_lpips_scale": (I, [P, P, L, I, F, F, P, P, P]),
+    "mvae_lpips_scale_bwd": (I, [P, P, L, I, F, P, P]),
+    "mvae_relu_fwd": (I, [P, P, L, P]),
+    "mvae_relu_bwd": (I, [P, P, P, L, P]),
+    "mvae_maxpool_fwd": (I, [P, P, P, I, I, I, I, I, I, P]),
+    "mvae_maxpool_bwd": (I, [P, P, P, I, I, I, I, I, I, P]),
+    "mvae_lpips_dist": (I, [P, P, P, P, I, I, I, F, P]),
+    "mvae_lpips_dist_bwd": (I, [P, P, P, P, P, P, I, I, I, P]),
 }
 
 

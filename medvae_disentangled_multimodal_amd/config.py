@@ -25,6 +25,8 @@ TARGET_MAP = {
     "src.models.Encoder": f"{_PKG}.Encoder",
     "src.models.Decoder": f"{_PKG}.Decoder",
     "src.losses.VAELoss": f"{_PKG}.VAELoss",
+    "src.losses.LPIPSLoss": f"{_PKG}.LPIPSLoss",
+    "src.losses.LPIPSWithDiscriminator": f"{_PKG}.LPIPSWithDiscriminator",
 }
 
 

@@ -123,11 +123,14 @@ struct Img {
   static constexpr int SIZE = 2 * PLANE;
 };
 
+// PREC 3: hi and lo planes (3xBF16); PREC 1: hi plane only (bf16 operands, fp32 accumulate)
+template <int PREC>
 __device__ __forceinline__ void st_split(__bf16* img, int plane, int off, const float4& v) {
   const __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y, h2 = (__bf16)v.z, h3 = (__bf16)v.w;
   *(bf16x4*)(img + off) = bf16x4{h0, h1, h2, h3};
-  *(bf16x4*)(img + plane + off) = bf16x4{(__bf16)(v.x - (float)h0), (__bf16)(v.y - (float)h1),
-                                         (__bf16)(v.z - (float)h2), (__bf16)(v.w - (float)h3)};
+  if constexpr (PREC == 3)
+    *(bf16x4*)(img + plane + off) = bf16x4{(__bf16)(v.x - (float)h0), (__bf16)(v.y - (float)h1),
+                                           (__bf16)(v.z - (float)h2), (__bf16)(v.w - (float)h3)};
 }
 
 // fragment of a 32x32x16 MFMA operand: lane l holds element [row0 + (l&31)][ks*16 + 8*(l>>5) + j]
@@ -190,7 +193,7 @@ __device__ __forceinline__ int row_of_tid(int tid) {
 // ------------------------------------------------------------------------------------------
 
 // ROW image, source element (row, k) at P[row*ld + k]
-template <int ROWS, int VEC, int NT, bool IS_A>
+template <int ROWS, int VEC, int NT, bool IS_A, int PREC>
 struct LoadRowK {
   static constexpr bool COL = false;
   static constexpr int RP = NT / 8;     // rows per pass (8 float4 per 32-wide row)
@@ -219,7 +222,7 @@ struct LoadRowK {
     }
   }
   __device__ void store_slot(__bf16* img, int i) {
-    st_split(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+    st_split<PREC>(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
   }
   __device__ void advance() { k += BK; }
   __device__ void load(const GemmArgs& a) {
@@ -234,7 +237,7 @@ struct LoadRowK {
 };
 
 // ROW image, implicit im2col of an NHWC tensor: element (pixel m, k = (r*S+s)*Cx + c)
-template <int ROWS, int VEC, int NT, int MODE>
+template <int ROWS, int VEC, int NT, int MODE, int PREC>
 struct LoadConvA {
   static constexpr bool COL = false;
   static constexpr int RP = NT / 8;
@@ -298,7 +301,7 @@ struct LoadConvA {
     }
   }
   __device__ void store_slot(__bf16* img, int i) {
-    st_split(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+    st_split<PREC>(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
   }
   __device__ void advance() { k += BK; }
   __device__ void load(const GemmArgs& a) {
@@ -313,7 +316,7 @@ struct LoadConvA {
 };
 
 // COL image, source element (row, k) at P[k*ld + row] (rows contiguous)
-template <int ROWS, int VEC, int NT, bool IS_A>
+template <int ROWS, int VEC, int NT, bool IS_A, int PREC>
 struct LoadColK {
   static constexpr bool COL = true;
   static constexpr int C4 = ROWS / 4;                 // float4 per k-row
@@ -348,7 +351,7 @@ struct LoadColK {
     constexpr int P_ = Img<ROWS, true>::PITCH;
     const int krow = kr + i * (NT / C4);
     if (krow < BK) {
-      st_split(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+      st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
       if constexpr (IS_A) {
         bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
       }
@@ -367,7 +370,7 @@ struct LoadColK {
 
 // COL image for the wgrad B operand: rows n' = (r*S+s)*Cx + c (filter element), k = output pixel.
 // element = X[b][src(oh,ow,r,s)][c], contiguous along c.
-template <int ROWS, int VEC, int NT, int MODE>
+template <int ROWS, int VEC, int NT, int MODE, int PREC>
 struct LoadWgradX {
   static constexpr bool COL = true;
   static constexpr int C4 = ROWS / 4;
@@ -430,7 +433,7 @@ struct LoadWgradX {
   __device__ void store_slot(__bf16* img, int i) {
     constexpr int P_ = Img<ROWS, true>::PITCH;
     const int krow = kr + i * (NT / C4);
-    if (krow < BK) st_split(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+    if (krow < BK) st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
   }
   __device__ void advance() { k += BK; }
   __device__ void load(const GemmArgs& a) {
@@ -444,28 +447,39 @@ struct LoadWgradX {
   }
 };
 
-template <int KIND, int ROWS, int VEC, int NT, bool IS_A>
-struct Loader;
-template <int ROWS, int VEC, int NT, bool IS_A>
-struct Loader<0, ROWS, VEC, NT, IS_A> : LoadRowK<ROWS, VEC, NT, IS_A> {};
-template <int ROWS, int VEC, int NT, bool IS_A>
-struct Loader<1, ROWS, VEC, NT, IS_A> : LoadColK<ROWS, VEC, NT, IS_A> {};
-template <int ROWS, int VEC, int NT>
-struct Loader<2, ROWS, VEC, NT, true> : LoadConvA<ROWS, VEC, NT, MODE_FWD> {};
-template <int ROWS, int VEC, int NT>
-struct Loader<3, ROWS, VEC, NT, true> : LoadConvA<ROWS, VEC, NT, MODE_UPS> {};
-template <int ROWS, int VEC, int NT>
-struct Loader<4, ROWS, VEC, NT, true> : LoadConvA<ROWS, VEC, NT, MODE_DGRAD> {};
-template <int ROWS, int VEC, int NT>
-struct Loader<2, ROWS, VEC, NT, false> : LoadWgradX<ROWS, VEC, NT, MODE_FWD> {};
-template <int ROWS, int VEC, int NT>
-struct Loader<3, ROWS, VEC, NT, false> : LoadWgradX<ROWS, VEC, NT, MODE_UPS> {};
+// one 32x32x16 product step: 3xBF16 (lo*hi + hi*lo + hi*hi, small terms first) or plain bf16
+template <int PREC>
+__device__ __forceinline__ void mma(f32x16& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
+                                    const bf16x8& bl) {
+  if constexpr (PREC == 3) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  }
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+}
 
-template <int BM, int BN, int WGM, int WGN, int AK, int VA, int BKIND, int VB>
+template <int KIND, int ROWS, int VEC, int NT, bool IS_A, int PREC>
+struct Loader;
+template <int ROWS, int VEC, int NT, bool IS_A, int PREC>
+struct Loader<0, ROWS, VEC, NT, IS_A, PREC> : LoadRowK<ROWS, VEC, NT, IS_A, PREC> {};
+template <int ROWS, int VEC, int NT, bool IS_A, int PREC>
+struct Loader<1, ROWS, VEC, NT, IS_A, PREC> : LoadColK<ROWS, VEC, NT, IS_A, PREC> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<2, ROWS, VEC, NT, true, PREC> : LoadConvA<ROWS, VEC, NT, MODE_FWD, PREC> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<3, ROWS, VEC, NT, true, PREC> : LoadConvA<ROWS, VEC, NT, MODE_UPS, PREC> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<4, ROWS, VEC, NT, true, PREC> : LoadConvA<ROWS, VEC, NT, MODE_DGRAD, PREC> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<2, ROWS, VEC, NT, false, PREC> : LoadWgradX<ROWS, VEC, NT, MODE_FWD, PREC> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<3, ROWS, VEC, NT, false, PREC> : LoadWgradX<ROWS, VEC, NT, MODE_UPS, PREC> {};
+
+template <int BM, int BN, int WGM, int WGN, int AK, int VA, int BKIND, int VB, int PREC>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   constexpr int NT = 64 * WGM * WGN;
-  using LA = Loader<AK, BM, VA, NT, true>;
-  using LB = Loader<BKIND, BN, VB, NT, false>;
+  using LA = Loader<AK, BM, VA, NT, true, PREC>;
+  using LB = Loader<BKIND, BN, VB, NT, false, PREC>;
   using IA = Img<BM, LA::COL>;
   using IB = Img<BN, LB::COL>;
   constexpr int BUF = IA::SIZE + IB::SIZE;
@@ -536,17 +550,16 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         bh[j] = read_frag<BN, LB::COL>(Bi, brow + j * 32, ks, lane);
-        bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, ks, lane);
+        if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, ks, lane);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const bf16x8 ah = read_frag<BM, LA::COL>(Ai, arow + i * 32, ks, lane);
-        const bf16x8 al = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow + i * 32, ks, lane);
+        bf16x8 al{};
+        if constexpr (PREC == 3) al = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow + i * 32, ks, lane);
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
+          mma<PREC>(acc[i][j], ah, al, bh[j], bl[j]);
         }
       }
     }
@@ -572,29 +585,27 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       bh[j] = read_frag<BN, LB::COL>(Bi, brow + j * 32, 0, lane);
-      bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, 0, lane);
+      if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, 0, lane);
     }
     ah[0] = read_frag<BM, LA::COL>(Ai, arow, 0, lane);
-    al[0] = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow, 0, lane);
+    if constexpr (PREC == 3) al[0] = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow, 0, lane);
 #pragma unroll
     for (int st = 0; st < STEPS; ++st) {
       const int i = st % TM, cur = st & 1;
       if (st + 1 < STEPS) {
         const int ks1 = (st + 1) / TM, i1 = (st + 1) % TM;
         ah[cur ^ 1] = read_frag<BM, LA::COL>(Ai, arow + i1 * 32, ks1, lane);
-        al[cur ^ 1] = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow + i1 * 32, ks1, lane);
+        if constexpr (PREC == 3) al[cur ^ 1] = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow + i1 * 32, ks1, lane);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[cur], bh[j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cur], bl[j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cur], bh[j], acc[i][j], 0, 0, 0);
+        mma<PREC>(acc[i][j], ah[cur], al[cur], bh[j], bl[j]);
       }
       if (st == TM - 1) {  // B fragments of the second k-half
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           bh[j] = read_frag<BN, LB::COL>(Bi, brow + j * 32, 1, lane);
-          bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, 1, lane);
+          if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, 1, lane);
         }
       }
 #pragma unroll
@@ -715,6 +726,10 @@ __global__ void splitk_reduce_kernel(GemmArgs a);
 // ------------------------------------------------------------------------------------------
 enum { T256x256 = 0, T256x128 = 1, T128x256 = 2, T128x128 = 3, T64x64 = 4 };
 
+// process-wide GEMM arithmetic (mvae_set_math_mode): 3xBF16 fp32 emulation (default) or bf16
+enum { MATH_3XBF16 = 0, MATH_BF16 = 1 };
+int math_mode();
+
 inline long long tiles_of(int cfg, const GemmArgs& a) {
   static const int TM_[] = {256, 256, 128, 128, 64};
   static const int TN_[] = {256, 128, 256, 128, 64};
@@ -765,7 +780,10 @@ void launch_cfg(GemmArgs& a, hipStream_t st) {
   a.tiles_m = cdiv(a.M, BM);
   a.tiles_n = cdiv(a.N, BN);
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splits);
-  hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB>), grid, dim3(64 * WGM * WGN), 0, st, a);
+  if (math_mode() == MATH_BF16)
+    hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, 1>), grid, dim3(64 * WGM * WGN), 0, st, a);
+  else
+    hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, 3>), grid, dim3(64 * WGM * WGN), 0, st, a);
 }
 
 template <int AK, int VA, int BKIND, int VB>

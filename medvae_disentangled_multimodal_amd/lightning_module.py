@@ -20,7 +20,8 @@ import torch
 import torch.nn as nn
 
 from .disentangled import DisentangledConditionalVAE
-from .losses import DisentangledVAELoss, LPIPSLoss, VAELoss
+from . import ops
+from .losses import DisentangledVAELoss, LPIPSLoss, LPIPSWithDiscriminator, VAELoss
 from .optim import Adam, AdamW, FlatParameters, FusedAdam
 from .schedulers import get_scheduler
 
@@ -42,8 +43,15 @@ def _model_kind(model: nn.Module) -> str:
 
 class VAELightningModule(_Base):
     def __init__(self, model: nn.Module, optimizer_config: Dict[str, Any], scheduler_config: Dict[str, Any],
-                 loss_config: Dict[str, Any], gradient_clip_val: Optional[float] = None, **kwargs):
+                 loss_config: Dict[str, Any], gradient_clip_val: Optional[float] = None,
+                 precision="32", **kwargs):
+        """`precision` stands in for the Lightning Trainer's flag ("32" or "bf16-mixed"): it selects
+        the GEMM arithmetic of the step (ops.set_precision)."""
         super().__init__()
+        if precision not in ops._PRECISION:
+            raise ValueError(f"precision {precision!r} is not supported on the MI355X path")
+        self.precision = precision
+        self.global_step_count = 0
         self.model = model
         self.optimizer_config = dict(optimizer_config)
         self.scheduler_config = dict(scheduler_config or {"type": "none"})
@@ -73,7 +81,22 @@ class VAELightningModule(_Base):
                 separation_weight=self.loss_config.get("separation_weight", 0.1),
                 contrastive_weight=self.loss_config.get("contrastive_weight", 0.05))
         elif t == "lpips":
-            self.criterion = LPIPSLoss()
+            # the reference passes posteriors/priors kwargs LPIPSLoss cannot take (TypeError there);
+            # here the objective is the perceptual distance alone
+            self.criterion = LPIPSLoss(net=self.loss_config.get("lpips_net", "alex"),
+                                       weights=self.loss_config.get("lpips_weights"),
+                                       allow_synthetic=self.loss_config.get("allow_synthetic_lpips", False))
+        elif t == "lpips_discriminator":
+            self.criterion = LPIPSWithDiscriminator(
+                discriminator_factor=self.loss_config.get("discriminator_factor", 1.0),
+                perceptual_factor=self.loss_config.get("perceptual_factor", 1.0),
+                kl_factor=self.loss_config.get("kl_factor", 1.0),
+                discriminator_iter_start=self.loss_config.get("discriminator_iter_start", 50001),
+                use_biomedclip_loss=self.loss_config.get("use_biomedclip_loss", False),
+                discriminator_config=self.loss_config.get("discriminator", {}),
+                lpips_weights=self.loss_config.get("lpips_weights"),
+                allow_synthetic_lpips=self.loss_config.get("allow_synthetic_lpips", False),
+                lpips_net=self.loss_config.get("lpips_net", "alex"))
         else:
             raise ValueError(f"Unknown/unsupported loss type on the MI355X path: {t}")
         self.use_discriminator = False
@@ -108,6 +131,19 @@ class VAELightningModule(_Base):
             outputs = self.model(x, **kw)
         if isinstance(self.criterion, DisentangledVAELoss):
             loss_dict = self.criterion(outputs, x)
+        elif isinstance(self.criterion, LPIPSWithDiscriminator):
+            # generator objective (lightning_module.py:131-149); the discriminator step has nothing to
+            # learn before discriminator_iter_start (its loss is a constant 0)
+            loss_g, log = self.criterion(inputs=x, reconstructions=outputs["reconstruction"], latent=outputs["z"],
+                                         posteriors=outputs["posterior"], optimizer_idx=0,
+                                         global_step=self.global_step_count, split="train")
+            for k, v in log.items():
+                self.log(k, v)
+            self._last_outputs = outputs
+            return loss_g
+        elif isinstance(self.criterion, LPIPSLoss):
+            p = self.criterion(x, outputs["reconstruction"])
+            loss_dict = {"loss": p, "p_loss": p}
         else:
             loss_dict = self.criterion(inputs=x, reconstructions=outputs["reconstruction"],
                                        posteriors=outputs["posterior"], priors=outputs["prior"])
@@ -155,10 +191,15 @@ class VAELightningModule(_Base):
         if self.optimizer is None:
             self.configure_optimizers()
         self.model.train()
-        self.optimizer.zero_grad()
-        loss = self.training_step(batch, batch_idx, eps=eps)
-        loss.backward()
-        if self.process_group is not None:
-            self.process_group.allreduce_gradients(self.flat)
-        self.optimizer.step(used=self._used_mask())
+        prev = ops.set_precision(self.precision)
+        try:
+            self.optimizer.zero_grad()
+            loss = self.training_step(batch, batch_idx, eps=eps)
+            loss.backward()
+            if self.process_group is not None:
+                self.process_group.allreduce_gradients(self.flat)
+            self.optimizer.step(used=self._used_mask())
+        finally:
+            ops.restore_math_mode(prev)
+        self.global_step_count += 1
         return loss

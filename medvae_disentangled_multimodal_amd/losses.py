@@ -74,9 +74,59 @@ class DisentangledVAELoss(nn.Module):
 
 
 class LPIPSLoss(nn.Module):
-    """Perceptual loss of the reference (vae_losses.py:67-94) needs the pretrained `lpips` AlexNet
-    weights, which cannot be fetched here; construction fails loudly instead of silently degrading."""
+    """Perceptual loss of the reference (vae_losses.py:67-94): LPIPS(x*2-1, rec*2-1).mean(), gray
+    inputs repeated to 3 channels. Backed by `lpips.LPIPS` (AlexNet) on the HIP kernels; the
+    pretrained weights come from `weights=` / MVAE_LPIPS_WEIGHTS (see lpips.py)."""
 
-    def __init__(self, *a, **k):
+    def __init__(self, net: str = "alex", use_gpu: bool = True, weights=None, allow_synthetic: bool = False,
+                 seed: int = 0):
         super().__init__()
-        raise NotImplementedError("LPIPS needs pretrained backbone weights that are not available offline")
+        from .lpips import LPIPS
+        self.lpips = LPIPS(net=net, weights=weights, allow_synthetic=allow_synthetic, seed=seed)
+        if use_gpu and torch.cuda.is_available():
+            self.lpips = self.lpips.cuda()
+
+    def forward(self, inputs: torch.Tensor, reconstructions: torch.Tensor) -> torch.Tensor:
+        if inputs.shape[1] == 1:
+            inputs = inputs.repeat(1, 3, 1, 1)
+        if reconstructions.shape[1] == 1:
+            reconstructions = reconstructions.repeat(1, 3, 1, 1)
+        return self.lpips(inputs, reconstructions, pre_a=2.0, pre_b=-1.0).mean()
+
+
+class LPIPSWithDiscriminator(nn.Module):
+    """Generator objective of the reference's combined loss (vae_losses.py:214-362):
+    perceptual_factor * LPIPS + kl_factor * KL(q || N(0, I)).sum() / B (+ d_weight * g_loss once
+    global_step >= discriminator_iter_start). The reference calls `posteriors.kl()`, which a
+    torch Normal does not have; the closed-form KL is used. The
+    adversarial branch (NLayerDiscriminator, adaptive weight) is the next scope row and raises."""
+
+    def __init__(self, discriminator_factor: float = 1.0, perceptual_factor: float = 1.0, kl_factor: float = 1.0,
+                 discriminator_iter_start: int = 50001, use_biomedclip_loss: bool = False,
+                 biomedclip_factor: float = 1.0, discriminator_config=None, lpips_weights=None,
+                 allow_synthetic_lpips: bool = False, lpips_net: str = "alex"):
+        super().__init__()
+        if use_biomedclip_loss:
+            raise NotImplementedError("BiomedCLIP loss is outside the MI355X hot path")
+        self.discriminator_factor = discriminator_factor
+        self.perceptual_factor = perceptual_factor
+        self.kl_factor = kl_factor
+        self.discriminator_iter_start = discriminator_iter_start
+        self.perceptual_loss = LPIPSLoss(net=lpips_net, weights=lpips_weights, allow_synthetic=allow_synthetic_lpips)
+
+    def forward(self, inputs, reconstructions, latent=None, posteriors=None, optimizer_idx: int = 0,
+                global_step: int = 0, last_layer=None, split: str = "train", **kwargs):
+        bsz = inputs.shape[0]
+        d_valid = global_step >= self.discriminator_iter_start
+        if d_valid:
+            raise NotImplementedError("adversarial branch (NLayerDiscriminator) is not built yet")
+        if optimizer_idx == 1:
+            zero = torch.zeros((), device=inputs.device)
+            return zero, {f"{split}/d_loss": zero}
+        p_loss = self.perceptual_loss(inputs, reconstructions)
+        kl_loss = ops.kl_closed_form_sum(posteriors._mvae_mean, posteriors._mvae_logvar, bsz)
+        zero = torch.zeros((), device=inputs.device)
+        loss = self.perceptual_factor * p_loss + self.kl_factor * kl_loss
+        log = {f"{split}/total_loss": loss.detach(), f"{split}/kl_loss": kl_loss.detach(),
+               f"{split}/p_loss": p_loss.detach(), f"{split}/d_weight": zero, f"{split}/g_loss": zero}
+        return loss, log

@@ -496,3 +496,150 @@ def mse_mean(a, b):
 
 def l1_mean(a, b):
     return ReconFn.apply(a, b, 2)
+
+
+# ------------------------------------------------------------------------------------------
+# GEMM arithmetic (trainer precision)
+# ------------------------------------------------------------------------------------------
+_PRECISION = {"32": 0, "32-true": 0, "fp32": 0, 32: 0, "bf16": 1, "bf16-mixed": 1, "bf16-true": 1}
+
+
+def set_precision(precision) -> int:
+    """Map the reference trainer's `precision` flag onto the GEMM arithmetic of every following
+    conv/bmm launch: "32" -> 3xBF16 fp32 emulation, "bf16-mixed" -> bf16 operands with fp32
+    accumulation (what autocast runs these ops in). Returns the previous mode."""
+    if precision not in _PRECISION:
+        raise ValueError(f"precision {precision!r} is not supported on the MI355X path "
+                         f"(supported: {sorted(map(str, _PRECISION))})")
+    prev = _lib.query("mvae_get_math_mode")
+    _lib.call("mvae_set_math_mode", _PRECISION[precision])
+    return prev
+
+
+def restore_math_mode(mode: int):
+    _lib.call("mvae_set_math_mode", int(mode))
+
+
+# ------------------------------------------------------------------------------------------
+# perceptual loss pieces (LPIPS, vae_losses.py:67-94)
+# ------------------------------------------------------------------------------------------
+def _like_cl(t):
+    return torch.empty_like(t, memory_format=CL) if t.dim() == 4 else torch.empty_like(t)
+
+
+class ReluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        _check(x, "relu input")
+        x = nhwc(x)
+        y = _like_cl(x)
+        _lib.call("mvae_relu_fwd", x.data_ptr(), y.data_ptr(), x.numel(), _stream(x))
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = nhwc(dy.float())
+        dx = _like_cl(y)
+        _lib.call("mvae_relu_bwd", y.data_ptr(), dy.data_ptr(), dx.data_ptr(), y.numel(), _stream(y))
+        return dx
+
+
+def relu(x):
+    return ReluFn.apply(x)
+
+
+class MaxPoolFn(torch.autograd.Function):
+    """nn.MaxPool2d(kernel_size=k, stride=s), no padding (torchvision alexnet 3/2, vgg16 2/2)."""
+
+    @staticmethod
+    def forward(ctx, x, k: int, s: int):
+        _check(x, "maxpool input")
+        x = nhwc(x)
+        n, c, h, w = x.shape
+        ho, wo = (h - k) // s + 1, (w - k) // s + 1
+        y = torch.empty((n, c, ho, wo), device=x.device, dtype=torch.float32, memory_format=CL)
+        arg = torch.empty((n, ho, wo, c), device=x.device, dtype=torch.uint8)
+        _lib.call("mvae_maxpool_fwd", x.data_ptr(), y.data_ptr(), arg.data_ptr(), n, h, w, c, k, s, _stream(x))
+        ctx.save_for_backward(arg)
+        ctx.shape, ctx.k, ctx.s = (n, c, h, w), k, s
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        n, c, h, w = ctx.shape
+        dy = nhwc(dy.float())
+        dx = torch.empty((n, c, h, w), device=dy.device, dtype=torch.float32, memory_format=CL)
+        _lib.call("mvae_maxpool_bwd", dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), n, h, w, c, ctx.k, ctx.s,
+                  _stream(dy))
+        return dx, None, None
+
+
+def max_pool(x, k: int, s: int):
+    return MaxPoolFn.apply(x, k, s)
+
+
+def max_pool3s2(x):
+    return MaxPoolFn.apply(x, 3, 2)
+
+
+class LpipsScaleFn(torch.autograd.Function):
+    """y = (a*x + b - shift[c]) * inv_scale[c]  (`x*2-1` then lpips' ScalingLayer)."""
+
+    @staticmethod
+    def forward(ctx, x, shift, inv_scale, a: float, b: float):
+        _check(x, "lpips input")
+        x = nhwc(x.float())
+        y = _like_cl(x)
+        _lib.call("mvae_lpips_scale", x.data_ptr(), y.data_ptr(), x.numel(), x.shape[1], float(a), float(b),
+                  shift.data_ptr(), inv_scale.data_ptr(), _stream(x))
+        ctx.save_for_backward(inv_scale)
+        ctx.a = float(a)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (inv_scale,) = ctx.saved_tensors
+        dy = nhwc(dy.float())
+        dx = _like_cl(dy)
+        _lib.call("mvae_lpips_scale_bwd", dy.data_ptr(), dx.data_ptr(), dy.numel(), dy.shape[1], ctx.a,
+                  inv_scale.data_ptr(), _stream(dy))
+        return dx, None, None, None, None
+
+
+def lpips_scale(x, shift, inv_scale, a=2.0, b=-1.0):
+    return LpipsScaleFn.apply(x, shift, inv_scale, a, b)
+
+
+class LpipsDistFn(torch.autograd.Function):
+    """Per-image LPIPS layer distance: mean over pixels of sum_c w_c (f0/|f0| - f1/|f1|)^2."""
+
+    @staticmethod
+    def forward(ctx, f0, f1, w):
+        _check(f0, "lpips features")
+        f0, f1 = nhwc(f0), nhwc(f1)
+        n, c, h, wd = f0.shape
+        w = w.detach().contiguous().float()
+        score = torch.empty(n, device=f0.device, dtype=torch.float32)
+        _lib.call("mvae_lpips_dist", f0.data_ptr(), f1.data_ptr(), w.data_ptr(), score.data_ptr(), n, h * wd, c, 0.0,
+                  _stream(f0))
+        ctx.save_for_backward(f0, f1, w)
+        return score
+
+    @staticmethod
+    def backward(ctx, g):
+        f0, f1, w = ctx.saved_tensors
+        n, c, h, wd = f0.shape
+        g = g.contiguous().float()
+        need0, need1 = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        df0 = _like_cl(f0)
+        df1 = _like_cl(f1) if need1 else None
+        _lib.call("mvae_lpips_dist_bwd", f0.data_ptr(), f1.data_ptr(), w.data_ptr(), g.data_ptr(), df0.data_ptr(),
+                  _ptr(df1), n, h * wd, c, _stream(f0))
+        return (df0 if need0 else None), df1, None
+
+
+def lpips_dist(f0, f1, w):
+    return LpipsDistFn.apply(f0, f1, w)

@@ -486,3 +486,76 @@ def train_step(P: Dict[str, Tensor], a: Arch, x, cond, eps, loss_cfg: dict, opt_
                   tuple(opt_cfg.get("betas", (0.9, 0.999))), 1e-8, wd, decoupled)
     return {"out": out, "loss": ld, "grads": raw, "clipped": grads, "total_norm": total,
             "params": newP, "state": state}
+
+
+# --------------------------------------------------------------------------------------------
+# LPIPS (net="alex"): src/losses/vae_losses.py:67-94 wraps the third-party `lpips` 0.1.4
+# (uv.lock:1585, not installed here). Restated from that package's published algorithm:
+#   lpips.LPIPS.forward (version 0.1): ScalingLayer -> alexnet slices relu1..relu5 ->
+#   normalize_tensor (x / (sqrt(sum_c x^2) + 1e-10)) -> (f0 - f1)^2 -> NetLinLayer (1x1, no bias;
+#   its Dropout is inactive in eval mode) -> spatial_average -> sum over layers.
+#   AlexNet features = torchvision.models.alexnet().features[0:12].
+# Parity against the real package is UNPINNED (no weights / package offline).
+# --------------------------------------------------------------------------------------------
+LPIPS_SHIFT = (-0.030, -0.088, -0.188)
+LPIPS_SCALE = (0.458, 0.448, 0.450)
+
+
+def lpips_alex(W: Dict[str, Tensor], in0: Tensor, in1: Tensor, pre=(2.0, -1.0)) -> Tensor:
+    """W: conv{1..5}.weight/.bias and lins.{0..4} (the HIP module's state-dict names)."""
+    shift = torch.tensor(LPIPS_SHIFT, dtype=in0.dtype).view(1, 3, 1, 1)
+    scale = torch.tensor(LPIPS_SCALE, dtype=in0.dtype).view(1, 3, 1, 1)
+
+    def feats(x):
+        x = (pre[0] * x + pre[1] - shift) / scale
+        out = []
+        h = F.relu(F.conv2d(x, W["conv1.weight"], W["conv1.bias"], stride=4, padding=2))
+        out.append(h)
+        h = F.relu(F.conv2d(F.max_pool2d(h, 3, 2), W["conv2.weight"], W["conv2.bias"], padding=2))
+        out.append(h)
+        h = F.relu(F.conv2d(F.max_pool2d(h, 3, 2), W["conv3.weight"], W["conv3.bias"], padding=1))
+        out.append(h)
+        h = F.relu(F.conv2d(h, W["conv4.weight"], W["conv4.bias"], padding=1))
+        out.append(h)
+        h = F.relu(F.conv2d(h, W["conv5.weight"], W["conv5.bias"], padding=1))
+        out.append(h)
+        return out
+
+    def normalize(f):
+        return f / (torch.sqrt(torch.sum(f * f, dim=1, keepdim=True)) + 1e-10)
+
+    score = 0
+    for k, (a, b) in enumerate(zip(feats(in0), feats(in1))):
+        d = (normalize(a) - normalize(b)) ** 2
+        lin = W[f"lins.{k}"].view(1, -1, 1, 1)
+        score = score + (d * lin).sum(1, keepdim=True).mean((2, 3), keepdim=True)
+    return score
+
+
+def lpips_vgg(W: Dict[str, Tensor], in0: Tensor, in1: Tensor, pre=(2.0, -1.0)) -> Tensor:
+    """lpips net="vgg": torchvision vgg16().features taps relu1_2, relu2_2, relu3_3, relu4_3, relu5_3
+    (lpips.pretrained_networks.vgg16 slices [0:4],[4:9],[9:16],[16:23],[23:30]); W: vgg.{0..12}.weight/.bias
+    and lins.{0..4}."""
+    shift = torch.tensor(LPIPS_SHIFT, dtype=in0.dtype).view(1, 3, 1, 1)
+    scale = torch.tensor(LPIPS_SCALE, dtype=in0.dtype).view(1, 3, 1, 1)
+
+    def feats(x):
+        h = (pre[0] * x + pre[1] - shift) / scale
+        out, i = [], 0
+        for block, n in enumerate((2, 2, 3, 3, 3)):
+            if block:
+                h = F.max_pool2d(h, 2, 2)
+            for _ in range(n):
+                h = F.relu(F.conv2d(h, W[f"vgg.{i}.weight"], W[f"vgg.{i}.bias"], padding=1))
+                i += 1
+            out.append(h)
+        return out
+
+    def normalize(f):
+        return f / (torch.sqrt(torch.sum(f * f, dim=1, keepdim=True)) + 1e-10)
+
+    score = 0
+    for k, (a, b) in enumerate(zip(feats(in0), feats(in1))):
+        d = (normalize(a) - normalize(b)) ** 2
+        score = score + (d * W[f"lins.{k}"].view(1, -1, 1, 1)).sum(1, keepdim=True).mean((2, 3), keepdim=True)
+    return score
