@@ -34,24 +34,107 @@ def init_from_env(backend: Optional[str] = None):
 
 class DataParallel:
     """Attach to a VAELightningModule: broadcasts the initial parameters from rank 0 and averages
-    the flat gradient buffer after every backward."""
+    the flat gradient buffer every step.
 
-    def __init__(self, module, group=None, bucket_bytes: int = BUCKET_BYTES):
+    Overlap: the flat buffer is cut into buckets of whole parameters in REVERSE registration order
+    (the order backward produces gradients: decoder first). Every op reports each parameter whose
+    flat-slot gradient it has finished (ops.GRAD_HOOK; autograd-accumulated parameters through a
+    post-accumulate hook), and a bucket's all-reduce is launched asynchronously (RCCL runs it on its
+    own stream, ordered after the kernels that wrote the bucket) as soon as its last parameter
+    reports -- so the collective of the decoder's gradients runs while the encoder's backward is
+    still computing. Buckets are launched strictly in bucket order (a ready bucket waits for its
+    predecessors), so every rank issues the same sequence of collectives even when ranks use
+    different parameters (the disentangled model's per-modality heads). `allreduce_gradients`
+    launches whatever never reported (parameters unused this step) and makes the compute stream
+    wait for all collectives before the optimizer."""
+
+    def __init__(self, module, group=None, bucket_bytes: int = BUCKET_BYTES, overlap: bool = True):
         self.module = module
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.bucket_elems = max(1, bucket_bytes // 4)
         if module.flat is None:
             module.configure_optimizers()
+        flat = module.flat
         if self.world > 1:
-            dist.broadcast(module.flat.data, src=0, group=group)
+            dist.broadcast(flat.data, src=0, group=group)
         module.optimizer.grad_scale = 1.0 / self.world
         module.process_group = self
+        self.overlap = overlap and self.world > 1
+        self._plan(flat)
+        self._works = []
+        self._armed = False
+        if self.overlap:
+            from . import ops
+            ops.GRAD_HOOK = self._on_grad
+
+    def _plan(self, flat):
+        """Buckets of whole parameters, reverse order, each >= bucket_elems (the last may be smaller)."""
+        self.buckets = []  # (start, end) element ranges of flat.grad
+        self.param_bucket = {}
+        members, lo, hi = [], None, None
+        for i in reversed(range(len(flat.params))):
+            p, off = flat.params[i], flat.offsets[i]
+            end = off + (p.numel() + 3) // 4 * 4
+            members.append(i)
+            lo = off
+            hi = end if hi is None else hi
+            if hi - lo >= self.bucket_elems:
+                self._close(members, lo, hi)
+                members, lo, hi = [], None, None
+        if members:
+            self._close(members, 0 if lo is None else lo, hi)
+        self.expected = [0] * len(self.buckets)
+        for b in self.param_bucket.values():
+            self.expected[b] += 1
+
+    def _close(self, members, lo, hi):
+        b = len(self.buckets)
+        self.buckets.append((lo, hi))
+        for i in members:
+            self.param_bucket[id(self.module.flat.params[i])] = b
+
+    def begin_backward(self):
+        """Arm the per-step readiness counters (call before loss.backward())."""
+        self.pending = list(self.expected)
+        self.launched = [False] * len(self.buckets)
+        self.next_bucket = 0
+        self.seen = set()
+        self._works = []
+        self._armed = True
+
+    def _on_grad(self, p):
+        if not self._armed:
+            return
+        key = id(p)
+        b = self.param_bucket.get(key)
+        if b is None or key in self.seen:
+            return
+        self.seen.add(key)
+        self.pending[b] -= 1
+        while self.next_bucket < len(self.buckets) and self.pending[self.next_bucket] == 0:
+            self._launch(self.next_bucket)
+            self.next_bucket += 1
+
+    def _launch(self, b):
+        lo, hi = self.buckets[b]
+        self.launched[b] = True
+        g = self.module.flat.grad[lo:hi]
+        self._works.append(dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
     def allreduce_gradients(self, flat):
         if self.world == 1:
             return
-        g = flat.grad
-        n = g.numel()
-        for s in range(0, n, self.bucket_elems):
-            dist.all_reduce(g[s:s + self.bucket_elems], op=dist.ReduceOp.SUM, group=self.group)
+        if not self.overlap or not self._armed:
+            g = flat.grad
+            n = g.numel()
+            for s in range(0, n, self.bucket_elems):
+                dist.all_reduce(g[s:s + self.bucket_elems], op=dist.ReduceOp.SUM, group=self.group)
+            return
+        for b in range(self.next_bucket, len(self.buckets)):  # incl. parameters that produced no gradient
+            self._launch(b)
+        self.next_bucket = len(self.buckets)
+        for w in self._works:
+            w.wait()
+        self._works = []
+        self._armed = False

@@ -195,6 +195,8 @@ class VAELightningModule(_Base):
         try:
             self.optimizer.zero_grad()
             loss = self.training_step(batch, batch_idx, eps=eps)
+            if self.process_group is not None:
+                self.process_group.begin_backward()
             loss.backward()
             if self.process_group is not None:
                 self.process_group.allreduce_gradients(self.flat)

@@ -92,6 +92,18 @@ def _main_grad(p: torch.Tensor):
     return getattr(p, "_mvae_main_grad", None)
 
 
+# Called with each parameter whose flat-slot gradient the backward pass has just finished writing
+# (set by ddp.DataParallel to launch bucket all-reduces while the rest of backward runs).
+GRAD_HOOK = None
+
+
+def _grad_done(*params):
+    if GRAD_HOOK is not None:
+        for p in params:
+            if p is not None:
+                GRAD_HOOK(p)
+
+
 # ------------------------------------------------------------------------------------------
 # convolution
 # ------------------------------------------------------------------------------------------
@@ -253,6 +265,10 @@ class Conv2dFn(torch.autograd.Function):
                 bias_grad_raw(dy.data_ptr(), n * ho * wo, co, db_ret, 0.0, dy.device, _stream(dy))
         if ctx.has_res and ctx.needs_input_grad[3]:
             dres = dy
+        if ctx.needs_input_grad[1] and dw_ret is None:
+            _grad_done(ctx.weight_ref)
+        if want_b and db_ret is None:
+            _grad_done(ctx.bias_ref)
         return dx, dw_ret, db_ret, dres, None
 
 
@@ -301,6 +317,10 @@ class GroupNormFn(torch.autograd.Function):
         _lib.call("mvae_group_norm_bwd_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
                   mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(dg), _ptr(db), n, h * w, c, groups, silu,
                   drop_p, seed, ws.data_ptr(), ws.numel(), _stream(x))
+        if ctx.needs_input_grad[1] and dg_ret is None:
+            _grad_done(ctx.gamma_ref)
+        if ctx.needs_input_grad[2] and db_ret is None:
+            _grad_done(ctx.beta_ref)
         return dx, dg_ret, db_ret, None, None, None, None, None
 
 

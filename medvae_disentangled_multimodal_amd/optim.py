@@ -20,6 +20,17 @@ CHUNK = 65536
 ALIGN = 4  # floats (16 bytes): every tensor starts 16B-aligned for float4 loads
 
 
+def _after_autograd_accumulate(p: torch.Tensor):
+    """Parameters whose gradient autograd accumulates (torch glue ops): keep the result in the flat
+    slot even if autograd swapped in a new .grad tensor, then report the gradient as complete."""
+    mg = p._mvae_main_grad
+    if p.grad is not None and p.grad.data_ptr() != mg.data_ptr():
+        mg.copy_(p.grad)
+        p.grad = mg
+    from . import ops
+    ops._grad_done(p)
+
+
 class FlatParameters:
     def __init__(self, module: torch.nn.Module, device=None):
         self.module = module
@@ -44,6 +55,8 @@ class FlatParameters:
             gv = self._view(self.grad, off, p)
             p._mvae_main_grad = gv
             p.grad = gv
+            if p.requires_grad:
+                p.register_post_accumulate_grad_hook(_after_autograd_accumulate)
         # chunk table for the multi-tensor kernels
         ct, cs, cl, tcb = [], [], [], [0]
         for t, (p, off) in enumerate(zip(self.params, offs)):

@@ -41,13 +41,32 @@ def _worker(rank, world, init_file, out_file):
     xs, ys = x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4]
     mod.flat.zero_grad()
     loss = torch.nn.functional.mse_loss(model(xs), ys)
+    dp.begin_backward()
     loss.backward()
+    # overlap: every bucket whose parameters all reported was launched during backward, in order
+    assert all(dp.launched), dp.launched
+    assert dp.next_bucket == len(dp.buckets) > 1
     dp.allreduce_gradients(mod.flat)
     avg = mod.flat.grad * mod.optimizer.grad_scale
     if rank == 0:
         torch.save({"params": mod.flat.data.clone(), "grad": avg.clone()}, out_file)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def test_bucket_plan_covers_flat_buffer():
+    from medvae_disentangled_multimodal_amd import ddp
+    model = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.Tanh(), torch.nn.Linear(5, 3), torch.nn.Linear(3, 9))
+    mod = _Mod(model)
+    dp = ddp.DataParallel.__new__(ddp.DataParallel)
+    dp.module, dp.bucket_elems = mod, 16
+    dp._plan(mod.flat)
+    # contiguous, non-overlapping, reverse order, covering the whole buffer, whole parameters only
+    spans = sorted(dp.buckets)
+    assert spans[0][0] == 0 and spans[-1][1] == mod.flat.numel
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    assert dp.buckets[0][1] == mod.flat.numel  # the decoder-side (last) parameters go first
+    assert sum(dp.expected) == len(mod.flat.params)
 
 
 def test_flat_gradient_allreduce_matches_global_batch():
@@ -70,3 +89,47 @@ def test_flat_gradient_allreduce_matches_global_batch():
     torch.nn.functional.mse_loss(ref(x), y).backward()
     assert torch.allclose(res["grad"], f.grad, rtol=1e-5, atol=1e-7)
     assert flat_ref.numel() <= f.numel
+
+
+def _worker_unused(rank, world, init_file, out_file):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    from medvae_disentangled_multimodal_amd import ddp
+    torch.manual_seed(5)
+    a, b = torch.nn.Linear(4, 4), torch.nn.Linear(4, 4)  # b (last => first bucket) is used by rank 0 only
+    model = torch.nn.ModuleList([a, b])
+    mod = _Mod(model)
+    dp = ddp.DataParallel(mod, bucket_bytes=16)
+    x = torch.full((2, 4), float(rank + 1))
+    mod.flat.zero_grad()
+    out = a(x)
+    if rank == 0:
+        out = b(out)
+    dp.begin_backward()
+    out.sum().backward()
+    dp.allreduce_gradients(mod.flat)  # same collective sequence on both ranks: no hang
+    if rank == 0:
+        torch.save({"b_w": b.weight._mvae_main_grad.clone(), "a_b": a.bias._mvae_main_grad.clone()}, out_file)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_overlap_with_rank_dependent_unused_parameters():
+    with tempfile.TemporaryDirectory() as d:
+        init_file = os.path.join(d, "init")
+        out_file = os.path.join(d, "out.pt")
+        mp.spawn(_worker_unused, args=(2, init_file, out_file), nprocs=2, join=True)
+        res = torch.load(out_file, weights_only=True)
+    torch.manual_seed(5)
+    a, b = torch.nn.Linear(4, 4), torch.nn.Linear(4, 4)
+    h0 = a(torch.full((2, 4), 1.0))
+    b(h0).sum().backward()
+    gb0 = b.weight.grad.clone()
+    a.zero_grad()
+    b.zero_grad()
+    a(torch.full((2, 4), 2.0)).sum().backward()
+    ga1 = a.bias.grad.clone()
+    a.zero_grad()
+    b(a(torch.full((2, 4), 1.0))).sum().backward()
+    ga0 = a.bias.grad.clone()
+    assert torch.allclose(res["b_w"], gb0, atol=1e-6)         # only rank 0 contributed
+    assert torch.allclose(res["a_b"], ga0 + ga1, atol=1e-6)   # summed over ranks
