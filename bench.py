@@ -63,6 +63,21 @@ BF16_DENSE_PEAK_TF = 2500.0
 PEAK_3XBF16_TF = BF16_DENSE_PEAK_TF / 3.0
 
 
+def _pmc_traffic(config):
+    """HBM bytes per gemm3x_kernel launch from the committed PMC passes (tools/pmc_traffic.sh:
+    FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc, separate passes) -- counters cannot be read inside
+    this timed run, so the profile of the same command is attached."""
+    path = os.path.join(ROOT, "profiles", f"r01_{config}_gemm_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        t = json.load(f)
+    return {"bytes_per_launch": round(t["traffic_bytes_per_launch"]), "unit": "B",
+            "fetch_bytes_per_launch": round(t["fetch_bytes_per_launch"]),
+            "write_bytes_per_launch": round(t["write_bytes_per_launch"]), "launches": t["launches"],
+            "source": os.path.relpath(path, ROOT)}
+
+
 def make_batch(cfg, device, gen):
     B, r = cfg["batch"], cfg["res"]
     C = cfg["kwargs"]["input_channels"]
@@ -188,7 +203,7 @@ def main():
         peak = BF16_DENSE_PEAK_TF if bf16 else PEAK_3XBF16_TF
         roofline = {"bound": "mfma", "kernel": "gemm3x_kernel (implicit-GEMM conv + attention bmm, all launches)",
                     "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-                    "frac": round(ach / peak, 4), "traffic": None,
+                    "frac": round(ach / peak, 4), "traffic": _pmc_traffic(args.config),
                     "peak_note": ("bf16 dense MFMA peak 2.5 PF/s (bf16 operands, fp32 accumulate)" if bf16 else
                                   "3xBF16 fp32-emulation ceiling = bf16 dense MFMA 2.5 PF/s / 3; "
                                   "native fp32 MFMA peak is 157.3 TF/s"),
