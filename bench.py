@@ -203,7 +203,8 @@ def main():
         peak = BF16_DENSE_PEAK_TF if bf16 else PEAK_3XBF16_TF
         roofline = {"bound": "mfma", "kernel": "gemm3x_kernel (implicit-GEMM conv + attention bmm, all launches)",
                     "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-                    "frac": round(ach / peak, 4), "traffic": _pmc_traffic(args.config),
+                    "frac": round(ach / peak, 4), "traffic": (_pmc_traffic(args.config) or {}).get("bytes_per_launch"),
+                    "traffic_unit": "HBM bytes per launch (PMC)", "traffic_detail": _pmc_traffic(args.config),
                     "peak_note": ("bf16 dense MFMA peak 2.5 PF/s (bf16 operands, fp32 accumulate)" if bf16 else
                                   "3xBF16 fp32-emulation ceiling = bf16 dense MFMA 2.5 PF/s / 3; "
                                   "native fp32 MFMA peak is 157.3 TF/s"),
