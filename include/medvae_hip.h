@@ -148,6 +148,17 @@ int mvae_lpips_dist(const float* f0, const float* f1, const float* w, float* sco
 int mvae_lpips_dist_bwd(const float* f0, const float* f1, const float* w, const float* gscore, float* df0, float* df1,
                         int nb, int npix, int c, void* stream);
 
+/* ---- validation metrics (validation_step, src/lightning_module.py:220-300; src/utils/metrics.py:14-73) ----
+ * SSIM exactly as torchmetrics 1.7.4 structural_similarity_index_measure (11x11 Gaussian, sigma 1.5,
+ * k1 0.01, k2 0.03, border-cropped map): per_image[b] = mean SSIM of image b (NHWC, h, w >= 11). */
+int mvae_ssim(const float* x, const float* y, int nb, int h, int w, int c, float data_range, float* per_image,
+              void* stream);
+/* compute_kl_metrics on [pixels][zc] latents (row stride ld): out = {kl_total, kl_mean, kl_std (unbiased),
+ * kl_per_dim_mean}, where the per-"sample" sums run over the channel dim (dim 1 of the NCHW latent). */
+int mvae_kl_stats(const float* mu, const float* logvar, long long ld, long long npix, int zc, float* out,
+                  void* workspace, size_t workspace_bytes, void* stream);
+size_t mvae_kl_stats_workspace_bytes(long long npix);
+
 #ifdef __cplusplus
 }
 #endif

@@ -55,6 +55,9 @@ SIGNATURES = {
     "mvae_maxpool_bwd": (I, [P, P, P, I, I, I, I, I, I, P]),
     "mvae_lpips_dist": (I, [P, P, P, P, I, I, I, F, P]),
     "mvae_lpips_dist_bwd": (I, [P, P, P, P, P, P, I, I, I, P]),
+    "mvae_ssim": (I, [P, P, I, I, I, I, F, P, P]),
+    "mvae_kl_stats": (I, [P, P, L, L, I, P, P, Z, P]),
+    "mvae_kl_stats_workspace_bytes": (Z, [L]),
 }
 
 

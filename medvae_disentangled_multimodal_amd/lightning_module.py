@@ -155,6 +155,70 @@ class VAELightningModule(_Base):
         return loss
 
     # ---------------------------------------------------------------------------------------
+    def _forward_batch(self, batch):
+        if len(batch) == 4:
+            x, labels, modality, modality_indices = batch
+        elif len(batch) == 3:
+            x, labels, modality = batch
+            modality_indices = None
+        else:
+            x, modality, modality_indices = batch[0], None, None
+        if self._kind == "indices" and modality is not None:
+            if modality_indices is None:
+                modality_indices = torch.argmax(modality, dim=1)
+            return x, self.model(x, modality_indices)
+        if self._kind == "condition" and modality is not None:
+            return x, self.model(x, modality)
+        return x, self.model(x)
+
+    def _eval_step(self, batch, split: str):
+        """validation_step / test_step (lightning_module.py:220-386): reconstruction + KL metrics on
+        the device (metrics.py), the objective for the `{split}/loss` monitor."""
+        from .metrics import compute_kl_metrics_device, compute_reconstruction_metrics_device
+        x, outputs = self._forward_batch(batch)
+        rec = outputs["reconstruction"]
+        mean = outputs["mean"] if "mean" in outputs else outputs["mu"]
+        logvar = outputs["logvar"]
+        for k, v in compute_reconstruction_metrics_device(x, rec).items():
+            self.log(f"{split}/{k}", v, prog_bar=False, logger=True, on_epoch=True)
+        for k, v in compute_kl_metrics_device(mean, logvar).items():
+            self.log(f"{split}/{k}", v, prog_bar=False, logger=True, on_epoch=True)
+        if isinstance(self.criterion, DisentangledVAELoss):
+            loss = self.criterion(outputs, x)["loss"]
+        elif isinstance(self.criterion, LPIPSWithDiscriminator):
+            loss, _ = self.criterion(inputs=x, reconstructions=rec, latent=outputs["z"],
+                                     posteriors=outputs["posterior"], optimizer_idx=0,
+                                     global_step=self.global_step_count, split=split)
+        elif isinstance(self.criterion, LPIPSLoss):
+            loss = self.criterion(x, rec)
+        else:
+            loss = self.criterion(inputs=x, reconstructions=rec, posteriors=outputs["posterior"],
+                                  priors=outputs["prior"])["loss"]
+        loss = torch.where(torch.isfinite(loss), loss, torch.full_like(loss, 1e6))
+        self.log(f"{split}/loss", loss, prog_bar=True, logger=True, on_epoch=True)
+        return outputs
+
+    def validation_step(self, batch, batch_idx: int):
+        return self._eval_step(batch, "val")
+
+    def test_step(self, batch, batch_idx: int):
+        return self._eval_step(batch, "test")
+
+    @torch.no_grad()
+    def evaluate(self, batch, split: str = "val"):
+        """Stand-alone validation of one batch (what Lightning's loop does around validation_step):
+        eval mode, no autograd, the configured precision; returns the logged `{split}/*` tensors."""
+        was_training = self.model.training
+        self.model.eval()
+        prev = ops.set_precision(self.precision)
+        try:
+            self._eval_step(batch, split)
+        finally:
+            ops.restore_math_mode(prev)
+            self.model.train(was_training)
+        return {k: v for k, v in self.logged.items() if k.startswith(f"{split}/")}
+
+    # ---------------------------------------------------------------------------------------
     def configure_optimizers(self):
         if self.flat is None:
             self.flat = FlatParameters(self.model)

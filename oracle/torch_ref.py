@@ -559,3 +559,43 @@ def lpips_vgg(W: Dict[str, Tensor], in0: Tensor, in1: Tensor, pre=(2.0, -1.0)) -
         d = (normalize(a) - normalize(b)) ** 2
         score = score + (d * W[f"lins.{k}"].view(1, -1, 1, 1)).sum(1, keepdim=True).mean((2, 3), keepdim=True)
     return score
+
+
+# --------------------------------------------------------------------------------------------
+# validation metrics: src/utils/metrics.py:14-73 (compute_reconstruction_metrics uses torchmetrics
+# 1.7.4 psnr/ssim, pinned in uv.lock:4071; not installed here -> restated from its published code:
+# functional/image/ssim.py _ssim_update with gaussian_kernel=True, sigma=1.5, k1=0.01, k2=0.03,
+# reflect pad (k-1)/2 then the map cropped by the same pad; psnr.py with data_range=1.0, base 10)
+# --------------------------------------------------------------------------------------------
+def ssim_torchmetrics(preds: Tensor, target: Tensor, data_range: float = 1.0) -> Tensor:
+    sigma, k1, k2 = 1.5, 0.01, 0.03
+    ks = int(3.5 * sigma + 0.5) * 2 + 1
+    pad = (ks - 1) // 2
+    c1, c2 = (k1 * data_range) ** 2, (k2 * data_range) ** 2
+    ch = preds.shape[1]
+    dist = torch.arange((1 - ks) / 2, (1 + ks) / 2, 1, dtype=preds.dtype)
+    gauss = torch.exp(-torch.pow(dist / sigma, 2) / 2)
+    g1 = (gauss / gauss.sum()).unsqueeze(0)
+    kernel = torch.matmul(g1.t(), g1).expand(ch, 1, ks, ks)
+    p = F.pad(preds, (pad, pad, pad, pad), mode="reflect")
+    t = F.pad(target, (pad, pad, pad, pad), mode="reflect")
+    out = F.conv2d(torch.cat((p, t, p * p, t * t, p * t)), kernel, groups=ch).split(preds.shape[0])
+    mu_p_sq, mu_t_sq, mu_pt = out[0].pow(2), out[1].pow(2), out[0] * out[1]
+    s_p = torch.clamp(out[2] - mu_p_sq, min=0.0)
+    s_t = torch.clamp(out[3] - mu_t_sq, min=0.0)
+    s_pt = out[4] - mu_pt
+    full = ((2 * mu_pt + c1) * (2 * s_pt + c2)) / ((mu_p_sq + mu_t_sq + c1) * (s_p + s_t + c2))
+    return full[..., pad:-pad, pad:-pad].reshape(preds.shape[0], -1).mean(-1).mean()
+
+
+def reconstruction_metrics(original: Tensor, reconstructed: Tensor) -> Dict[str, float]:
+    mse = F.mse_loss(reconstructed, original)
+    return {"mse": float(mse), "mae": float(F.l1_loss(reconstructed, original)),
+            "psnr": float(-10.0 * torch.log10(mse)), "ssim": float(ssim_torchmetrics(reconstructed, original, 1.0))}
+
+
+def kl_metrics(mean: Tensor, logvar: Tensor) -> Dict[str, float]:
+    kl = 0.5 * (mean.pow(2) + logvar.exp() - logvar - 1)
+    per_sample = kl.sum(dim=1)
+    return {"kl_total": float(kl.sum()), "kl_mean": float(per_sample.mean()), "kl_std": float(per_sample.std()),
+            "kl_per_dim_mean": float(kl.mean(dim=0).mean())}

@@ -57,3 +57,14 @@ def test_lpips_module_weight_names_and_refusal():
     assert m2.pretrained is True
     assert torch.equal(m2.conv3.weight, m.conv3.weight * 2)
     assert torch.equal(m2.lins[4], m.lins[4])
+
+
+def test_ssim_oracle_properties():
+    from oracle.torch_ref import ssim_torchmetrics
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(2, 3, 32, 32, generator=g, dtype=torch.float64)
+    assert float(ssim_torchmetrics(x, x)) == pytest.approx(1.0, abs=1e-12)
+    y = x + 0.3 * torch.randn(x.shape, generator=g, dtype=torch.float64)
+    s = float(ssim_torchmetrics(y, x))
+    assert 0.0 < s < 1.0
+    assert float(ssim_torchmetrics(x, y)) == pytest.approx(s, rel=1e-12)  # symmetric
