@@ -159,6 +159,20 @@ int mvae_kl_stats(const float* mu, const float* logvar, long long ld, long long 
                   void* workspace, size_t workspace_bytes, void* stream);
 size_t mvae_kl_stats_workspace_bytes(long long npix);
 
+/* ---- on-device MedMNIST batches (row (f)1: MedMNISTDataset.__getitem__ + transforms + collate,
+ * src/data/medmnist_data.py:16-72,186-251,319-375) ---------------------------------------------------
+ * store: resident uint8 images (sample s at byte sample_offset[s], [h][w][sample_channels[s]]);
+ * converts to sample_target_channels[s] (1/3), optional per-sample augmentation `aug` (12 floats per
+ * sample: flip, inverse-rotation rows scaled by (w/2, h/2), brightness f / 1-f, contrast f / 1-f,
+ * order, 2 pad; NULL = evaluation transform), Normalize(0.5, 0.5), zero-pads to cout channels.
+ * Writes x NHWC [nb][h][w][cout], onehot [nb][n_modalities], modality_idx [nb], labels [nb]. */
+int mvae_decode_batch(const unsigned char* store, const long long* sample_offset, const int* sample_channels,
+                      const int* sample_target_channels, const int* sample_modality, const long long* sample_label,
+                      const long long* index, const float* aug, int nb, int h, int w, int cout, int n_modalities,
+                      float* x, float* onehot, long long* modality_idx, long long* labels, void* workspace,
+                      size_t workspace_bytes, void* stream);
+size_t mvae_decode_batch_workspace_bytes(int nb, int h);
+
 #ifdef __cplusplus
 }
 #endif

@@ -58,6 +58,8 @@ SIGNATURES = {
     "mvae_ssim": (I, [P, P, I, I, I, I, F, P, P]),
     "mvae_kl_stats": (I, [P, P, L, L, I, P, P, Z, P]),
     "mvae_kl_stats_workspace_bytes": (Z, [L]),
+    "mvae_decode_batch": (I, [P, P, P, P, P, P, P, P, I, I, I, I, I, P, P, P, P, P, Z, P]),
+    "mvae_decode_batch_workspace_bytes": (Z, [I, I]),
 }
 
 

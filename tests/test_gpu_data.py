@@ -1,0 +1,111 @@
+"""On-device MedMNIST batches vs the CPU oracle of the reference's __getitem__ + transforms +
+collate (oracle/data_ref.py; torchvision restated, not installed). Synthetic uint8 datasets in the
+MedMNIST npz layout. Evaluation transform: bit-exact. Training transform with the SAME explicit
+random parameters: rotated coordinates may round differently only on exact ties (< 0.5 % of
+pixels), jitter values within 2e-6."""
+import math
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import data_ref as D
+
+pytestmark = pytest.mark.gpu
+
+
+def _arrays(size, seed=0):
+    rng = np.random.default_rng(seed)
+    return {
+        "chestmnist": (rng.integers(0, 256, (5, size, size), dtype=np.uint8), rng.integers(0, 2, (5, 14))),
+        "pathmnist": (rng.integers(0, 256, (4, size, size, 3), dtype=np.uint8), rng.integers(0, 9, (4, 1))),
+        "octmnist": (rng.integers(0, 256, (3, size, size), dtype=np.uint8), rng.integers(0, 4, (3, 1))),
+        "organamnist": (rng.integers(0, 256, (3, size, size, 3), dtype=np.uint8), rng.integers(0, 11, (3, 1))),
+    }
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _oracle_batch(arrs, names, index, augs=None):
+    flat = []
+    for n in names:
+        imgs, labels = arrs[n]
+        for k in range(len(imgs)):
+            flat.append((n, imgs[k]))
+    ims = [D.sample(flat[i][1], flat[i][0], None if augs is None else augs[j]) for j, i in enumerate(index)]
+    return D.collate(ims)
+
+
+@pytest.mark.parametrize("size", [28, 64])
+def test_eval_batch_bit_exact(dev, size):
+    from medvae_disentangled_multimodal_amd import data
+    arrs = _arrays(size)
+    names = list(arrs)
+    with tempfile.TemporaryDirectory() as d:  # through the npz files, MedMNIST layout
+        for n, (im, lab) in arrs.items():
+            np.savez(data.npz_path(d, n, size), train_images=im, train_labels=lab)
+        ds = data.DeviceMedMNIST(names, "train", size, d, device=dev)
+    assert len(ds) == 15
+    index = [0, 6, 9, 14, 3, 12]
+    x, labels, onehot, midx = ds.batch(index)
+    ref = _oracle_batch(arrs, names, index)
+    assert x.shape == ref.shape and x.is_contiguous(memory_format=torch.channels_last)
+    diff = (x.cpu() - ref).abs()
+    assert torch.equal(x.cpu(), ref), (int((diff > 0).sum()), float(diff.max()), torch.nonzero(diff)[:5].tolist())
+    mods = [data.MODALITIES.index(n) for n in names for _ in range(len(arrs[n][0]))]
+    assert midx.cpu().tolist() == [mods[i] for i in index]
+    assert torch.equal(onehot.cpu(), torch.nn.functional.one_hot(midx.cpu(), 12).float())
+    all_labels = np.concatenate([data.standardize_labels(arrs[n][1]) for n in names])
+    assert labels.view(-1).cpu().tolist() == all_labels[index].tolist()
+    # gray-only batch keeps 1 channel (no padding), as the collate does
+    x1, *_ = ds.batch([0, 1])
+    assert x1.shape[1] == 1
+
+
+def test_train_batch_matches_given_parameters(dev):
+    from medvae_disentangled_multimodal_amd import data
+    size = 64
+    arrs = _arrays(size, 1)
+    names = list(arrs)
+    ds = data.DeviceMedMNIST(names, "train", size, arrays=arrs, device=dev)
+    index = list(range(15))
+    rng = np.random.default_rng(5)
+    aug = data.draw_augmentation(len(index), size, size, rng)
+    # the same parameters in the oracle's form
+    rng = np.random.default_rng(5)
+    params = []
+    for _ in index:
+        flip = rng.random() < 0.5
+        angle = rng.uniform(-10.0, 10.0)
+        b, c = rng.uniform(0.9, 1.1), rng.uniform(0.9, 1.1)
+        perm = list(rng.permutation(4))
+        params.append((flip, angle, b, c, perm.index(0) < perm.index(1)))
+    x, *_ = ds.batch(index, aug)
+    ref = _oracle_batch(arrs, names, index, params)
+    diff = (x.cpu() - ref).abs()
+    assert float((diff > 2e-6).float().mean()) < 5e-3
+    assert float(diff.median()) == 0.0
+
+
+def test_loader_sharding_and_epochs(dev):
+    from medvae_disentangled_multimodal_amd import data
+    arrs = _arrays(28, 2)
+    ds = data.DeviceMedMNIST(list(arrs), "train", 28, arrays=arrs, device=dev)
+    seen = []
+    for rank in range(2):
+        dl = data.DeviceDataLoader(ds, batch_size=4, shuffle=True, augment=True, seed=3, num_replicas=2, rank=rank)
+        n = 0
+        for x, labels, onehot, midx in dl:
+            assert x.shape[0] <= 4 and torch.isfinite(x).all()
+            assert float(x.min()) >= -1.0 and float(x.max()) <= 1.0
+            n += x.shape[0]
+        assert n == math.ceil(15 / 2)
+        seen += dl.sampler.indices()
+    assert sorted(set(seen)) == list(range(15))

@@ -83,3 +83,20 @@ def test_ops_refuse_cpu_tensors():
     w = torch.zeros(4, 4, 3, 3)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         ops.conv2d(x, w, None, ops.ConvGeom(3, 3, 1, 1, 1, 1, 1))
+
+
+def test_distributed_sampler_semantics():
+    """data.DistributedSampler == torch.utils.data.DistributedSampler(shuffle=True, drop_last=False)."""
+    import torch.utils.data as tud
+    from medvae_disentangled_multimodal_amd.data import DistributedSampler, standardize_labels
+    ds = list(range(23))
+    for world in (1, 2, 4):
+        for rank in range(world):
+            ref = tud.DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=True, seed=7)
+            ref.set_epoch(3)
+            mine = DistributedSampler(23, world, rank, True, 7)
+            mine.set_epoch(3)
+            assert mine.indices() == list(iter(ref))
+    import numpy as np
+    assert standardize_labels(np.array([[3], [1]])).tolist() == [3, 1]
+    assert standardize_labels(np.array([[0, 1, 1], [0, 0, 0]])).tolist() == [1, 0]
