@@ -105,7 +105,8 @@ int mvae_reparam_bwd(const float* dz, const float* eps, const float* logvar, lon
                      long long npix, int zc, void* stream);
 /* out[0] = scale * sum(term): kind 0 = KL(N(mu,e^{lv/2})||N(0,1)) (vae_losses.py:58),
  * 1 = squared error (mse, :41), 2 = absolute error (l1, :43), 3 = -0.5*(1+lv-mu^2-e^lv)
- * (DisentangledVAELoss, disentangled_conditional_vae.py:524). Device scalar out, no host sync. */
+ * (DisentangledVAELoss, disentangled_conditional_vae.py:524), adversarial terms on logits a
+ * (vae_losses.py:297-352): 4 = relu(1-a), 5 = relu(1+a), 6 = a. Device scalar out, no host sync. */
 int mvae_loss_reduce(int kind, const float* a, const float* b, long long ld, long long npix, int zc,
                      double scale, float* out, void* workspace, size_t workspace_bytes, void* stream);
 size_t mvae_reduce_workspace_bytes(void);
@@ -172,6 +173,24 @@ int mvae_decode_batch(const unsigned char* store, const long long* sample_offset
                       float* x, float* onehot, long long* modality_idx, long long* labels, void* workspace,
                       size_t workspace_bytes, void* stream);
 size_t mvae_decode_batch_workspace_bytes(int nb, int h);
+
+/* Gradient of the adversarial terms (kinds 4-6) w.r.t. the logits, times gscale[0] * mult. */
+int mvae_adv_bwd(int kind, const float* a, const float* gscale, double mult, float* da, long long n, void* stream);
+
+/* ---- adversarial branch (row (f)2): NLayerDiscriminator (src/models/discriminator.py:11-82) -------
+ * BatchNorm2d over NHWC rows (N*H*W) fused with LeakyReLU(slope; slope < 0 = none). training: batch
+ * statistics -> mean/rstd (saved for backward), running stats updated (momentum, unbiased var) when
+ * run_mean != NULL; training == 0: running statistics. Backward (training mode) accumulates into
+ * dgamma/dbeta. */
+int mvae_batch_norm_fwd_nhwc(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd,
+                             float* run_mean, float* run_var, long long rows, int c, float eps, float momentum,
+                             int training, float slope, void* workspace, size_t workspace_bytes, void* stream);
+int mvae_batch_norm_bwd_nhwc(const float* x, const float* y, const float* dy, const float* gamma, const float* mean,
+                             const float* rstd, float* dx, float* dgamma, float* dbeta, long long rows, int c,
+                             float slope, void* workspace, size_t workspace_bytes, void* stream);
+size_t mvae_batch_norm_workspace_bytes(long long rows, int c);
+int mvae_leaky_relu_fwd(const float* x, float* y, float slope, long long n, void* stream);
+int mvae_leaky_relu_bwd(const float* y, const float* dy, float* dx, float slope, long long n, void* stream);
 
 #ifdef __cplusplus
 }

@@ -60,6 +60,12 @@ SIGNATURES = {
     "mvae_kl_stats_workspace_bytes": (Z, [L]),
     "mvae_decode_batch": (I, [P, P, P, P, P, P, P, P, I, I, I, I, I, P, P, P, P, P, Z, P]),
     "mvae_decode_batch_workspace_bytes": (Z, [I, I]),
+    "mvae_adv_bwd": (I, [I, P, P, D, P, L, P]),
+    "mvae_batch_norm_fwd_nhwc": (I, [P, P, P, P, P, P, P, P, L, I, F, F, I, F, P, Z, P]),
+    "mvae_batch_norm_bwd_nhwc": (I, [P, P, P, P, P, P, P, P, P, L, I, F, P, Z, P]),
+    "mvae_batch_norm_workspace_bytes": (Z, [L, I]),
+    "mvae_leaky_relu_fwd": (I, [P, P, F, L, P]),
+    "mvae_leaky_relu_bwd": (I, [P, P, P, F, L, P]),
 }
 
 

@@ -47,7 +47,8 @@ __global__ void __launch_bounds__(256) reparam_bwd_kernel(const float* __restric
 }
 
 // kind 0: KL elementwise sum (torch.distributions form) ; kind 1: squared error sum ;
-// kind 2: absolute error sum ; kind 3: "-0.5*(1 + lv - mu^2 - exp(lv))" sum (DisentangledVAELoss)
+// kind 2: absolute error sum ; kind 3: "-0.5*(1 + lv - mu^2 - exp(lv))" sum (DisentangledVAELoss);
+// kinds 4-6 (discriminator hinge / generator terms, vae_losses.py:297-352): relu(1-a), relu(1+a), a
 __global__ void __launch_bounds__(256) reduce_partial_kernel(int kind, const float* __restrict__ a,
                                                              const float* __restrict__ b, long long ld, long long npix,
                                                              int zc, double* __restrict__ part) {
@@ -66,6 +67,9 @@ __global__ void __launch_bounds__(256) reduce_partial_kernel(int kind, const flo
       } else {
         acc += 1.f + l - m * m - expf(l);
       }
+    } else if (kind >= 4) {  // adversarial terms on logits a: relu(1 - a), relu(1 + a), a
+      const float v = a[e];
+      acc += kind == 4 ? (double)fmaxf(1.f - v, 0.f) : kind == 5 ? (double)fmaxf(1.f + v, 0.f) : (double)v;
     } else {
       const float d = a[e] - b[e];
       acc += kind == 1 ? (double)d * d : (double)fabsf(d);
@@ -99,6 +103,17 @@ __global__ void __launch_bounds__(256) kl_bwd_kernel(const float* __restrict__ m
     const float s = expf(0.5f * l);
     dmu[e] = g * m;
     dlv[e] = g * 0.5f * (s * s - 1.f);
+  }
+}
+
+// d/da of the adversarial terms (kinds 4-6) times gscale[0] * mult
+__global__ void __launch_bounds__(256) adv_bwd_kernel(int kind, const float* __restrict__ a,
+                                                      const float* __restrict__ gscale, double mult,
+                                                      float* __restrict__ da, long long n) {
+  const float g = (float)(gscale[0] * mult);
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const float v = a[e];
+    da[e] = kind == 4 ? (1.f - v > 0.f ? -g : 0.f) : kind == 5 ? (1.f + v > 0.f ? g : 0.f) : g;
   }
 }
 
@@ -143,7 +158,7 @@ int mvae_reparam_bwd(const float* dz, const float* eps, const float* logvar, lon
 // dense [n] (npix = n, zc = 1, ld unused).
 int mvae_loss_reduce(int kind, const float* a, const float* b, long long ld, long long npix, int zc, double scale,
                      float* out, void* workspace, size_t workspace_bytes, void* stream) {
-  if (kind < 0 || kind > 3 || npix <= 0 || zc <= 0) { set_error("loss_reduce: bad args"); return MVAE_EINVAL; }
+  if (kind < 0 || kind > 6 || npix <= 0 || zc <= 0) { set_error("loss_reduce: bad args"); return MVAE_EINVAL; }
   if (workspace_bytes < RED_BLOCKS * sizeof(double)) { set_error("loss_reduce: workspace"); return MVAE_EWORKSPACE; }
   hipStream_t st = (hipStream_t)stream;
   const long long n = npix * zc;
@@ -167,6 +182,12 @@ int mvae_recon_bwd(int kind, const float* a, const float* b, const float* gscale
   if ((kind != 1 && kind != 2) || n <= 0) { set_error("recon_bwd: bad args"); return MVAE_EINVAL; }
   hipLaunchKernelGGL(recon_bwd_kernel, dim3(egrid(n)), dim3(256), 0, (hipStream_t)stream, kind, a, b, gscale, mult, da,
                      n);
+  return launch_status();
+}
+
+int mvae_adv_bwd(int kind, const float* a, const float* gscale, double mult, float* da, long long n, void* stream) {
+  if (kind < 4 || kind > 6 || n <= 0) { set_error("adv_bwd: bad args"); return MVAE_EINVAL; }
+  hipLaunchKernelGGL(adv_bwd_kernel, dim3(egrid(n)), dim3(256), 0, (hipStream_t)stream, kind, a, gscale, mult, da, n);
   return launch_status();
 }
 

@@ -58,7 +58,11 @@ class DataParallel:
         flat = module.flat
         if self.world > 1:
             dist.broadcast(flat.data, src=0, group=group)
+            if getattr(module, "flat_d", None) is not None:  # discriminator of the adversarial branch
+                dist.broadcast(module.flat_d.data, src=0, group=group)
         module.optimizer.grad_scale = 1.0 / self.world
+        if getattr(module, "optimizer_d", None) is not None:
+            module.optimizer_d.grad_scale = 1.0 / self.world
         module.process_group = self
         self.overlap = overlap and self.world > 1
         self._plan(flat)
@@ -121,6 +125,14 @@ class DataParallel:
         self.launched[b] = True
         g = self.module.flat.grad[lo:hi]
         self._works.append(dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+
+    def allreduce_flat(self, flat):
+        """Synchronous bucketed all-reduce of another flat gradient buffer (the discriminator's)."""
+        if self.world == 1:
+            return
+        g = flat.grad
+        for s in range(0, g.numel(), self.bucket_elems):
+            dist.all_reduce(g[s:s + self.bucket_elems], op=dist.ReduceOp.SUM, group=self.group)
 
     def allreduce_gradients(self, flat):
         if self.world == 1:

@@ -99,7 +99,9 @@ class VAELightningModule(_Base):
                 lpips_net=self.loss_config.get("lpips_net", "alex"))
         else:
             raise ValueError(f"Unknown/unsupported loss type on the MI355X path: {t}")
-        self.use_discriminator = False
+        self.use_discriminator = t == "lpips_discriminator"
+        self.flat_d = None
+        self.optimizer_d = None
 
     # ---------------------------------------------------------------------------------------
     def forward(self, x, condition=None, **kw):
@@ -155,7 +157,7 @@ class VAELightningModule(_Base):
         return loss
 
     # ---------------------------------------------------------------------------------------
-    def _forward_batch(self, batch):
+    def _forward_batch(self, batch, eps=None):
         if len(batch) == 4:
             x, labels, modality, modality_indices = batch
         elif len(batch) == 3:
@@ -163,13 +165,15 @@ class VAELightningModule(_Base):
             modality_indices = None
         else:
             x, modality, modality_indices = batch[0], None, None
+        kw = {} if eps is None else {"eps": eps}
         if self._kind == "indices" and modality is not None:
             if modality_indices is None:
                 modality_indices = torch.argmax(modality, dim=1)
-            return x, self.model(x, modality_indices)
+            self._usage = modality_indices
+            return x, self.model(x, modality_indices, **kw)
         if self._kind == "condition" and modality is not None:
-            return x, self.model(x, modality)
-        return x, self.model(x)
+            return x, self.model(x, modality, **kw)
+        return x, self.model(x, **kw)
 
     def _eval_step(self, batch, split: str):
         """validation_step / test_step (lightning_module.py:220-386): reconstruction + KL metrics on
@@ -232,6 +236,11 @@ class VAELightningModule(_Base):
             raise ValueError(f"Unknown optimizer: {oc['type']}")
         opt.max_grad_norm = self.gradient_clip_val
         self.optimizer = opt
+        if self.use_discriminator and self.optimizer_d is None:
+            # lightning_module.py:427-433: Adam(lr * 0.5, betas (0.5, 0.999)) over the discriminator
+            disc = self.criterion.discriminator.to(self.flat.device)
+            self.flat_d = FlatParameters(disc)
+            self.optimizer_d = Adam(self.flat_d, lr=oc["lr"] * 0.5, betas=(0.5, 0.999))
         self.scheduler = get_scheduler(opt, self.scheduler_config)
         if self.scheduler is not None:
             return [opt], [{"scheduler": self.scheduler, "monitor": "val/loss", "interval": "epoch",
@@ -250,10 +259,57 @@ class VAELightningModule(_Base):
         used = (pm == -1) | ((pm >= 0) & present[pm.clamp_min(0)])
         return used.to(torch.int32)
 
+    def _adversarial_fit_step(self, batch, eps=None) -> torch.Tensor:
+        """The reference's manual-optimisation step (lightning_module.py:131-175) once the
+        discriminator is active: generator step (VAE optimizer), then discriminator step. As under
+        Lightning's manual optimisation, no automatic gradient clipping; global_step counts both
+        optimizer steps."""
+        disc = self.criterion.discriminator
+        self.model.train()
+        disc.train()
+        x, outputs = self._forward_batch(batch, eps)
+        rec = outputs["reconstruction"]
+        loss_g, log_g = self.criterion(inputs=x, reconstructions=rec, latent=outputs["z"],
+                                       posteriors=outputs["posterior"], optimizer_idx=0,
+                                       global_step=self.global_step_count, last_layer=self.model.decoder.conv_out,
+                                       split="train")
+        self.optimizer.zero_grad()
+        if self.process_group is not None:
+            self.process_group.begin_backward()
+        loss_g.backward()
+        if self.process_group is not None:
+            self.process_group.allreduce_gradients(self.flat)
+        clip = self.optimizer.max_grad_norm
+        self.optimizer.max_grad_norm = None
+        try:
+            self.optimizer.step(used=self._used_mask())
+        finally:
+            self.optimizer.max_grad_norm = clip
+        loss_d, log_d = self.criterion(inputs=x, reconstructions=rec.detach(), latent=outputs["z"].detach(),
+                                       posteriors=outputs["posterior"], optimizer_idx=1,
+                                       global_step=self.global_step_count, last_layer=None, split="train")
+        self.optimizer_d.zero_grad()
+        loss_d.backward()
+        if self.process_group is not None:
+            self.process_group.allreduce_flat(self.flat_d)
+        self.optimizer_d.step()
+        for k, v in {**log_g, **log_d}.items():
+            self.log(k, v)
+        self._last_outputs = outputs
+        self.global_step_count += 2
+        return loss_g
+
     def fit_step(self, batch, batch_idx: int = 0, eps: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """One automatic-optimisation step of Lightning's loop, fused."""
+        """One optimisation step of Lightning's loop, fused (automatic optimisation, or the
+        reference's manual generator/discriminator pair once the discriminator is active)."""
         if self.optimizer is None:
             self.configure_optimizers()
+        if self.use_discriminator and self.global_step_count >= self.criterion.discriminator_iter_start:
+            prev = ops.set_precision(self.precision)
+            try:
+                return self._adversarial_fit_step(batch, eps)
+            finally:
+                ops.restore_math_mode(prev)
         self.model.train()
         prev = ops.set_precision(self.precision)
         try:

@@ -95,11 +95,15 @@ class LPIPSLoss(nn.Module):
 
 
 class LPIPSWithDiscriminator(nn.Module):
-    """Generator objective of the reference's combined loss (vae_losses.py:214-362):
-    perceptual_factor * LPIPS + kl_factor * KL(q || N(0, I)).sum() / B (+ d_weight * g_loss once
-    global_step >= discriminator_iter_start). The reference calls `posteriors.kl()`, which a
-    torch Normal does not have; the closed-form KL is used. The
-    adversarial branch (NLayerDiscriminator, adaptive weight) is the next scope row and raises."""
+    """The reference's combined objective (vae_losses.py:214-382) on the HIP kernels.
+
+    optimizer_idx 0 (generator): perceptual_factor * LPIPS + kl_factor * KL(q || N(0, I)).sum() / B
+    + d_weight * g_loss, g_loss = -mean(D(rec)) and the adaptive d_weight = |dNLL/dW| / (|dG/dW| + 1e-4)
+    (clamped to [0, 1e4], times discriminator_factor) w.r.t. the decoder's last conv, once global_step
+    >= discriminator_iter_start. optimizer_idx 1 (discriminator): hinge loss
+    0.5 * (mean(relu(1 - D(x))) + mean(relu(1 + D(rec)))) once active, else 0.
+    The reference calls `posteriors.kl()`, which a torch Normal does not have; the closed-form KL is
+    used."""
 
     def __init__(self, discriminator_factor: float = 1.0, perceptual_factor: float = 1.0, kl_factor: float = 1.0,
                  discriminator_iter_start: int = 50001, use_biomedclip_loss: bool = False,
@@ -108,25 +112,60 @@ class LPIPSWithDiscriminator(nn.Module):
         super().__init__()
         if use_biomedclip_loss:
             raise NotImplementedError("BiomedCLIP loss is outside the MI355X hot path")
+        from .discriminator import NLayerDiscriminator
         self.discriminator_factor = discriminator_factor
         self.perceptual_factor = perceptual_factor
         self.kl_factor = kl_factor
         self.discriminator_iter_start = discriminator_iter_start
         self.perceptual_loss = LPIPSLoss(net=lpips_net, weights=lpips_weights, allow_synthetic=allow_synthetic_lpips)
+        if discriminator_config is None:
+            discriminator_config = {"input_nc": 3, "ndf": 64, "n_layers": 3}
+        self.discriminator = NLayerDiscriminator(**discriminator_config)
+
+    def calculate_adaptive_weight(self, nll_loss, g_loss, last_layer):
+        with ops.autograd_weight_grads():  # the probes must not touch the flat gradient buffer
+            nll_grads = torch.autograd.grad(nll_loss, last_layer.weight, retain_graph=True)[0]
+            g_grads = torch.autograd.grad(g_loss, last_layer.weight, retain_graph=True)[0]
+        d_weight = torch.norm(nll_grads) / (torch.norm(g_grads) + 1e-4)
+        return torch.clamp(d_weight, 0.0, 1e4).detach()
 
     def forward(self, inputs, reconstructions, latent=None, posteriors=None, optimizer_idx: int = 0,
                 global_step: int = 0, last_layer=None, split: str = "train", **kwargs):
         bsz = inputs.shape[0]
         d_valid = global_step >= self.discriminator_iter_start
-        if d_valid:
-            raise NotImplementedError("adversarial branch (NLayerDiscriminator) is not built yet")
-        if optimizer_idx == 1:
-            zero = torch.zeros((), device=inputs.device)
-            return zero, {f"{split}/d_loss": zero}
-        p_loss = self.perceptual_loss(inputs, reconstructions)
-        kl_loss = ops.kl_closed_form_sum(posteriors._mvae_mean, posteriors._mvae_logvar, bsz)
         zero = torch.zeros((), device=inputs.device)
-        loss = self.perceptual_factor * p_loss + self.kl_factor * kl_loss
-        log = {f"{split}/total_loss": loss.detach(), f"{split}/kl_loss": kl_loss.detach(),
-               f"{split}/p_loss": p_loss.detach(), f"{split}/d_weight": zero, f"{split}/g_loss": zero}
-        return loss, log
+        if optimizer_idx == 0:
+            p_loss = self.perceptual_loss(inputs, reconstructions)
+            kl_loss = ops.kl_closed_form_sum(posteriors._mvae_mean, posteriors._mvae_logvar, bsz)
+            d_weight, g_loss = zero, zero
+            if d_valid:
+                rec = reconstructions.repeat(1, 3, 1, 1) if reconstructions.shape[1] == 1 else reconstructions
+                dparams = list(self.discriminator.parameters())
+                flags = [p.requires_grad for p in dparams]
+                for p in dparams:  # the generator step updates only the VAE: skip D's weight gradients
+                    p.requires_grad_(False)
+                try:
+                    g_loss = ops.neg_mean(self.discriminator(rec))
+                finally:
+                    for p, f in zip(dparams, flags):
+                        p.requires_grad_(f)
+                try:
+                    d_weight = self.calculate_adaptive_weight(p_loss, g_loss, last_layer) if last_layer is not None \
+                        else zero
+                except RuntimeError:
+                    d_weight = zero
+                d_weight = d_weight * self.discriminator_factor
+            loss = self.perceptual_factor * p_loss + self.kl_factor * kl_loss + d_weight * g_loss
+            log = {f"{split}/total_loss": loss.detach(), f"{split}/kl_loss": kl_loss.detach(),
+                   f"{split}/p_loss": p_loss.detach(), f"{split}/d_weight": d_weight.detach(),
+                   f"{split}/g_loss": g_loss.detach()}
+            return loss, log
+        if d_valid:
+            x = inputs.repeat(1, 3, 1, 1) if inputs.shape[1] == 1 else inputs
+            r = reconstructions.repeat(1, 3, 1, 1) if reconstructions.shape[1] == 1 else reconstructions
+            logits_real = self.discriminator(x.contiguous().detach())
+            logits_fake = self.discriminator(r.contiguous().detach())
+            d_loss = 0.5 * (ops.hinge_real(logits_real) + ops.hinge_fake(logits_fake))
+        else:
+            d_loss = zero
+        return d_loss, {f"{split}/d_loss": d_loss.detach()}

@@ -88,8 +88,28 @@ class _timed:
         return False
 
 
+_WEIGHT_GRADS_TO_AUTOGRAD = [False]
+
+
 def _main_grad(p: torch.Tensor):
+    if _WEIGHT_GRADS_TO_AUTOGRAD[0]:
+        return None
     return getattr(p, "_mvae_main_grad", None)
+
+
+class autograd_weight_grads:
+    """Within this context the ops hand parameter gradients back to autograd instead of accumulating
+    them into the flat gradient buffer -- for `torch.autograd.grad(loss, param)` probes such as the
+    adaptive adversarial weight (vae_losses.py:364-382)."""
+
+    def __enter__(self):
+        self.prev = _WEIGHT_GRADS_TO_AUTOGRAD[0]
+        _WEIGHT_GRADS_TO_AUTOGRAD[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _WEIGHT_GRADS_TO_AUTOGRAD[0] = self.prev
+        return False
 
 
 # Called with each parameter whose flat-slot gradient the backward pass has just finished writing
@@ -663,3 +683,120 @@ class LpipsDistFn(torch.autograd.Function):
 
 def lpips_dist(f0, f1, w):
     return LpipsDistFn.apply(f0, f1, w)
+
+
+# ------------------------------------------------------------------------------------------
+# adversarial branch: BatchNorm2d(+LeakyReLU), LeakyReLU, hinge / mean terms (row (f)2)
+# ------------------------------------------------------------------------------------------
+class BatchNormFn(torch.autograd.Function):
+    """nn.BatchNorm2d (+ the following in-place LeakyReLU when slope >= 0) over NHWC."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, run_mean, run_var, training: bool, momentum: float, eps: float, slope: float):
+        _check(x, "batch_norm input")
+        x = nhwc(x)
+        n, c, h, w = x.shape
+        rows = n * h * w
+        y = torch.empty_like(x, memory_format=CL)
+        mean = torch.empty(c, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        ws = ARENA.get("bn", _lib.query("mvae_batch_norm_workspace_bytes", rows, c), x.device)
+        _lib.call("mvae_batch_norm_fwd_nhwc", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
+                  mean.data_ptr(), rstd.data_ptr(), _ptr(run_mean), _ptr(run_var), rows, c, float(eps),
+                  float(momentum), int(training), float(slope), ws.data_ptr(), ws.numel(), _stream(x))
+        ctx.save_for_backward(x, y, gamma, mean, rstd)
+        ctx.training, ctx.slope = training, slope
+        ctx.gamma_ref, ctx.beta_ref = gamma, beta
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, gamma, mean, rstd = ctx.saved_tensors
+        if not ctx.training:
+            raise RuntimeError("BatchNorm backward is built for training-mode statistics only")
+        dy = nhwc(dy)
+        n, c, h, w = x.shape
+        rows = n * h * w
+        dx = torch.empty_like(x, memory_format=CL)
+        dg = _main_grad(ctx.gamma_ref) if ctx.needs_input_grad[1] else None
+        db = _main_grad(ctx.beta_ref) if ctx.needs_input_grad[2] else None
+        dg_ret = db_ret = None
+        if ctx.needs_input_grad[1] and dg is None:
+            dg = dg_ret = torch.zeros(c, device=x.device, dtype=torch.float32)
+        if ctx.needs_input_grad[2] and db is None:
+            db = db_ret = torch.zeros(c, device=x.device, dtype=torch.float32)
+        ws = ARENA.get("bn", _lib.query("mvae_batch_norm_workspace_bytes", rows, c), x.device)
+        _lib.call("mvae_batch_norm_bwd_nhwc", x.data_ptr(), y.data_ptr(), dy.data_ptr(), gamma.data_ptr(),
+                  mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(dg), _ptr(db), rows, c, float(ctx.slope),
+                  ws.data_ptr(), ws.numel(), _stream(x))
+        if ctx.needs_input_grad[1] and dg_ret is None:
+            _grad_done(ctx.gamma_ref)
+        if ctx.needs_input_grad[2] and db_ret is None:
+            _grad_done(ctx.beta_ref)
+        return dx, dg_ret, db_ret, None, None, None, None, None, None
+
+
+def batch_norm(x, gamma, beta, run_mean, run_var, training, momentum=0.1, eps=1e-5, slope=-1.0):
+    return BatchNormFn.apply(x, gamma, beta, run_mean, run_var, training, momentum, eps, slope)
+
+
+class LeakyReluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, slope: float):
+        _check(x, "leaky_relu input")
+        x = nhwc(x)
+        y = _like_cl(x)
+        _lib.call("mvae_leaky_relu_fwd", x.data_ptr(), y.data_ptr(), float(slope), x.numel(), _stream(x))
+        ctx.save_for_backward(y)
+        ctx.slope = slope
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = nhwc(dy.float())
+        dx = _like_cl(y)
+        _lib.call("mvae_leaky_relu_bwd", y.data_ptr(), dy.data_ptr(), dx.data_ptr(), float(ctx.slope), y.numel(),
+                  _stream(y))
+        return dx, None
+
+
+def leaky_relu(x, slope=0.2):
+    return LeakyReluFn.apply(x, slope)
+
+
+class AdvTermFn(torch.autograd.Function):
+    """scale * sum(term(a)): kind 4 relu(1-a), 5 relu(1+a), 6 a (hinge / generator terms)."""
+
+    @staticmethod
+    def forward(ctx, a, kind: int, scale: float):
+        _check(a, "logits")
+        a = a.contiguous() if a.dim() != 4 else nhwc(a)
+        out = torch.empty((), device=a.device, dtype=torch.float32)
+        ws = ARENA.get("red", _lib.query("mvae_reduce_workspace_bytes"), a.device)
+        _lib.call("mvae_loss_reduce", kind, a.data_ptr(), a.data_ptr(), 1, a.numel(), 1, float(scale), out.data_ptr(),
+                  ws.data_ptr(), ws.numel(), _stream(a))
+        ctx.save_for_backward(a)
+        ctx.kind, ctx.scale = kind, scale
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (a,) = ctx.saved_tensors
+        g = g.contiguous().float()
+        da = _like_cl(a)
+        _lib.call("mvae_adv_bwd", ctx.kind, a.data_ptr(), g.data_ptr(), float(ctx.scale), da.data_ptr(), a.numel(),
+                  _stream(a))
+        return da, None, None
+
+
+def hinge_real(logits):  # mean(relu(1 - logits))
+    return AdvTermFn.apply(logits, 4, 1.0 / logits.numel())
+
+
+def hinge_fake(logits):  # mean(relu(1 + logits))
+    return AdvTermFn.apply(logits, 5, 1.0 / logits.numel())
+
+
+def neg_mean(logits):  # -mean(logits)
+    return AdvTermFn.apply(logits, 6, -1.0 / logits.numel())

@@ -599,3 +599,28 @@ def kl_metrics(mean: Tensor, logvar: Tensor) -> Dict[str, float]:
     per_sample = kl.sum(dim=1)
     return {"kl_total": float(kl.sum()), "kl_mean": float(per_sample.mean()), "kl_std": float(per_sample.std()),
             "kl_per_dim_mean": float(kl.mean(dim=0).mean())}
+
+
+# --------------------------------------------------------------------------------------------
+# adversarial branch: NLayerDiscriminator (src/models/discriminator.py:11-82) and the hinge /
+# generator terms + adaptive weight of LPIPSWithDiscriminator (src/losses/vae_losses.py:297-382)
+# --------------------------------------------------------------------------------------------
+def discriminator(W: Dict[str, Tensor], x: Tensor, n_layers: int = 3, training: bool = True,
+                  running: Optional[Dict[str, Tensor]] = None, momentum: float = 0.1) -> Tensor:
+    """W: main.{i}.weight/.bias (+ BatchNorm running stats in `running`, updated in place)."""
+    i = 0
+    h = F.leaky_relu(F.conv2d(x, W["main.0.weight"], W["main.0.bias"], stride=2, padding=1), 0.2)
+    i = 2
+    for n in range(1, n_layers + 1):
+        stride = 2 if n < n_layers else 1
+        h = F.conv2d(h, W[f"main.{i}.weight"], W.get(f"main.{i}.bias"), stride=stride, padding=1)
+        rm = running[f"main.{i + 1}.running_mean"] if running is not None else None
+        rv = running[f"main.{i + 1}.running_var"] if running is not None else None
+        h = F.batch_norm(h, rm, rv, W[f"main.{i + 1}.weight"], W[f"main.{i + 1}.bias"], training, momentum, 1e-5)
+        h = F.leaky_relu(h, 0.2)
+        i += 3
+    return F.conv2d(h, W[f"main.{i}.weight"], W[f"main.{i}.bias"], stride=1, padding=1)
+
+
+def hinge_d_loss(logits_real: Tensor, logits_fake: Tensor) -> Tensor:
+    return 0.5 * (torch.mean(F.relu(1.0 - logits_real)) + torch.mean(F.relu(1.0 + logits_fake)))
