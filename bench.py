@@ -168,7 +168,7 @@ def main():
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    loss_v = float(loss)
+    loss_v = float(loss.detach())
 
     roofline = None
     bf16 = cfg.get("precision", "32") == "bf16-mixed"
@@ -183,9 +183,10 @@ def main():
         ops.PROFILE = None
         tot_ms = sum(r[2].elapsed_time(r[3]) for r in rec)
         tot_fl = sum(r[1] for r in rec)
+        tot_ref = sum(r[5] for r in rec)
         if args.detail and rank == 0:
             agg = {}
-            for tag, f, s, e, shp in rec:
+            for tag, f, s, e, shp, _ in rec:
                 d = agg.setdefault((tag, shp), [0, 0.0, 0.0])
                 d[0] += 1
                 d[1] += f
@@ -194,7 +195,7 @@ def main():
                 print(f"[detail] {tag:10s} {str(shp):42s} x{cnt:3d} {ms:8.2f} ms {f / (ms * 1e-3) / 1e12:7.1f} TF/s",
                       file=sys.stderr)
         by = {}
-        for tag, f, s, e, _ in rec:
+        for tag, f, s, e, _, _ in rec:
             d = by.setdefault(tag, [0, 0.0, 0.0])
             d[0] += 1
             d[1] += f
@@ -208,6 +209,9 @@ def main():
                     "peak_note": ("bf16 dense MFMA peak 2.5 PF/s (bf16 operands, fp32 accumulate)" if bf16 else
                                   "3xBF16 fp32-emulation ceiling = bf16 dense MFMA 2.5 PF/s / 3; "
                                   "native fp32 MFMA peak is 157.3 TF/s"),
+                    "achieved_note": ("algorithmic FLOPs of the algorithms run (Upsample convs in sub-pixel form "
+                                      "count 4/9 of the reference conv's FLOPs)"),
+                    "reference_equivalent_TFLOP/s": round(tot_ref / (tot_ms * 1e-3) / 1e12, 2),
                     "launches_per_step": len(rec), "avg_launch_us": round(tot_ms * 1e3 / len(rec), 2),
                     "gemm_ms_per_step": round(tot_ms, 2), "instrumented_step_ms": round(step_ms, 2),
                     "gemm_share_of_step": round(tot_ms / step_ms, 3),

@@ -56,6 +56,21 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
                            int wo, int mode, float* workspace, size_t workspace_bytes, void* stream);
 size_t mvae_conv2d_wgrad_workspace_bytes(int nb, int cin, int cout, int kh, int kw, int ho, int wo);
 
+/* Upsample's conv (nearest x2 then 3x3, stride 1, pad 1; encoder_decoder.py:194-209) in sub-pixel form:
+ * output parity class (ph, pw) is a 2x2 conv of the low-resolution x [nb][h][w_][cin] with the tap-summed
+ * weights w4 [4][cout][2][2][cin] (mvae_conv_weight_upsample_fwd), written interleaved into
+ * y [nb][2h][2w_][cout] -- 4/9 of the reference's MACs, no upsampled intermediate. Same result as
+ * mvae_conv2d_nhwc mode 1 up to fp32 summation order. */
+int mvae_conv2d_upsample_nhwc(const float* x, const float* w4, const float* bias, const float* residual, float* y,
+                              int nb, int h, int w_, int cin, int cout, void* stream);
+int mvae_conv_weight_upsample_fwd(const float* w, float* w4, int cout, int cin, void* stream);
+/* Its weight (+ bias) gradient: per-class [cout] x [4*cin] GEMMs over the class pixels, deterministic
+ * split-K partials in the workspace, then a fixed-order combine into dw [cout][3][3][cin] (beta-accumulate). */
+int mvae_conv2d_wgrad_upsample_nhwc(const float* dy, const float* x, float* dw, float* dbias, float beta, int nb,
+                                    int h, int w_, int cin, int cout, float* workspace, size_t workspace_bytes,
+                                    void* stream);
+size_t mvae_conv2d_wgrad_upsample_workspace_bytes(int nb, int h, int w_, int cin, int cout);
+
 /* Weight re-layouts for the input gradient: KRSC -> [cin][kh][kw][cout]; and the 4x4 tap-summed
  * kernel [cin][4][4][cout] for Upsample's conv (encoder_decoder.py:205-209). */
 int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int kw, int cin, void* stream);

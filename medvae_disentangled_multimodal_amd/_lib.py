@@ -30,6 +30,10 @@ SIGNATURES = {
     "mvae_conv2d_wgrad_workspace_bytes": (Z, [I, I, I, I, I, I, I]),
     "mvae_conv_weight_transpose": (I, [P, P, I, I, I, I, P]),
     "mvae_conv_weight_upsample_dgrad": (I, [P, P, I, I, P]),
+    "mvae_conv2d_upsample_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, P]),
+    "mvae_conv_weight_upsample_fwd": (I, [P, P, I, I, P]),
+    "mvae_conv2d_wgrad_upsample_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, P, Z, P]),
+    "mvae_conv2d_wgrad_upsample_workspace_bytes": (Z, [I, I, I, I, I]),
     "mvae_bias_grad": (I, [P, L, I, L, P, F, P, Z, P]),
     "mvae_bias_grad_workspace_bytes": (Z, [L, I]),
     "mvae_gemm_strided_batched": (I, [I, I, I, I, I, F, P, L, L, P, L, L, F, P, L, L, I, P, P, L, L, P, Z, P]),

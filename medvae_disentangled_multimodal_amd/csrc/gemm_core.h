@@ -36,9 +36,12 @@
 namespace mvae {
 
 // operand kinds
-enum { A_ROWK = 0, A_COLM = 1, A_CONV_FWD = 2, A_CONV_UPS = 3, A_CONV_DGRAD = 4 };
-enum { B_ROWK = 0, B_COLN = 1, B_WGRAD_FWD = 2, B_WGRAD_UPS = 3 };
-enum { MODE_FWD = 0, MODE_UPS = 1, MODE_DGRAD = 2 };
+enum { A_ROWK = 0, A_COLM = 1, A_CONV_FWD = 2, A_CONV_UPS = 3, A_CONV_DGRAD = 4, A_CONV_SUBPIX = 5, A_COLM_PIX = 6 };
+enum { B_ROWK = 0, B_COLN = 1, B_WGRAD_FWD = 2, B_WGRAD_UPS = 3, B_WGRAD_SUBPIX = 4 };
+// MODE_SUBPIX: one parity class (ph, pw) of "nearest-x2 upsample then 3x3 conv" as a stride-1 2x2 conv
+// on the low-resolution input whose padding shifts with the parity: pad = pad_t - ph (batch entry
+// bidx = 2*ph + pw carries the class)
+enum { MODE_FWD = 0, MODE_UPS = 1, MODE_DGRAD = 2, MODE_SUBPIX = 3 };
 
 constexpr int BK = 32;
 
@@ -79,7 +82,22 @@ struct GemmArgs {
   // tap (which overflows L2 and re-fetches the input once per tap)
   int perm_rs = 1;
   Magic mg_rs = {0x80000001u, 31};  // make_magic(1)
+  // parity-class output/pixel remap (sub-pixel decompositions): when sub_w2 > 0 the GEMM's pixel index
+  // m = (n, i, j) over an [Ho][Wo] class grid maps to the full-resolution pixel (n, 2i+ph, 2j+pw) of a
+  // [2Ho][2Wo = sub_w2] image: 4m - 2j + ph*sub_w2 + pw, class (ph, pw) = bidx + sub_par
+  int sub_w2 = 0, sub_par = 0;
+  int out_remap = 0;  // epilogue writes C row sub_pixel(m) (conv outputs); else row m
 };
+
+// full-resolution pixel of class-grid pixel m (see GemmArgs::sub_w2)
+__device__ __forceinline__ int sub_pixel(const GemmArgs& a, int m, int par_off) {
+  const int j = m - mdiv(m, a.mg_wo) * a.Wo;
+  return 4 * m - 2 * j + par_off;
+}
+__device__ __forceinline__ int sub_par_off(const GemmArgs& a, int bidx) {
+  const int par = bidx + a.sub_par;
+  return (par >> 1) * a.sub_w2 + (par & 1);
+}
 
 // column of the reference K order where (permuted) K-tile starting at k begins; k % 32 == 0
 // (branch-free: perm_rs = 1 gives chunk = t, tap = 0, i.e. the identity)
@@ -150,10 +168,15 @@ __device__ __forceinline__ bf16x8 read_frag(const __bf16* plane, int row0, int k
 
 // source pixel of output pixel (oh,ow) for filter tap (r,s); MODE is a compile-time constant
 template <int MODE>
-__device__ __forceinline__ bool tap_src(const GemmArgs& a, int oh, int ow, int r, int s, int& ih, int& iw) {
+__device__ __forceinline__ bool tap_src(const GemmArgs& a, int pt, int pl, int oh, int ow, int r, int s, int& ih,
+                                        int& iw) {
   if constexpr (MODE == MODE_FWD) {
     ih = oh * a.stride - a.pad_t + r;
     iw = ow * a.stride - a.pad_l + s;
+    return ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
+  } else if constexpr (MODE == MODE_SUBPIX) {  // stride 1, class-dependent padding pt / pl
+    ih = oh - pt + r;
+    iw = ow - pl + s;
     return ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
   } else if constexpr (MODE == MODE_UPS) {  // nearest x2 upsample, then conv (stride 1)
     const int uh = oh - a.pad_t + r, uw = ow - a.pad_l + s;
@@ -202,7 +225,7 @@ struct LoadRowK {
   unsigned ld;
   int rows, K, row0, k, kc, r0, kk;
   float4 v[NS];
-  __device__ void init(const GemmArgs& a, const float* p, int row0_, int kb, int tid) {
+  __device__ void init(const GemmArgs& a, const float* p, int row0_, int kb, int tid, int) {
     rs = make_rsrc(p, IS_A ? a.a_bytes : a.b_bytes);
     ld = (unsigned)(IS_A ? a.lda : a.ldb); rows = IS_A ? a.M : a.N; K = a.K;
     row0 = row0_; k = kb; kc = tid & 7; r0 = row_of_tid(tid);
@@ -251,9 +274,12 @@ struct LoadConvA {
   int cc[NE], rr[NE], ss[NE];
   bool kv[NE];
   float4 v[NS];
-  __device__ void init(const GemmArgs& a, const float* x, int row0, int kb, int tid) {
+  int pt, pl;  // MODE_SUBPIX: padding of this batch entry's parity class
+  __device__ void init(const GemmArgs& a, const float* x, int row0, int kb, int tid, int bidx) {
     rs = make_rsrc(x, a.a_bytes);
     kc = tid & 7; r0 = row_of_tid(tid); k = kb;
+    pt = a.pad_t - ((bidx + a.sub_par) >> 1);
+    pl = a.pad_l - ((bidx + a.sub_par) & 1);
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const int m = row0 + r0 + RP * i;
@@ -283,7 +309,7 @@ struct LoadConvA {
   __device__ void load_slot(const GemmArgs& a, int i) {
     if (VEC == 4) {
       int ih = 0, iw = 0;
-      const bool tv = tap_src<MODE>(a, oh[i], ow[i], rr[0], ss[0], ih, iw);
+      const bool tv = tap_src<MODE>(a, pt, pl, oh[i], ow[i], rr[0], ss[0], ih, iw);
       const bool ok = mv[i] & kv[0] & tv;
       const unsigned off = ((base[i] + (unsigned)(ih * a.W + iw)) * (unsigned)a.Cx + (unsigned)cc[0]) * 4u;
       v[i] = bload4(rs, ok ? off : OOB);
@@ -292,7 +318,7 @@ struct LoadConvA {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         int ih = 0, iw = 0;
-        const bool tv = tap_src<MODE>(a, oh[i], ow[i], rr[e], ss[e], ih, iw);
+        const bool tv = tap_src<MODE>(a, pt, pl, oh[i], ow[i], rr[e], ss[e], ih, iw);
         const bool ok = mv[i] & kv[e] & tv;
         const unsigned off = ((base[i] + (unsigned)(ih * a.W + iw)) * (unsigned)a.Cx + (unsigned)cc[e]) * 4u;
         t[e] = bload1(rs, ok ? off : OOB);
@@ -326,7 +352,7 @@ struct LoadColK {
   int rows, K, row0, k, c4, kr;
   float4 v[NS];
   float bs[4] = {0.f, 0.f, 0.f, 0.f};  // A side: running row sums of every staged element
-  __device__ void init(const GemmArgs& a, const float* p, int row0_, int kb, int tid) {
+  __device__ void init(const GemmArgs& a, const float* p, int row0_, int kb, int tid, int) {
     rs = make_rsrc(p, IS_A ? a.a_bytes : a.b_bytes);
     ld = (unsigned)(IS_A ? a.lda : a.ldb); rows = IS_A ? a.M : a.N; K = a.K;
     row0 = row0_; k = kb; c4 = tid % C4; kr = tid / C4;
@@ -368,6 +394,64 @@ struct LoadColK {
   }
 };
 
+// COL image of A = dY^T whose k (pixel) index walks one parity class of a full-resolution image:
+// element (row, k) at P[sub_pixel(k)*ld + row] (the wgrad of the sub-pixel Upsample conv)
+template <int ROWS, int VEC, int NT, int PREC>
+struct LoadColPix {
+  static constexpr bool COL = true;
+  static constexpr int C4 = ROWS / 4;
+  static constexpr int NS = (BK * C4 + NT - 1) / NT;
+  __amdgpu_buffer_rsrc_t rs;
+  unsigned ld;
+  int rows, K, row0, k, c4, kr, krw, par_off;
+  unsigned pix[NS];
+  float4 v[NS];
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};
+  __device__ void init(const GemmArgs& a, const float* p, int row0_, int kb, int tid, int bidx) {
+    rs = make_rsrc(p, a.a_bytes);
+    ld = (unsigned)a.lda; rows = a.M; K = a.K;
+    row0 = row0_; k = kb; c4 = tid % C4; kr = tid / C4;
+    krw = (C4 % 64 == 0) ? __builtin_amdgcn_readfirstlane(kr) : kr;
+    par_off = sub_par_off(a, bidx);
+  }
+  __device__ void prep(const GemmArgs& a) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) pix[i] = (unsigned)sub_pixel(a, min(k + krw + i * (NT / C4), K - 1), par_off);
+  }
+  __device__ void load_slot(const GemmArgs&, int i) {
+    const int col = row0 + c4 * 4;
+    const int krow = kr + i * (NT / C4);
+    const bool kv = krow < BK && k + krow < K;
+    const unsigned base = (pix[i] * ld + (unsigned)col) * 4u;
+    if (VEC == 4) {
+      v[i] = bload4(rs, (kv && col < rows) ? base : OOB);
+    } else {
+      v[i].x = bload1(rs, (kv && col + 0 < rows) ? base : OOB);
+      v[i].y = bload1(rs, (kv && col + 1 < rows) ? base + 4 : OOB);
+      v[i].z = bload1(rs, (kv && col + 2 < rows) ? base + 8 : OOB);
+      v[i].w = bload1(rs, (kv && col + 3 < rows) ? base + 12 : OOB);
+    }
+  }
+  __device__ void store_slot(__bf16* img, int i) {
+    constexpr int P_ = Img<ROWS, true>::PITCH;
+    const int krow = kr + i * (NT / C4);
+    if (krow < BK) {
+      st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+      bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
+    }
+  }
+  __device__ void advance() { k += BK; }
+  __device__ void load(const GemmArgs& a) {
+    prep(a);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) load_slot(a, i);
+  }
+  __device__ void store(__bf16* img) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) store_slot(img, i);
+  }
+};
+
 // COL image for the wgrad B operand: rows n' = (r*S+s)*Cx + c (filter element), k = output pixel.
 // element = X[b][src(oh,ow,r,s)][c], contiguous along c.
 template <int ROWS, int VEC, int NT, int MODE, int PREC>
@@ -381,9 +465,12 @@ struct LoadWgradX {
   bool nv[4];
   int pb[NS], poh[NS], pow_[NS];  // pixel decomposition of this thread's k-rows (current tile)
   float4 v[NS];
-  __device__ void init(const GemmArgs& a, const float* x, int row0, int kb, int tid) {
+  int pt, pl;
+  __device__ void init(const GemmArgs& a, const float* x, int row0, int kb, int tid, int bidx) {
     rs = make_rsrc(x, a.b_bytes);
     k = kb; c4 = tid % C4; kr = tid / C4;
+    pt = a.pad_t - ((bidx + a.sub_par) >> 1);
+    pl = a.pad_l - ((bidx + a.sub_par) & 1);
     for (int e = 0; e < 4; ++e) {
       const int n = row0 + c4 * 4 + e;
       nv[e] = n < a.N;
@@ -412,7 +499,7 @@ struct LoadWgradX {
     const bool kv = krow < BK && (k + krow < a.K);
     if (VEC == 4) {
       int ih = 0, iw = 0;
-      const bool tv = tap_src<MODE>(a, poh[i], pow_[i], rr[0], ss[0], ih, iw);
+      const bool tv = tap_src<MODE>(a, pt, pl, poh[i], pow_[i], rr[0], ss[0], ih, iw);
       const bool ok = kv & nv[0] & tv;
       const unsigned off = (((unsigned)pb[i] * img + (unsigned)(ih * a.W + iw)) * (unsigned)a.Cx + (unsigned)cc[0]) * 4u;
       v[i] = bload4(rs, ok ? off : OOB);
@@ -421,7 +508,7 @@ struct LoadWgradX {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         int ih = 0, iw = 0;
-        const bool tv = tap_src<MODE>(a, poh[i], pow_[i], rr[e], ss[e], ih, iw);
+        const bool tv = tap_src<MODE>(a, pt, pl, poh[i], pow_[i], rr[e], ss[e], ih, iw);
         const bool ok = kv & nv[e] & tv;
         const unsigned off =
             (((unsigned)pb[i] * img + (unsigned)(ih * a.W + iw)) * (unsigned)a.Cx + (unsigned)cc[e]) * 4u;
@@ -474,6 +561,12 @@ template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<2, ROWS, VEC, NT, false, PREC> : LoadWgradX<ROWS, VEC, NT, MODE_FWD, PREC> {};
 template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<3, ROWS, VEC, NT, false, PREC> : LoadWgradX<ROWS, VEC, NT, MODE_UPS, PREC> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<5, ROWS, VEC, NT, true, PREC> : LoadConvA<ROWS, VEC, NT, MODE_SUBPIX, PREC> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<6, ROWS, VEC, NT, true, PREC> : LoadColPix<ROWS, VEC, NT, PREC> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<4, ROWS, VEC, NT, false, PREC> : LoadWgradX<ROWS, VEC, NT, MODE_SUBPIX, PREC> {};
 
 template <int BM, int BN, int WGM, int WGN, int AK, int VA, int BKIND, int VB, int PREC>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
@@ -510,8 +603,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 
   LA la;
   LB lb;
-  la.init(a, a.A + bidx * a.sA, m0, kb, tid);
-  lb.init(a, a.B + bidx * a.sB, n0, kb, tid);
+  la.init(a, a.A + bidx * a.sA, m0, kb, tid, bidx);
+  lb.init(a, a.B + bidx * a.sB, n0, kb, tid, bidx);
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -655,7 +748,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 
   // wgrad: the conv bias gradient (row sums of A = dY^T over this split's pixels) falls out of the
   // A staging for free; one column of tiles (tn == 0) publishes it, fixed-order reduction in LDS.
-  if constexpr (AK == A_COLM) {
+  if constexpr (AK == A_COLM || AK == A_COLM_PIX) {
     if (a.bias_ws != nullptr && tn == 0) {
       constexpr int KRN = NT / (BM / 4);
       float* red = (float*)lds;
@@ -698,6 +791,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   const bool has_res = a.res != nullptr;
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(has_res ? a.res + bidx * a.sR : a.C, has_res ? a.r_bytes : 0u);
   const __amdgpu_buffer_rsrc_t br = make_rsrc(a.bias ? a.bias : a.C, a.bias ? (unsigned)(a.N * 4) : 0u);
+  const bool remap = a.out_remap != 0;
+  const int par_off = sub_par_off(a, bidx);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + brow + j * 32 + (lane & 31);
@@ -708,9 +803,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + arow + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const bool ok = row < a.M && col < a.N;
+        const int orow = remap ? sub_pixel(a, ok ? row : 0, par_off) : row;
         float v = a.alpha * acc[i][j][r] + bv;
-        if (has_res) v += bload1(rr, ok ? ((unsigned)row * (unsigned)a.ldr + col) * 4u : OOB);
-        const unsigned co = ok ? ((unsigned)row * (unsigned)a.ldc + col) * 4u : OOB;
+        if (has_res) v += bload1(rr, ok ? ((unsigned)orow * (unsigned)a.ldr + col) * 4u : OOB);
+        const unsigned co = ok ? ((unsigned)orow * (unsigned)a.ldc + col) * 4u : OOB;
         if (a.beta != 0.f) v += a.beta * bload1(cr, co);
         bstore1(cr, co, v);
       }

@@ -10,9 +10,49 @@ __global__ void bias_reduce_kernel(const float* __restrict__ part, int splits, i
   for (int z = 0; z < splits; ++z) s += part[(long long)z * m + i];
   dbias[i] = (beta != 0.f ? beta * dbias[i] : 0.f) + s;
 }
+
+// Upsample-conv weight gradient from the per-class partials of the sub-pixel form:
+// part[cls][z][co][(2a+b)*cin + ci] (cls = 2*ph+pw, z = split) ->
+// dw[co][r][s][ci] = beta*dw + sum_{(ph,a) in P(r), (pw,b) in P(s)} sum_z part[2ph+pw][z][co][(2a+b)*cin+ci]
+// with P(0) = {(0,0),(1,0)}, P(1) = {(0,1),(1,0)}, P(2) = {(0,1),(1,1)} (fixed summation order)
+__global__ void __launch_bounds__(256) ups_wgrad_combine_kernel(const float* __restrict__ part, int splits, int cout,
+                                                                int cin, float* __restrict__ dw, float beta) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)cout * cin) return;
+  const int co = (int)(idx / cin), ci = (int)(idx - (long long)co * cin);
+  const long long n4 = 4LL * cin;
+  float g[4][4];
+#pragma unroll
+  for (int cls = 0; cls < 4; ++cls)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float s = 0.f;
+      for (int z = 0; z < splits; ++z) s += part[((long long)(cls * splits + z) * cout + co) * n4 + t * cin + ci];
+      g[cls][t] = s;
+    }
+  const int pp[3][2][2] = {{{0, 0}, {1, 0}}, {{0, 1}, {1, 0}}, {{0, 1}, {1, 1}}};  // P(r): (parity, tap)
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      float v = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          v += g[2 * pp[r][u][0] + pp[q][e][0]][2 * pp[r][u][1] + pp[q][e][1]];
+      float* o = dw + (((long long)co * 3 + r) * 3 + q) * cin + ci;
+      *o = (beta != 0.f ? beta * *o : 0.f) + v;
+    }
+}
 }  // namespace mvae
 
 using namespace mvae;
+
+static void ups_wgrad_shape(GemmArgs& a, int nb, int h, int wd, int cin, int cout) {
+  a.M = cout; a.N = 4 * cin; a.K = nb * h * wd; a.batch = 4;
+}
+static size_t ups_part_bytes(const GemmArgs& a) { return (size_t)a.batch * a.splits * a.M * a.N * sizeof(float); }
 
 static void wgrad_shape(GemmArgs& a, int nb, int cin, int cout, int kh, int kw, int ho, int wo) {
   a.M = cout; a.N = kh * kw * cin; a.K = nb * ho * wo; a.batch = 1;
@@ -72,6 +112,75 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
     if (rc) return rc;
   }
   return MVAE_OK;
+}
+
+// Weight (+ bias) gradient of Upsample's convolution through its sub-pixel form (see
+// mvae_conv2d_upsample_nhwc): per parity class a [cout] x [2*2*cin] GEMM over the class's pixels (A = dY^T
+// walking the class, B = 2x2 gather of the low-resolution x), deterministic split-K partials, then a fixed-
+// order combine into the 3x3 kernel. 4/9 of the reference's MACs.
+int mvae_conv2d_wgrad_upsample_nhwc(const float* dy, const float* x, float* dw, float* dbias, float beta, int nb,
+                                    int h, int wd, int cin, int cout, float* workspace, size_t workspace_bytes,
+                                    void* stream) {
+  if (nb <= 0 || h <= 0 || wd <= 0 || cin <= 0 || cout <= 0) { set_error("wgrad_upsample: bad sizes"); return MVAE_EINVAL; }
+  const long long in_img = (long long)h * wd * cin * 4, out_img = 4LL * h * wd * cout * 4;
+  if (std::max(in_img, out_img) > MAX_DESC_BYTES || 16LL * cout * cin * 4 > MAX_DESC_BYTES) {
+    set_error("wgrad_upsample: one image exceeds 4 GiB");
+    return MVAE_EINVAL;
+  }
+  if (workspace == nullptr) { set_error("wgrad_upsample: workspace required"); return MVAE_EWORKSPACE; }
+  const int chunk = (int)std::min<long long>(nb, MAX_DESC_BYTES / std::max(in_img, out_img));
+  hipStream_t st = (hipStream_t)stream;
+  const bool va = (cout % 4 == 0) && al16(dy);
+  const bool vb = (cin % 4 == 0) && al16(x);
+  for (int b0 = 0; b0 < nb; b0 += chunk) {
+    const int n = std::min(chunk, nb - b0);
+    GemmArgs a{};
+    ups_wgrad_shape(a, n, h, wd, cin, cout);
+    a.A = dy + (long long)b0 * (out_img / 4); a.lda = cout; a.sA = 0;
+    a.B = x + (long long)b0 * (in_img / 4); a.sB = 0;
+    a.alpha = 1.f; a.beta = 0.f;
+    a.a_bytes = (unsigned)(out_img * n); a.b_bytes = (unsigned)(in_img * n);
+    a.H = h; a.W = wd; a.Cx = cin; a.Ho = h; a.Wo = wd; a.R = 2; a.S = 2;
+    set_gather_magic(a);
+    a.stride = 1; a.pad_t = 1; a.pad_l = 1;
+    a.sub_w2 = 2 * wd; a.sub_par = 0; a.out_remap = 0;
+    const int cfg = choose_tile(a, va && vb, true);
+    const size_t bias_bytes = dbias ? ((size_t)4 * 64 * a.M * sizeof(float) + 256) : 0;
+    if (workspace_bytes < bias_bytes) { set_error("wgrad_upsample: workspace too small"); return MVAE_EWORKSPACE; }
+    const size_t avail = workspace_bytes - bias_bytes;
+    set_splits(a, choose_splits(a, cfg));
+    while (a.splits > 1 && ups_part_bytes(a) > avail) set_splits(a, a.splits / 2);
+    if (ups_part_bytes(a) > avail) { set_error("wgrad_upsample: workspace too small"); return MVAE_EWORKSPACE; }
+    a.ws = workspace;
+    // one split: the kernel writes C = the class partials directly ([cls][1][M][N], same layout)
+    a.C = workspace; a.ldc = a.N; a.sC = (long long)a.M * a.N; a.c_bytes = (unsigned)((long long)a.M * a.N * 4);
+    a.bias_ws = dbias ? (float*)((char*)workspace + ((ups_part_bytes(a) + 255) & ~(size_t)255)) : nullptr;
+    if (va && vb) launch_big<A_COLM_PIX, 4, B_WGRAD_SUBPIX, 4>(a, st, cfg);
+    else if (va) launch_small<A_COLM_PIX, 4, B_WGRAD_SUBPIX, 1>(a, st, cfg);
+    else if (vb) launch_small<A_COLM_PIX, 1, B_WGRAD_SUBPIX, 4>(a, st, cfg);
+    else launch_small<A_COLM_PIX, 1, B_WGRAD_SUBPIX, 1>(a, st, cfg);
+    const float bt = b0 == 0 ? beta : 1.f;
+    if (dbias)
+      hipLaunchKernelGGL(bias_reduce_kernel, dim3(cdiv(a.M, 256)), dim3(256), 0, st, (const float*)a.bias_ws,
+                         a.splits * a.batch, a.M, dbias, bt);
+    const long long tot = (long long)cout * cin;
+    hipLaunchKernelGGL(ups_wgrad_combine_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st,
+                       (const float*)workspace, a.splits, cout, cin, dw, bt);
+    const int rc = launch_status();
+    if (rc) return rc;
+  }
+  return MVAE_OK;
+}
+
+size_t mvae_conv2d_wgrad_upsample_workspace_bytes(int nb, int h, int wd, int cin, int cout) {
+  GemmArgs a{};
+  ups_wgrad_shape(a, nb, h, wd, cin, cout);
+  size_t b = 0;
+  for (int big = 0; big < 2; ++big) {
+    set_splits(a, choose_splits(a, choose_tile(a, big != 0, true)));
+    b = std::max(b, ups_part_bytes(a));
+  }
+  return ((b + 255) & ~(size_t)255) + (size_t)4 * 64 * a.M * sizeof(float) + 256;
 }
 
 size_t mvae_conv2d_wgrad_workspace_bytes(int nb, int cin, int cout, int kh, int kw, int ho, int wo) {

@@ -66,6 +66,37 @@ __global__ void __launch_bounds__(256) w_ups_dgrad_kernel(const float* __restric
   }
 }
 
+// forward weights of the sub-pixel Upsample conv: w4[2*ph+pw][co][a][b][ci] = sum of w[co][r][s][ci] over
+// r in T(ph, a), s in T(pw, b): T(0,0) = {0}, T(0,1) = {1,2}, T(1,0) = {0,1}, T(1,1) = {2}
+__device__ __forceinline__ int sub_mask(int p, int a) { return p == 0 ? (a == 0 ? 0b001 : 0b110) : (a == 0 ? 0b011 : 0b100); }
+
+__global__ void __launch_bounds__(256) w_ups_fwd_kernel(const float* __restrict__ w, float* __restrict__ w4, int cout,
+                                                        int cin) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)cout * cin) return;
+  const int co = (int)(idx / cin), ci = (int)(idx - (long long)co * cin);
+  float t[3][3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) t[r][s] = w[(((long long)co * 3 + r) * 3 + s) * cin + ci];
+#pragma unroll
+  for (int cls = 0; cls < 4; ++cls)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int mr = sub_mask(cls >> 1, a), ms = sub_mask(cls & 1, b);
+        float v = 0.f;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int s = 0; s < 3; ++s)
+            if (((mr >> r) & 1) && ((ms >> s) & 1)) v += t[r][s];
+        w4[((((long long)cls * cout + co) * 2 + a) * 2 + b) * cin + ci] = v;
+      }
+}
+
 // column sums: part[chunk][n] = sum over rows in chunk ; then out[n] += sum_chunks (fixed order)
 __global__ void __launch_bounds__(256) colsum_partial_kernel(const float* __restrict__ x, long long rows, int n,
                                                              long long ld, int rows_per_chunk,
@@ -119,6 +150,15 @@ int mvae_conv_weight_upsample_dgrad(const float* w, float* wt, int cout, int cin
   if (cout <= 0 || cin <= 0) { set_error("w_ups: bad sizes"); return MVAE_EINVAL; }
   hipLaunchKernelGGL(w_ups_dgrad_kernel, dim3((cin + 63) / 64, (cout + 63) / 64, 16), dim3(256), 0,
                      (hipStream_t)stream, w, wt, cout, cin);
+  return launch_status();
+}
+
+// w4 [4][cout][2][2][cin] for the sub-pixel forward of "nearest-x2 upsample then 3x3 conv"
+int mvae_conv_weight_upsample_fwd(const float* w, float* w4, int cout, int cin, void* stream) {
+  if (cout <= 0 || cin <= 0) { set_error("w_ups_fwd: bad sizes"); return MVAE_EINVAL; }
+  const long long tot = (long long)cout * cin;
+  hipLaunchKernelGGL(w_ups_fwd_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, w, w4,
+                     cout, cin);
   return launch_status();
 }
 

@@ -10,6 +10,7 @@ Every op requires CUDA(HIP) tensors: there is no CPU fallback.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -69,10 +70,14 @@ PROFILE = None
 
 
 class _timed:
-    __slots__ = ("tag", "flops", "s", "shape")
+    """HIP-event bracket of one GEMM-family launch (bench.py roofline). `flops` = the algorithmic work of
+    the algorithm this launch runs (useful MACs x 2: the sub-pixel Upsample forms count 4/9 of the
+    reference conv); `ref_flops` = the reference conv's count for the same result (default: flops)."""
+    __slots__ = ("tag", "flops", "s", "shape", "ref_flops")
 
-    def __init__(self, tag: str, flops: float, shape=None):
+    def __init__(self, tag: str, flops: float, shape=None, ref_flops=None):
         self.tag, self.flops, self.shape = tag, flops, shape
+        self.ref_flops = flops if ref_flops is None else ref_flops
 
     def __enter__(self):
         if PROFILE is not None:
@@ -84,7 +89,7 @@ class _timed:
         if PROFILE is not None:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
-            PROFILE.append((self.tag, self.flops, self.s, e, self.shape))
+            PROFILE.append((self.tag, self.flops, self.s, e, self.shape, self.ref_flops))
         return False
 
 
@@ -155,22 +160,42 @@ def _krsc(w: torch.Tensor) -> torch.Tensor:
     return w if w.is_contiguous(memory_format=CL) else w.contiguous(memory_format=CL)
 
 
+def _subpixel_upsample(g: ConvGeom) -> bool:
+    """Upsample's conv (nearest x2 then 3x3 s1 p1, encoder_decoder.py:205-209) runs in sub-pixel form:
+    4 parity classes of 2x2 convs on the low-resolution input (4/9 of the MACs)."""
+    return g.upsample and g.kh == 3 and g.kw == 3 and g.stride == 1 and \
+        g.pad_t == g.pad_l == g.pad_b == g.pad_r == 1 and SUBPIXEL_UPSAMPLE
+
+
+SUBPIXEL_UPSAMPLE = os.environ.get("MVAE_NO_SUBPIXEL") is None
+
+
 def conv2d_forward_raw(x, w, b, res, g: ConvGeom):
     n, c, h, wd = x.shape
     co = w.shape[0]
     ho, wo = g.out_hw(h, wd)
     y = torch.empty((n, co, ho, wo), device=x.device, dtype=torch.float32, memory_format=CL)
-    with _timed("conv_fwd", 2.0 * n * ho * wo * co * c * g.kh * g.kw, (n, c, h, wd, co, g.kh, g.stride, g.upsample)):
-        _conv_fwd_launch(x, w, b, res, y, g, n, c, h, wd, co, ho, wo)
+    ref = 2.0 * n * ho * wo * co * c * g.kh * g.kw
+    alg = ref * 4 / 9 if _subpixel_upsample(g) else ref
+    w4 = None
+    if _subpixel_upsample(g):  # tap-summed per-class weights (outside the timed GEMM launch)
+        w4 = ARENA.get("w4", 16 * co * c * 4, x.device)
+        _lib.call("mvae_conv_weight_upsample_fwd", w.data_ptr(), w4.data_ptr(), co, c, _stream(x))
+    with _timed("conv_fwd", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
+        _conv_fwd_launch(x, w, b, res, y, g, n, c, h, wd, co, ho, wo, w4)
     return y
 
 
-def _conv_fwd_launch(x, w, b, res, y, g, n, c, h, wd, co, ho, wo):
+def _conv_fwd_launch(x, w, b, res, y, g, n, c, h, wd, co, ho, wo, w4=None):
     if g.pointwise:
         # 1x1 conv = GEMM [pixels][cin] x [cout][cin]^T
         _lib.call("mvae_gemm_strided_batched", 0, 1, n * h * wd, co, c, 1.0, x.data_ptr(), c, 0,
                   w.data_ptr(), c, 0, 0.0, y.data_ptr(), co, 0, 1, _ptr(b), _ptr(res), co, 0, None, 0,
                   _stream(x))
+    elif w4 is not None:
+        st = _stream(x)
+        _lib.call("mvae_conv2d_upsample_nhwc", x.data_ptr(), w4.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n, h,
+                  wd, c, co, st)
     else:
         _lib.call("mvae_conv2d_nhwc", x.data_ptr(), w.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n, h, wd, c,
                   co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, 1 if g.upsample else 0, _stream(x))
@@ -182,7 +207,7 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom):
     _, _, ho, wo = dy.shape
     dx = torch.empty((n, c, h, wd), device=dy.device, dtype=torch.float32, memory_format=CL)
     st = _stream(dy)
-    flops = 2.0 * n * ho * wo * co * c * g.kh * g.kw  # algorithmic (reference) count
+    flops = 2.0 * n * ho * wo * co * c * g.kh * g.kw  # reference count
     if g.pointwise:
         # dx[m][c] = sum_n dy[m][n] W[n][c]  (W stored [K=cout][N=cin])
         with _timed("conv_dgrad", flops, (n, c, h, wd, co, g.kh, g.stride, g.upsample)):
@@ -192,8 +217,8 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom):
     if g.upsample:
         wt = ARENA.get("wt", c * 16 * co * 4, dy.device)
         _lib.call("mvae_conv_weight_upsample_dgrad", w.data_ptr(), wt.data_ptr(), co, c, st)
-        # dX = stride-2, pad-1 4x4 conv of dY with the tap-summed kernel
-        with _timed("conv_dgrad", flops, (n, c, h, wd, co, g.kh, g.stride, g.upsample)):
+        # dX = stride-2, pad-1 4x4 conv of dY with the tap-summed kernel (16 taps per low-res pixel)
+        with _timed("conv_dgrad", flops * 4 / 9, (n, c, h, wd, co, g.kh, g.stride, g.upsample), flops):
             _lib.call("mvae_conv2d_nhwc", dy.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
                       4, 4, 2, 1, 1, h, wd, 0, st)
         return dx
@@ -211,7 +236,9 @@ def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None):
     n, c, h, wd = x.shape
     co = dy.shape[1]
     _, _, ho, wo = dy.shape
-    with _timed("conv_wgrad", 2.0 * n * ho * wo * co * c * g.kh * g.kw, (n, c, h, wd, co, g.kh, g.stride, g.upsample)):
+    ref = 2.0 * n * ho * wo * co * c * g.kh * g.kw
+    alg = ref * 4 / 9 if _subpixel_upsample(g) else ref
+    with _timed("conv_wgrad", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
         return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db)
 
 
@@ -225,6 +252,12 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None):
         _lib.call("mvae_gemm_strided_batched", 1, 0, co, c, m, 1.0, dy.data_ptr(), co, 0, x.data_ptr(), c, 0,
                   float(beta), dw.data_ptr(), c, 0, 1, None, None, 0, 0, ws.data_ptr(), ws.numel(), st)
         return False
+    if _subpixel_upsample(g):
+        nbytes = _lib.query("mvae_conv2d_wgrad_upsample_workspace_bytes", n, h, wd, c, co)
+        ws = ARENA.get("ws", nbytes, dy.device)
+        _lib.call("mvae_conv2d_wgrad_upsample_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db),
+                  float(beta), n, h, wd, c, co, ws.data_ptr(), ws.numel(), st)
+        return db is not None
     nbytes = _lib.query("mvae_conv2d_wgrad_workspace_bytes", n, c, co, g.kh, g.kw, ho, wo)
     ws = ARENA.get("ws", nbytes, dy.device)
     _lib.call("mvae_conv2d_wgrad_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db), float(beta), n, h, wd,

@@ -52,6 +52,10 @@ CONV_CASES = [
     (64, 256, 256, 32, 32, 3, 1, (1, 1, 1, 1), False),
     (64, 256, 128, 16, 16, 3, 1, (1, 1, 1, 1), True),  # Upsample 16 -> 32
     (64, 128, 128, 64, 64, 3, 2, (0, 0, 1, 1), False),  # Downsample 64 -> 32
+    # sub-pixel Upsample: scalar-gather path (cin 3), non-square, Cin % 32 != 0, mid-size 256x256 tiles
+    (2, 3, 8, 5, 6, 3, 1, (1, 1, 1, 1), True),
+    (2, 48, 40, 6, 9, 3, 1, (1, 1, 1, 1), True),
+    (16, 512, 256, 8, 8, 3, 1, (1, 1, 1, 1), True),
 ]
 
 
@@ -101,6 +105,25 @@ def test_conv_fwd_dgrad_wgrad(dev, case):
     assert wm.grad is None and bm.grad is None
     assert rel(wm._mvae_main_grad - 0.5, wr.grad) < CONV_TOL
     assert float((bm._mvae_main_grad.cpu().double() - 0.25 - db_ref).abs().max()) < 1e-5 * scale
+
+
+def test_upsample_gather_mode_matches_subpixel(dev):
+    """The direct gather form of Upsample's conv (mvae_conv2d_nhwc mode 1: 9 taps on the upsampled grid)
+    and the sub-pixel form (4 parity classes of 2x2 convs) give the same result."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    g = torch.Generator().manual_seed(5)
+    n, ci, co, h, w = 3, 64, 32, 7, 9
+    x = cl(torch.randn(n, ci, h, w, generator=g), dev)
+    wt = cl(torch.randn(co, ci, 3, 3, generator=g) / 24.0, dev)
+    b = torch.randn(co, generator=g).to(dev)
+    ref = torch_conv(x.cpu(), wt.cpu(), b.cpu(), 1, (1, 1, 1, 1), True)
+    y1 = torch.empty((n, co, 2 * h, 2 * w), device=dev).contiguous(memory_format=torch.channels_last)
+    st = torch.cuda.current_stream().cuda_stream
+    _lib.call("mvae_conv2d_nhwc", x.data_ptr(), wt.data_ptr(), b.data_ptr(), None, y1.data_ptr(), n, h, w, ci, co,
+              3, 3, 1, 1, 1, 2 * h, 2 * w, 1, st)
+    y2 = ops.conv2d_forward_raw(x, wt, b, None, ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, True))
+    assert rel(y1, ref) < CONV_TOL and rel(y2, ref) < CONV_TOL
+    assert rel(y1, y2) < CONV_TOL
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
