@@ -6,7 +6,7 @@ ARCH ?= gfx950
 PKG := medvae_disentangled_multimodal_amd
 SRC := $(wildcard $(PKG)/csrc/*.hip) $(PKG)/csrc/errors.cpp
 OBJ := $(patsubst $(PKG)/csrc/%,build/%.o,$(SRC))
-CXXFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Wno-unused-variable
+CXXFLAGS := -O3 -std=c++17 -fPIC -fno-slp-vectorize --offload-arch=$(ARCH) -Wall -Wno-unused-function -Wno-unused-variable
 
 all: $(PKG)/libmvae_hip.so
 

@@ -43,7 +43,10 @@ int mvae_get_math_mode(void);
  * (src/models/encoder_decoder.py:123-146,76-81,250-299,356-418), Downsample's F.pad + stride-2 conv
  * (:184-188, mode 0 with pad_t=pad_l=0 and zero fill beyond H/W) and Upsample's F.interpolate +
  * conv (:205-209, mode 1). mode 2 = transposed gather (input gradient of a strided conv).
- * y = conv(x) + bias[cout] + residual (residual: ResnetBlock/AttnBlock skip add, :170, :107). */
+ * y = conv(x) + bias[cout] + residual (residual: ResnetBlock/AttnBlock skip add, :170, :107).
+ * mode | MVAE_CONV_WSPLIT: w is pre-split (mvae_split_bf16 layout; cin % 4 == 0) -- the 3xBF16 hi/lo split of
+ * the weight operand is done once per step instead of in every workgroup's staging. */
+#define MVAE_CONV_WSPLIT 16
 int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y,
                      int nb, int h, int w_, int cin, int cout, int kh, int kw, int stride, int pad_t,
                      int pad_l, int ho, int wo, int mode, void* stream);
@@ -56,14 +59,23 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
                            int wo, int mode, float* workspace, size_t workspace_bytes, void* stream);
 size_t mvae_conv2d_wgrad_workspace_bytes(int nb, int cin, int cout, int kh, int kw, int ho, int wo);
 
+/* Input gradient of a stride-2 conv (Downsample, encoder_decoder.py:184-188) by dx parity class: each
+ * class is a dense stride-1 conv of dy [nb][ho][wo][cout] with its own <= 2x2 taps of wt [cin][kh][kw][cout]
+ * (mvae_conv_weight_transpose), written interleaved into dx [nb][h][w_][cin] (h, w_ even): the useful
+ * MACs only, vs mode 2's transposed gather where 3/4 of the taps hit stride holes.
+ * workspace >= 4*kh*kw*cin*cout bytes (per-class weights). */
+int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, int nb, int h, int w_, int cin,
+                                   int cout, int kh, int kw, int pad_t, int pad_l, int ho, int wo, int w_split,
+                                   float* workspace, size_t workspace_bytes, void* stream);
+
 /* Upsample's conv (nearest x2 then 3x3, stride 1, pad 1; encoder_decoder.py:194-209) in sub-pixel form:
  * output parity class (ph, pw) is a 2x2 conv of the low-resolution x [nb][h][w_][cin] with the tap-summed
  * weights w4 [4][cout][2][2][cin] (mvae_conv_weight_upsample_fwd), written interleaved into
  * y [nb][2h][2w_][cout] -- 4/9 of the reference's MACs, no upsampled intermediate. Same result as
  * mvae_conv2d_nhwc mode 1 up to fp32 summation order. */
 int mvae_conv2d_upsample_nhwc(const float* x, const float* w4, const float* bias, const float* residual, float* y,
-                              int nb, int h, int w_, int cin, int cout, void* stream);
-int mvae_conv_weight_upsample_fwd(const float* w, float* w4, int cout, int cin, void* stream);
+                              int nb, int h, int w_, int cin, int cout, int w_split, void* stream);
+int mvae_conv_weight_upsample_fwd(const float* w, float* w4, int cout, int cin, int split, void* stream);
 /* Its weight (+ bias) gradient: per-class [cout] x [4*cin] GEMMs over the class pixels, deterministic
  * split-K partials in the workspace, then a fixed-order combine into dw [cout][3][3][cin] (beta-accumulate). */
 int mvae_conv2d_wgrad_upsample_nhwc(const float* dy, const float* x, float* dw, float* dbias, float beta, int nb,
@@ -71,10 +83,15 @@ int mvae_conv2d_wgrad_upsample_nhwc(const float* dy, const float* x, float* dw, 
                                     void* stream);
 size_t mvae_conv2d_wgrad_upsample_workspace_bytes(int nb, int h, int w_, int cin, int cout);
 
+/* 3xBF16 operand pre-split (same bytes as the fp32 tensor): per 4 values hi0..hi3 lo0..lo3 bf16,
+ * hi = bf16(x) (round to nearest even), lo = bf16(x - hi). The weight-prep entry points below take
+ * `split` to emit this layout directly (along their contiguous dimension, which must be % 4). */
+int mvae_split_bf16(const float* x, void* y, long long n, void* stream);
+
 /* Weight re-layouts for the input gradient: KRSC -> [cin][kh][kw][cout]; and the 4x4 tap-summed
  * kernel [cin][4][4][cout] for Upsample's conv (encoder_decoder.py:205-209). */
-int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int kw, int cin, void* stream);
-int mvae_conv_weight_upsample_dgrad(const float* w, float* wt, int cout, int cin, void* stream);
+int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int kw, int cin, int split, void* stream);
+int mvae_conv_weight_upsample_dgrad(const float* w, float* wt, int cout, int cin, int split, void* stream);
 
 /* Bias gradient: out[n] = beta*out[n] + sum_rows x[row*ld + n] (conv bias, encoder_decoder.py:123-146). */
 int mvae_bias_grad(const float* x, long long rows, int n, long long ld, float* out, float beta,

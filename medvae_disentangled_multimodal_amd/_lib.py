@@ -28,10 +28,12 @@ SIGNATURES = {
     "mvae_conv2d_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P]),
     "mvae_conv2d_wgrad_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),
     "mvae_conv2d_wgrad_workspace_bytes": (Z, [I, I, I, I, I, I, I]),
-    "mvae_conv_weight_transpose": (I, [P, P, I, I, I, I, P]),
-    "mvae_conv_weight_upsample_dgrad": (I, [P, P, I, I, P]),
-    "mvae_conv2d_upsample_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, P]),
-    "mvae_conv_weight_upsample_fwd": (I, [P, P, I, I, P]),
+    "mvae_conv_weight_transpose": (I, [P, P, I, I, I, I, I, P]),
+    "mvae_conv_weight_upsample_dgrad": (I, [P, P, I, I, I, P]),
+    "mvae_conv2d_dgrad_stride2_nhwc": (I, [P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),
+    "mvae_split_bf16": (I, [P, P, L, P]),
+    "mvae_conv2d_upsample_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, P]),
+    "mvae_conv_weight_upsample_fwd": (I, [P, P, I, I, I, P]),
     "mvae_conv2d_wgrad_upsample_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, P, Z, P]),
     "mvae_conv2d_wgrad_upsample_workspace_bytes": (Z, [I, I, I, I, I]),
     "mvae_bias_grad": (I, [P, L, I, L, P, F, P, Z, P]),

@@ -47,6 +47,19 @@ __device__ __forceinline__ float wave_max_f(float v) {
   return v;
 }
 
+// 3xBF16 operand pre-split of 4 fp32 values (the GEMM staging's split done once, in HBM):
+// {hi0..hi3, lo0..lo3} as bf16, hi = bf16(x) (RNE), lo = bf16(x - hi); 16 B like the fp32 group
+__device__ __forceinline__ unsigned pk_bf16x2(float a, float b) {
+  typedef __attribute__((ext_vector_type(2))) float f2;
+  typedef __attribute__((ext_vector_type(2))) __bf16 h2;
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f2{a, b}, h2));
+}
+__device__ __forceinline__ uint4 split4_bf16(float4 v) {
+  const unsigned h01 = pk_bf16x2(v.x, v.y), h23 = pk_bf16x2(v.z, v.w);
+  return uint4{h01, h23, pk_bf16x2(v.x - __uint_as_float(h01 << 16), v.y - __uint_as_float(h01 & 0xFFFF0000u)),
+               pk_bf16x2(v.z - __uint_as_float(h23 << 16), v.w - __uint_as_float(h23 & 0xFFFF0000u))};
+}
+
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace mvae

@@ -3,6 +3,19 @@
 
 using namespace mvae;
 
+// wc[ci][t][co] = wt[ci][tap[t]][co] for the nt taps of one parity class (wt = [cin][rs][cout])
+__global__ void __launch_bounds__(256) tap_select_kernel(const float* __restrict__ wt, float* __restrict__ wc, int cin,
+                                                         int rs, int cout, int nt, int4 taps) {
+  const long long tot = (long long)cin * nt * cout;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < tot; e += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(e % cout);
+    const long long r = e / cout;
+    const int t = (int)(r % nt), ci = (int)(r / nt);
+    const int tap = t == 0 ? taps.x : t == 1 ? taps.y : t == 2 ? taps.z : taps.w;
+    wc[e] = wt[((long long)ci * rs + tap) * cout + co];
+  }
+}
+
 static bool kperm_enabled() {  // MVAE_NO_KPERM=1: reference K order (A/B experiments)
   static const bool on = getenv("MVAE_NO_KPERM") == nullptr;
   return on;
@@ -19,6 +32,8 @@ extern "C" {
 int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const float* residual,
                      float* y, int nb, int h, int wd, int cin, int cout, int kh, int kw,
                      int stride, int pad_t, int pad_l, int ho, int wo, int mode, void* stream) {
+  const bool presplit = (mode & MVAE_CONV_WSPLIT) != 0;
+  mode &= ~MVAE_CONV_WSPLIT;
   if (nb <= 0 || h <= 0 || wd <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || ho <= 0 || wo <= 0 ||
       stride <= 0 || mode < 0 || mode > 2 || (mode == 2 && (stride & (stride - 1)))) {
     set_error("conv2d: bad geometry");
@@ -34,6 +49,7 @@ int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const fl
   const int chunk = (int)std::min<long long>(nb, MAX_DESC_BYTES / std::max(in_img, out_img));
   hipStream_t st = (hipStream_t)stream;
   const bool v = (cin % 4 == 0) && al16(x) && al16(w);
+  if (presplit && !v) { set_error("conv2d: pre-split weights need cin %% 4 == 0 and 16-B aligned x, w"); return MVAE_EINVAL; }
   int shift = 0;
   while ((1 << shift) < stride) ++shift;
   for (int b0 = 0; b0 < nb; b0 += chunk) {
@@ -52,7 +68,11 @@ int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const fl
     set_gather_magic(a);
     a.stride = stride; a.stride_shift = shift; a.pad_t = pad_t; a.pad_l = pad_l;
     const int cfg = choose_tile(a, v, false);
-    if (mode == 0) {
+    if (presplit) {  // w holds split4_bf16 groups (MVAE_CONV_WSPLIT): no staging split for B
+      if (mode == 0) launch_big<A_CONV_FWD, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
+      else if (mode == 1) launch_big<A_CONV_UPS, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
+      else launch_big<A_CONV_DGRAD, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
+    } else if (mode == 0) {
       if (v) launch_big<A_CONV_FWD, 4, B_ROWK, 4>(a, st, cfg);
       else launch_small<A_CONV_FWD, 1, B_ROWK, 1>(a, st, cfg);
     } else if (mode == 1) {
@@ -68,6 +88,88 @@ int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const fl
   return MVAE_OK;
 }
 
+// Input gradient of a stride-2 convolution (Downsample, encoder_decoder.py:184-188) by parity class:
+// dx pixel (2m+p, 2j+q) only receives the taps r with r = p + pad_t (mod 2) (and likewise s), so each
+// of the 4 classes is a dense stride-1 conv of dY with its own <= 2x2 taps (9 taps over the 4 classes)
+// instead of the 9-tap transposed gather at every dx pixel, 3/4 of whose taps fall in stride holes.
+// wt = [cin][kh][kw][cout] (mvae_conv_weight_transpose); needs even h, w; workspace >= 4*kh*kw*cin*cout B.
+int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, int nb, int h, int wd, int cin,
+                                   int cout, int kh, int kw, int pad_t, int pad_l, int ho, int wo, int w_split,
+                                   float* workspace, size_t workspace_bytes, void* stream) {
+  if (nb <= 0 || h <= 0 || wd <= 0 || (h & 1) || (wd & 1) || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 ||
+      kh > 4 || kw > 4 || ho <= 0 || wo <= 0) {
+    set_error("dgrad_stride2: bad geometry (needs even h, w and kernel <= 4)");
+    return MVAE_EINVAL;
+  }
+  if (workspace == nullptr || workspace_bytes < (size_t)kh * kw * cin * cout * 4) {
+    set_error("dgrad_stride2: workspace too small");
+    return MVAE_EWORKSPACE;
+  }
+  const long long in_img = (long long)ho * wo * cout * 4, out_img = (long long)h * wd * cin * 4;
+  if (std::max(in_img, out_img) > MAX_DESC_BYTES || (long long)kh * kw * cin * cout * 4 > MAX_DESC_BYTES) {
+    set_error("dgrad_stride2: one image exceeds 4 GiB");
+    return MVAE_EINVAL;
+  }
+  const int chunk = (int)std::min<long long>(nb, MAX_DESC_BYTES / std::max(in_img, out_img));
+  hipStream_t st = (hipStream_t)stream;
+  const int hc = h / 2, wc = wd / 2;
+  float* wcls = workspace;
+  bool empty_class = false;  // a kernel too small to reach every parity: those dx pixels are 0
+  for (int p = 0; p < 2; ++p) {
+    bool hr = false, hs = false;
+    for (int r = 0; r < kh; ++r) hr |= ((p + pad_t - r) & 1) == 0;
+    for (int s_ = 0; s_ < kw; ++s_) hs |= ((p + pad_l - s_) & 1) == 0;
+    empty_class |= !hr || !hs;
+  }
+  if (empty_class && hipMemsetAsync(dx, 0, (size_t)nb * out_img, st) != hipSuccess) return launch_status();
+  for (int cls = 0; cls < 4; ++cls) {
+    const int p = cls >> 1, q = cls & 1;
+    // taps of this class in increasing dY row: r with (p + pad_t - r) even, descending r
+    int rl[4], sl[4], nr = 0, ns = 0;
+    for (int r = kh - 1; r >= 0; --r)
+      if (((p + pad_t - r) & 1) == 0) rl[nr++] = r;
+    for (int s_ = kw - 1; s_ >= 0; --s_)
+      if (((q + pad_l - s_) & 1) == 0) sl[ns++] = s_;
+    const int nt = nr * ns;
+    if (nt == 0) continue;  // zero-filled above
+    int tp[4] = {0, 0, 0, 0};
+    for (int a = 0; a < nr; ++a)
+      for (int b = 0; b < ns; ++b) tp[a * ns + b] = rl[a] * kw + sl[b];
+    if (nt > 4) { set_error("dgrad_stride2: class with more than 4 taps"); return MVAE_EINVAL; }
+    const long long tot = (long long)cin * nt * cout;
+    hipLaunchKernelGGL(tap_select_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 8192)), dim3(256), 0,
+                       st, wt, wcls, cin, kh * kw, cout, nt, make_int4(tp[0], tp[1], tp[2], tp[3]));
+    // dY row of class row m for tap a: m - pt + a with pt = (r_max - p - pad_t) / 2
+    const int pt = (rl[0] - p - pad_t) / 2, pl = (sl[0] - q - pad_l) / 2;
+    const bool v = (cout % 4 == 0) && al16(dy) && al16(wcls);
+    if (w_split && !v) { set_error("dgrad_stride2: pre-split weights need cout %% 4 == 0"); return MVAE_EINVAL; }
+    for (int b0 = 0; b0 < nb; b0 += chunk) {
+      const int n = std::min(chunk, nb - b0);
+      GemmArgs a{};
+      a.M = n * hc * wc; a.N = cin; a.K = nt * cout; a.batch = 1; a.splits = 1; a.k_split = a.K;
+      a.A = dy + (long long)b0 * (in_img / 4);
+      a.B = wcls; a.ldb = a.K;
+      a.C = dx + (long long)b0 * (out_img / 4); a.ldc = cin;
+      a.alpha = 1.f; a.beta = 0.f;
+      a.a_bytes = (unsigned)(in_img * n); a.b_bytes = (unsigned)(tot * 4);
+      a.c_bytes = (unsigned)(out_img * n); a.r_bytes = 0;
+      a.H = ho; a.W = wo; a.Cx = cout; a.Ho = hc; a.Wo = wc; a.R = nr; a.S = ns;
+      a.perm_rs = (v && cout % BK == 0 && nt > 1 && kperm_enabled()) ? nt : 1;
+      set_gather_magic(a);
+      a.stride = 1; a.stride_shift = 0; a.pad_t = pt; a.pad_l = pl;
+      a.sub_w2 = wd; a.sub_par = cls; a.out_remap = 1;
+      const int cfg = choose_tile(a, v, false);
+      if (w_split) launch_big<A_CONV_FWD, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
+      else if (v) launch_big<A_CONV_FWD, 4, B_ROWK, 4>(a, st, cfg);
+      else launch_small<A_CONV_FWD, 1, B_ROWK, 1>(a, st, cfg);
+      const int rc = gemm_finish(a, st);
+      if (rc) return rc;
+    }
+    wcls += tot;
+  }
+  return MVAE_OK;
+}
+
 // Sub-pixel form of Upsample's convolution (nearest x2 then 3x3, stride 1, pad 1;
 // encoder_decoder.py:194-209): output parity class (ph, pw) -- pixels (2i+ph, 2j+pw) -- is a 2x2 conv of
 // the LOW-resolution input x with the tap-summed weights w4[2*ph+pw] ([cout][2][2][cin], from
@@ -75,7 +177,7 @@ int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const fl
 // upsampled intermediate. The 4 classes are one batched launch whose epilogue writes interleaved rows.
 // y [nb][2h][2wd][cout] = conv3x3(upsample2(x)) + bias + residual
 int mvae_conv2d_upsample_nhwc(const float* x, const float* w4, const float* bias, const float* residual, float* y,
-                              int nb, int h, int wd, int cin, int cout, void* stream) {
+                              int nb, int h, int wd, int cin, int cout, int w_split, void* stream) {
   if (nb <= 0 || h <= 0 || wd <= 0 || cin <= 0 || cout <= 0) {
     set_error("conv2d_upsample: bad geometry");
     return MVAE_EINVAL;
@@ -89,6 +191,7 @@ int mvae_conv2d_upsample_nhwc(const float* x, const float* w4, const float* bias
   const int chunk = (int)std::min<long long>(nb, MAX_DESC_BYTES / std::max(in_img, out_img));
   hipStream_t st = (hipStream_t)stream;
   const bool v = (cin % 4 == 0) && al16(x) && al16(w4);
+  if (w_split && !v) { set_error("conv2d_upsample: pre-split weights need cin %% 4 == 0"); return MVAE_EINVAL; }
   for (int b0 = 0; b0 < nb; b0 += chunk) {
     const int n = std::min(chunk, nb - b0);
     GemmArgs a{};
@@ -106,7 +209,8 @@ int mvae_conv2d_upsample_nhwc(const float* x, const float* w4, const float* bias
     a.stride = 1; a.stride_shift = 0; a.pad_t = 1; a.pad_l = 1;
     a.sub_w2 = 2 * wd; a.sub_par = 0; a.out_remap = 1;
     const int cfg = choose_tile(a, v, false);
-    if (v) launch_big<A_CONV_SUBPIX, 4, B_ROWK, 4>(a, st, cfg);
+    if (w_split) launch_big<A_CONV_SUBPIX, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
+    else if (v) launch_big<A_CONV_SUBPIX, 4, B_ROWK, 4>(a, st, cfg);
     else launch_small<A_CONV_SUBPIX, 1, B_ROWK, 1>(a, st, cfg);
     const int rc = gemm_finish(a, st);
     if (rc) return rc;

@@ -32,18 +32,20 @@
 #include "common.h"
 #include <algorithm>
 #include <stdlib.h>
+#include <type_traits>
 
 namespace mvae {
 
 // operand kinds
 enum { A_ROWK = 0, A_COLM = 1, A_CONV_FWD = 2, A_CONV_UPS = 3, A_CONV_DGRAD = 4, A_CONV_SUBPIX = 5, A_COLM_PIX = 6 };
-enum { B_ROWK = 0, B_COLN = 1, B_WGRAD_FWD = 2, B_WGRAD_UPS = 3, B_WGRAD_SUBPIX = 4 };
+enum { B_ROWK = 0, B_COLN = 1, B_WGRAD_FWD = 2, B_WGRAD_UPS = 3, B_WGRAD_SUBPIX = 4, B_ROWK_SPLIT = 5 };
 // MODE_SUBPIX: one parity class (ph, pw) of "nearest-x2 upsample then 3x3 conv" as a stride-1 2x2 conv
 // on the low-resolution input whose padding shifts with the parity: pad = pad_t - ph (batch entry
 // bidx = 2*ph + pw carries the class)
 enum { MODE_FWD = 0, MODE_UPS = 1, MODE_DGRAD = 2, MODE_SUBPIX = 3 };
 
 constexpr int BK = 32;
+constexpr int MVAE_CONV_WSPLIT = 16;  // mvae_conv2d_nhwc mode flag: weights hold split4_bf16 groups
 
 // Exact division by a runtime constant d for 0 <= n < 2^31 (Granlund-Montgomery, N = 31):
 // q = (n * m) >> (31 + l), l = ceil(log2 d), m = floor(2^(31+l) / d) + 1 (< 2^32).
@@ -141,14 +143,26 @@ struct Img {
   static constexpr int SIZE = 2 * PLANE;
 };
 
-// PREC 3: hi and lo planes (3xBF16); PREC 1: hi plane only (bf16 operands, fp32 accumulate)
+// PREC 3: hi and lo planes (3xBF16); PREC 1: hi plane only (bf16 operands, fp32 accumulate).
+// hi = bf16(x), lo = bf16(x - hi); per element pair: 2 cvt_pk, 1 shift + 1 and (hi back to fp32), 2 sub
 template <int PREC>
 __device__ __forceinline__ void st_split(__bf16* img, int plane, int off, const float4& v) {
-  const __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y, h2 = (__bf16)v.z, h3 = (__bf16)v.w;
-  *(bf16x4*)(img + off) = bf16x4{h0, h1, h2, h3};
-  if constexpr (PREC == 3)
-    *(bf16x4*)(img + plane + off) = bf16x4{(__bf16)(v.x - (float)h0), (__bf16)(v.y - (float)h1),
-                                           (__bf16)(v.z - (float)h2), (__bf16)(v.w - (float)h3)};
+  typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
+  const unsigned h01 = pk_bf16x2(v.x, v.y), h23 = pk_bf16x2(v.z, v.w);
+  *(u32x2_t*)(img + off) = u32x2_t{h01, h23};
+  if constexpr (PREC == 3) {
+    const unsigned l01 = pk_bf16x2(v.x - __uint_as_float(h01 << 16), v.y - __uint_as_float(h01 & 0xFFFF0000u));
+    const unsigned l23 = pk_bf16x2(v.z - __uint_as_float(h23 << 16), v.w - __uint_as_float(h23 & 0xFFFF0000u));
+    *(u32x2_t*)(img + plane + off) = u32x2_t{l01, l23};
+  }
+}
+
+// slot already split in HBM (split4_bf16 layout: per 4 elements hi0..hi3 then lo0..lo3, 16 B)
+template <int PREC>
+__device__ __forceinline__ void st_presplit(__bf16* img, int plane, int off, const float4& v) {
+  typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
+  *(u32x2_t*)(img + off) = u32x2_t{__float_as_uint(v.x), __float_as_uint(v.y)};
+  if constexpr (PREC == 3) *(u32x2_t*)(img + plane + off) = u32x2_t{__float_as_uint(v.z), __float_as_uint(v.w)};
 }
 
 // fragment of a 32x32x16 MFMA operand: lane l holds element [row0 + (l&31)][ks*16 + 8*(l>>5) + j]
@@ -216,7 +230,7 @@ __device__ __forceinline__ int row_of_tid(int tid) {
 // ------------------------------------------------------------------------------------------
 
 // ROW image, source element (row, k) at P[row*ld + k]
-template <int ROWS, int VEC, int NT, bool IS_A, int PREC>
+template <int ROWS, int VEC, int NT, bool IS_A, int PREC, bool PRESPLIT = false>
 struct LoadRowK {
   static constexpr bool COL = false;
   static constexpr int RP = NT / 8;     // rows per pass (8 float4 per 32-wide row)
@@ -245,7 +259,10 @@ struct LoadRowK {
     }
   }
   __device__ void store_slot(__bf16* img, int i) {
-    st_split<PREC>(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+    if constexpr (PRESPLIT)
+      st_presplit<PREC>(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+    else
+      st_split<PREC>(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
   }
   __device__ void advance() { k += BK; }
   __device__ void load(const GemmArgs& a) {
@@ -567,6 +584,8 @@ template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<6, ROWS, VEC, NT, true, PREC> : LoadColPix<ROWS, VEC, NT, PREC> {};
 template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<4, ROWS, VEC, NT, false, PREC> : LoadWgradX<ROWS, VEC, NT, MODE_SUBPIX, PREC> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<5, ROWS, VEC, NT, false, PREC> : LoadRowK<ROWS, VEC, NT, false, PREC, true> {};
 
 template <int BM, int BN, int WGM, int WGN, int AK, int VA, int BKIND, int VB, int PREC>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
@@ -666,63 +685,69 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   // otherwise hoist all staging VALU into one block ahead of the MFMAs, idling the MFMA pipe).
   constexpr int STEPS = 2 * TM;
   constexpr int NSL = LA::NS + LB::NS;
-  for (; t + 2 < nt; ++t) {
-    __bf16* nb = lds + ((t & 1) ^ 1) * BUF;
-    const __bf16* Ai = lds + (t & 1) * BUF;
-    const __bf16* Bi = Ai + IA::SIZE;
-    la.advance();
-    lb.advance();
-    la.prep(a);
-    lb.prep(a);
-    bf16x8 bh[TN], bl[TN], ah[2], al[2];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      bh[j] = read_frag<BN, LB::COL>(Bi, brow + j * 32, 0, lane);
-      if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, 0, lane);
-    }
-    ah[0] = read_frag<BM, LA::COL>(Ai, arow, 0, lane);
-    if constexpr (PREC == 3) al[0] = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow, 0, lane);
-#pragma unroll
-    for (int st = 0; st < STEPS; ++st) {
-      const int i = st % TM, cur = st & 1;
-      if (st + 1 < STEPS) {
-        const int ks1 = (st + 1) / TM, i1 = (st + 1) % TM;
-        ah[cur ^ 1] = read_frag<BM, LA::COL>(Ai, arow + i1 * 32, ks1, lane);
-        if constexpr (PREC == 3) al[cur ^ 1] = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow + i1 * 32, ks1, lane);
-      }
+  // STAG: the wave runs each step's staging share BEFORE its MFMAs instead of after. Given to the
+  // second half of the workgroup (waves 4-7 share SIMDs with waves 0-3), it staggers the two waves of
+  // every SIMD: one issues VALU/LDS staging while its partner's MFMAs occupy the matrix pipe.
+  auto kloop = [&](auto stag) {
+    constexpr bool STAG = decltype(stag)::value;
+    for (; t + 2 < nt; ++t) {
+      __bf16* nb = lds + ((t & 1) ^ 1) * BUF;
+      const __bf16* Ai = lds + (t & 1) * BUF;
+      const __bf16* Bi = Ai + IA::SIZE;
+      la.advance();
+      lb.advance();
+      la.prep(a);
+      lb.prep(a);
+      bf16x8 bh[TN], bl[TN], ah[2], al[2];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        mma<PREC>(acc[i][j], ah[cur], al[cur], bh[j], bl[j]);
+        bh[j] = read_frag<BN, LB::COL>(Bi, brow + j * 32, 0, lane);
+        if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, 0, lane);
       }
-      if (st == TM - 1) {  // B fragments of the second k-half
+      ah[0] = read_frag<BM, LA::COL>(Ai, arow, 0, lane);
+      if constexpr (PREC == 3) al[0] = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow, 0, lane);
+      auto stage = [&](int st) {
+#pragma unroll
+        for (int q = st * NSL / STEPS; q < (st + 1) * NSL / STEPS; ++q) {
+          if (q < LA::NS) {
+            la.store_slot(nb, q);
+            la.load_slot(a, q);
+          } else {
+            lb.store_slot(nb + IA::SIZE, q - LA::NS);
+            lb.load_slot(a, q - LA::NS);
+          }
+        }
+      };
+#pragma unroll
+      for (int st = 0; st < STEPS; ++st) {
+        const int i = st % TM, cur = st & 1;
+        if constexpr (STAG) {
+          stage(st);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (st + 1 < STEPS) {
+          const int ks1 = (st + 1) / TM, i1 = (st + 1) % TM;
+          ah[cur ^ 1] = read_frag<BM, LA::COL>(Ai, arow + i1 * 32, ks1, lane);
+          if constexpr (PREC == 3) al[cur ^ 1] = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow + i1 * 32, ks1, lane);
+        }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          bh[j] = read_frag<BN, LB::COL>(Bi, brow + j * 32, 1, lane);
-          if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, 1, lane);
+          mma<PREC>(acc[i][j], ah[cur], al[cur], bh[j], bl[j]);
         }
-      }
+        if (st == TM - 1) {  // B fragments of the second k-half
 #pragma unroll
-      for (int q = st * NSL / STEPS; q < (st + 1) * NSL / STEPS; ++q) {
-        if (q < LA::NS) {
-#ifndef MVAE_EXP_NOSTORE
-          la.store_slot(nb, q);
-#endif
-#ifndef MVAE_EXP_NOLOAD
-          la.load_slot(a, q);
-#endif
-        } else {
-#ifndef MVAE_EXP_NOSTORE
-          lb.store_slot(nb + IA::SIZE, q - LA::NS);
-#endif
-#ifndef MVAE_EXP_NOLOAD
-          lb.load_slot(a, q - LA::NS);
-#endif
+          for (int j = 0; j < TN; ++j) {
+            bh[j] = read_frag<BN, LB::COL>(Bi, brow + j * 32, 1, lane);
+            if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, 1, lane);
+          }
         }
+        if constexpr (!STAG) stage(st);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
     }
-    __syncthreads();
-  }
+  };
+    kloop(std::false_type{});
 #else
   for (; t + 2 < nt; ++t) {  // block staging: all of tile t+1's staging, then tile t's MFMAs
     __bf16* nb = lds + ((t & 1) ^ 1) * BUF;

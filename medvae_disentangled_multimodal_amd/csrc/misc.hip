@@ -12,8 +12,32 @@ namespace mvae {
 
 // per tap t: [cout][cin] (row stride rs*cin) -> [cin][cout] (row stride rs*cout), 64x64 tiles through
 // LDS so both the reads (along cin) and the writes (along cout) are coalesced
+// write phase of a transposed 64x64 tile: tile[o_local][c_local] -> wt rows c (row stride rs*cout, tap t)
+// along o; split: groups of 4 consecutive o as split4_bf16 (needs cout % 4 == 0)
+__device__ __forceinline__ void write_transposed(const float (*tile)[65], float* __restrict__ wt, int c0, int o0, int t,
+                                                 int rs, int cin, int cout, int split) {
+  if (!split) {
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = c0 + ty + 4 * i, o = o0 + tx;
+      if (o < cout && c < cin) wt[((long long)c * rs + t) * cout + o] = tile[tx][ty + 4 * i];
+    }
+  } else {
+    const int g = threadIdx.x & 15, cr = threadIdx.x >> 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cl = cr + 16 * i, c = c0 + cl, o = o0 + 4 * g;
+      if (o < cout && c < cin) {
+        const float4 v{tile[4 * g][cl], tile[4 * g + 1][cl], tile[4 * g + 2][cl], tile[4 * g + 3][cl]};
+        *(uint4*)(wt + ((long long)c * rs + t) * cout + o) = split4_bf16(v);
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) w_transpose_kernel(const float* __restrict__ w, float* __restrict__ wt,
-                                                          int cout, int rs, int cin) {
+                                                          int cout, int rs, int cin, int split) {
   __shared__ float tile[64][65];
   const int t = blockIdx.z;
   const int c0 = blockIdx.x * 64, o0 = blockIdx.y * 64;
@@ -24,11 +48,7 @@ __global__ void __launch_bounds__(256) w_transpose_kernel(const float* __restric
     tile[ty + 4 * i][tx] = (o < cout && c < cin) ? w[((long long)o * rs + t) * cin + c] : 0.f;
   }
   __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int c = c0 + ty + 4 * i, o = o0 + tx;
-    if (o < cout && c < cin) wt[((long long)c * rs + t) * cout + o] = tile[tx][ty + 4 * i];
-  }
+  write_transposed(tile, wt, c0, o0, t, rs, cin, cout, split);
 }
 
 __device__ __forceinline__ int tap_mask(int t) {
@@ -39,7 +59,7 @@ __device__ __forceinline__ int tap_mask(int t) {
 // grid (cin/64, cout/64, 16 effective taps): sum the <= 4 contributing source taps of a 64x64
 // [cout][cin] tile (coalesced along cin), transpose through LDS, write along cout
 __global__ void __launch_bounds__(256) w_ups_dgrad_kernel(const float* __restrict__ w, float* __restrict__ wt,
-                                                          int cout, int cin) {
+                                                          int cout, int cin, int split) {
   __shared__ float tile[64][65];
   const int tu = blockIdx.z;
   const int mt = tap_mask(tu >> 2), mu = tap_mask(tu & 3);
@@ -59,11 +79,7 @@ __global__ void __launch_bounds__(256) w_ups_dgrad_kernel(const float* __restric
     tile[ty + 4 * i][tx] = s;
   }
   __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int c = c0 + ty + 4 * i, o = o0 + tx;
-    if (o < cout && c < cin) wt[((long long)c * 16 + tu) * cout + o] = tile[tx][ty + 4 * i];
-  }
+  write_transposed(tile, wt, c0, o0, tu, 16, cin, cout, split);
 }
 
 // forward weights of the sub-pixel Upsample conv: w4[2*ph+pw][co][a][b][ci] = sum of w[co][r][s][ci] over
@@ -71,15 +87,19 @@ __global__ void __launch_bounds__(256) w_ups_dgrad_kernel(const float* __restric
 __device__ __forceinline__ int sub_mask(int p, int a) { return p == 0 ? (a == 0 ? 0b001 : 0b110) : (a == 0 ? 0b011 : 0b100); }
 
 __global__ void __launch_bounds__(256) w_ups_fwd_kernel(const float* __restrict__ w, float* __restrict__ w4, int cout,
-                                                        int cin) {
+                                                        int cin, int split) {
+  // one thread per (co, group of 4 ci) (split; cin % 4 == 0) or per (co, ci)
+  const int gw = split ? 4 : 1, ng = cin / gw;
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long long)cout * cin) return;
-  const int co = (int)(idx / cin), ci = (int)(idx - (long long)co * cin);
-  float t[3][3];
+  if (idx >= (long long)cout * ng) return;
+  const int co = (int)(idx / ng), ci = (int)(idx - (long long)co * ng) * gw;
+  float t[3][3][4];
 #pragma unroll
   for (int r = 0; r < 3; ++r)
 #pragma unroll
-    for (int s = 0; s < 3; ++s) t[r][s] = w[(((long long)co * 3 + r) * 3 + s) * cin + ci];
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[r][s][e] = e < gw ? w[(((long long)co * 3 + r) * 3 + s) * cin + ci + e] : 0.f;
 #pragma unroll
   for (int cls = 0; cls < 4; ++cls)
 #pragma unroll
@@ -87,14 +107,23 @@ __global__ void __launch_bounds__(256) w_ups_fwd_kernel(const float* __restrict_
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const int mr = sub_mask(cls >> 1, a), ms = sub_mask(cls & 1, b);
-        float v = 0.f;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < 3; ++r)
 #pragma unroll
           for (int s = 0; s < 3; ++s)
-            if (((mr >> r) & 1) && ((ms >> s) & 1)) v += t[r][s];
-        w4[((((long long)cls * cout + co) * 2 + a) * 2 + b) * cin + ci] = v;
+            if (((mr >> r) & 1) && ((ms >> s) & 1))
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += t[r][s][e];
+        float* o = w4 + ((((long long)cls * cout + co) * 2 + a) * 2 + b) * cin + ci;
+        if (split) *(uint4*)o = split4_bf16(float4{v[0], v[1], v[2], v[3]});
+        else *o = v[0];
       }
+}
+
+__global__ void __launch_bounds__(256) split_bf16_kernel(const float4* __restrict__ x, uint4* __restrict__ y, long long n4) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x)
+    y[i] = split4_bf16(x[i]);
 }
 
 // column sums: part[chunk][n] = sum over rows in chunk ; then out[n] += sum_chunks (fixed order)
@@ -138,27 +167,37 @@ using namespace mvae;
 
 extern "C" {
 
-int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int kw, int cin, void* stream) {
-  if (cout <= 0 || kh <= 0 || kw <= 0 || cin <= 0) { set_error("w_transpose: bad sizes"); return MVAE_EINVAL; }
+int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int kw, int cin, int split, void* stream) {
+  if (cout <= 0 || kh <= 0 || kw <= 0 || cin <= 0 || (split && (cout & 3))) {
+    set_error("w_transpose: bad sizes");
+    return MVAE_EINVAL;
+  }
   hipLaunchKernelGGL(w_transpose_kernel, dim3((cin + 63) / 64, (cout + 63) / 64, kh * kw), dim3(256), 0,
-                     (hipStream_t)stream, w, wt, cout, kh * kw, cin);
+                     (hipStream_t)stream, w, wt, cout, kh * kw, cin, split);
   return launch_status();
 }
 
 // wt [cin][4][4][cout] for the dgrad of "nearest-x2 upsample then 3x3 conv"
-int mvae_conv_weight_upsample_dgrad(const float* w, float* wt, int cout, int cin, void* stream) {
-  if (cout <= 0 || cin <= 0) { set_error("w_ups: bad sizes"); return MVAE_EINVAL; }
+int mvae_conv_weight_upsample_dgrad(const float* w, float* wt, int cout, int cin, int split, void* stream) {
+  if (cout <= 0 || cin <= 0 || (split && (cout & 3))) { set_error("w_ups: bad sizes"); return MVAE_EINVAL; }
   hipLaunchKernelGGL(w_ups_dgrad_kernel, dim3((cin + 63) / 64, (cout + 63) / 64, 16), dim3(256), 0,
-                     (hipStream_t)stream, w, wt, cout, cin);
+                     (hipStream_t)stream, w, wt, cout, cin, split);
   return launch_status();
 }
 
 // w4 [4][cout][2][2][cin] for the sub-pixel forward of "nearest-x2 upsample then 3x3 conv"
-int mvae_conv_weight_upsample_fwd(const float* w, float* w4, int cout, int cin, void* stream) {
-  if (cout <= 0 || cin <= 0) { set_error("w_ups_fwd: bad sizes"); return MVAE_EINVAL; }
-  const long long tot = (long long)cout * cin;
+int mvae_conv_weight_upsample_fwd(const float* w, float* w4, int cout, int cin, int split, void* stream) {
+  if (cout <= 0 || cin <= 0 || (split && (cin & 3))) { set_error("w_ups_fwd: bad sizes"); return MVAE_EINVAL; }
+  const long long tot = (long long)cout * (split ? cin / 4 : cin);
   hipLaunchKernelGGL(w_ups_fwd_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, w, w4,
-                     cout, cin);
+                     cout, cin, split);
+  return launch_status();
+}
+
+int mvae_split_bf16(const float* x, void* y, long long n, void* stream) {
+  if (n <= 0 || (n & 3)) { set_error("split_bf16: n must be a positive multiple of 4"); return MVAE_EINVAL; }
+  hipLaunchKernelGGL(split_bf16_kernel, dim3(egrid(n / 4)), dim3(256), 0, (hipStream_t)stream, (const float4*)x, (uint4*)y,
+                     n / 4);
   return launch_status();
 }
 

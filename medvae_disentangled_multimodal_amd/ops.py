@@ -168,6 +168,15 @@ def _subpixel_upsample(g: ConvGeom) -> bool:
 
 
 SUBPIXEL_UPSAMPLE = os.environ.get("MVAE_NO_SUBPIXEL") is None
+STRIDE2_CLASSES = os.environ.get("MVAE_NO_STRIDE2_CLASSES") is None
+# weight operands handed to the GEMM pre-split into 3xBF16 hi/lo pairs (include/medvae_hip.h MVAE_CONV_WSPLIT):
+# the split is done once per step by the weight-prep kernels instead of in every workgroup's staging
+WEIGHT_SPLIT = os.environ.get("MVAE_NO_WEIGHT_SPLIT") is None
+MVAE_CONV_WSPLIT = 16
+
+
+def _al16(*ts) -> bool:
+    return all(t.data_ptr() % 16 == 0 for t in ts)
 
 
 def conv2d_forward_raw(x, w, b, res, g: ConvGeom):
@@ -176,29 +185,30 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom):
     ho, wo = g.out_hw(h, wd)
     y = torch.empty((n, co, ho, wo), device=x.device, dtype=torch.float32, memory_format=CL)
     ref = 2.0 * n * ho * wo * co * c * g.kh * g.kw
-    alg = ref * 4 / 9 if _subpixel_upsample(g) else ref
-    w4 = None
-    if _subpixel_upsample(g):  # tap-summed per-class weights (outside the timed GEMM launch)
-        w4 = ARENA.get("w4", 16 * co * c * 4, x.device)
-        _lib.call("mvae_conv_weight_upsample_fwd", w.data_ptr(), w4.data_ptr(), co, c, _stream(x))
+    sub = _subpixel_upsample(g)
+    alg = ref * 4 / 9 if sub else ref
+    st = _stream(x)
+    split = WEIGHT_SPLIT and c % 4 == 0 and _al16(x) and not g.pointwise
+    wg = w
+    if sub:  # tap-summed per-class weights (prepared outside the timed GEMM launch)
+        wg = ARENA.get("w4", 16 * co * c * 4, x.device)
+        _lib.call("mvae_conv_weight_upsample_fwd", w.data_ptr(), wg.data_ptr(), co, c, int(split), st)
+    elif split:
+        wg = ARENA.get("wsplit", w.numel() * 4, x.device)
+        _lib.call("mvae_split_bf16", w.data_ptr(), wg.data_ptr(), w.numel(), st)
     with _timed("conv_fwd", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
-        _conv_fwd_launch(x, w, b, res, y, g, n, c, h, wd, co, ho, wo, w4)
+        if g.pointwise:
+            # 1x1 conv = GEMM [pixels][cin] x [cout][cin]^T
+            _lib.call("mvae_gemm_strided_batched", 0, 1, n * h * wd, co, c, 1.0, x.data_ptr(), c, 0,
+                      w.data_ptr(), c, 0, 0.0, y.data_ptr(), co, 0, 1, _ptr(b), _ptr(res), co, 0, None, 0, st)
+        elif sub:
+            _lib.call("mvae_conv2d_upsample_nhwc", x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n,
+                      h, wd, c, co, int(split), st)
+        else:
+            mode = (1 if g.upsample else 0) | (MVAE_CONV_WSPLIT if split else 0)
+            _lib.call("mvae_conv2d_nhwc", x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n, h, wd, c,
+                      co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, mode, st)
     return y
-
-
-def _conv_fwd_launch(x, w, b, res, y, g, n, c, h, wd, co, ho, wo, w4=None):
-    if g.pointwise:
-        # 1x1 conv = GEMM [pixels][cin] x [cout][cin]^T
-        _lib.call("mvae_gemm_strided_batched", 0, 1, n * h * wd, co, c, 1.0, x.data_ptr(), c, 0,
-                  w.data_ptr(), c, 0, 0.0, y.data_ptr(), co, 0, 1, _ptr(b), _ptr(res), co, 0, None, 0,
-                  _stream(x))
-    elif w4 is not None:
-        st = _stream(x)
-        _lib.call("mvae_conv2d_upsample_nhwc", x.data_ptr(), w4.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n, h,
-                  wd, c, co, st)
-    else:
-        _lib.call("mvae_conv2d_nhwc", x.data_ptr(), w.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n, h, wd, c,
-                  co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, 1 if g.upsample else 0, _stream(x))
 
 
 def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom):
@@ -208,25 +218,36 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom):
     dx = torch.empty((n, c, h, wd), device=dy.device, dtype=torch.float32, memory_format=CL)
     st = _stream(dy)
     flops = 2.0 * n * ho * wo * co * c * g.kh * g.kw  # reference count
+    shp = (n, c, h, wd, co, g.kh, g.stride, g.upsample)
     if g.pointwise:
         # dx[m][c] = sum_n dy[m][n] W[n][c]  (W stored [K=cout][N=cin])
-        with _timed("conv_dgrad", flops, (n, c, h, wd, co, g.kh, g.stride, g.upsample)):
+        with _timed("conv_dgrad", flops, shp):
             _lib.call("mvae_gemm_strided_batched", 0, 0, n * h * wd, c, co, 1.0, dy.data_ptr(), co, 0, w.data_ptr(), c,
                       0, 0.0, dx.data_ptr(), c, 0, 1, None, None, 0, 0, None, 0, st)
         return dx
+    # the dgrad GEMM's K runs over cout: transposed weights [cin][taps][cout], pre-split when cout % 4 == 0
+    split = WEIGHT_SPLIT and co % 4 == 0 and _al16(dy)
+    wflag = MVAE_CONV_WSPLIT if split else 0
     if g.upsample:
         wt = ARENA.get("wt", c * 16 * co * 4, dy.device)
-        _lib.call("mvae_conv_weight_upsample_dgrad", w.data_ptr(), wt.data_ptr(), co, c, st)
+        _lib.call("mvae_conv_weight_upsample_dgrad", w.data_ptr(), wt.data_ptr(), co, c, int(split), st)
         # dX = stride-2, pad-1 4x4 conv of dY with the tap-summed kernel (16 taps per low-res pixel)
-        with _timed("conv_dgrad", flops * 4 / 9, (n, c, h, wd, co, g.kh, g.stride, g.upsample), flops):
+        with _timed("conv_dgrad", flops * 4 / 9, shp, flops):
             _lib.call("mvae_conv2d_nhwc", dy.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
-                      4, 4, 2, 1, 1, h, wd, 0, st)
+                      4, 4, 2, 1, 1, h, wd, wflag, st)
         return dx
     wt = ARENA.get("wt", c * g.kh * g.kw * co * 4, dy.device)
-    _lib.call("mvae_conv_weight_transpose", w.data_ptr(), wt.data_ptr(), co, g.kh, g.kw, c, st)
-    with _timed("conv_dgrad", flops, (n, c, h, wd, co, g.kh, g.stride, g.upsample)):
+    _lib.call("mvae_conv_weight_transpose", w.data_ptr(), wt.data_ptr(), co, g.kh, g.kw, c, int(split), st)
+    if g.stride == 2 and h % 2 == 0 and wd % 2 == 0 and g.kh <= 4 and g.kw <= 4 and STRIDE2_CLASSES:
+        # Downsample's input gradient by dx parity class: only the useful taps (no stride holes)
+        wc = ARENA.get("wcls", c * g.kh * g.kw * co * 4, dy.device)
+        with _timed("conv_dgrad", flops, shp):
+            _lib.call("mvae_conv2d_dgrad_stride2_nhwc", dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, h, wd, c, co,
+                      g.kh, g.kw, g.pad_t, g.pad_l, ho, wo, int(split), wc.data_ptr(), wc.numel(), st)
+        return dx
+    with _timed("conv_dgrad", flops, shp):
         _lib.call("mvae_conv2d_nhwc", dy.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
-                  g.kh, g.kw, g.stride, g.pad_t, g.pad_l, h, wd, 2, st)
+                  g.kh, g.kw, g.stride, g.pad_t, g.pad_l, h, wd, 2 | wflag, st)
     return dx
 
 

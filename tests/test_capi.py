@@ -33,6 +33,25 @@ def test_binding_covers_header():
     assert sorted(_lib.SIGNATURES) == _declared()
 
 
+def _arity():
+    """Parameter count of every declared entry point (ctypes silently passes surplus arguments, so
+    a binding with too few argtypes would shift every later argument)."""
+    src = open(os.path.join(ROOT, "include", "medvae_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(mvae_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", src):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def test_binding_arity_matches_header():
+    ar = _arity()
+    assert sorted(ar) == _declared()
+    bad = {n: (len(_lib.SIGNATURES[n][1]), k) for n, k in ar.items() if len(_lib.SIGNATURES[n][1]) != k}
+    assert not bad, bad
+
+
 def test_loader_binds_and_reports_errors_without_gpu():
     lib = _lib.load()
     assert lib.mvae_abi_version() == 1

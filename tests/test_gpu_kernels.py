@@ -56,6 +56,11 @@ CONV_CASES = [
     (2, 3, 8, 5, 6, 3, 1, (1, 1, 1, 1), True),
     (2, 48, 40, 6, 9, 3, 1, (1, 1, 1, 1), True),
     (16, 512, 256, 8, 8, 3, 1, (1, 1, 1, 1), True),
+    # stride-2 input gradient by parity class: symmetric pad, non-square, 4x4 (PatchGAN), 1x1 (empty classes)
+    (2, 32, 64, 10, 12, 3, 2, (1, 1, 1, 1), False),
+    (2, 16, 32, 16, 16, 4, 2, (1, 1, 1, 1), False),
+    (2, 32, 16, 8, 8, 1, 2, (0, 0, 0, 0), False),
+    (2, 6, 8, 8, 8, 3, 2, (0, 0, 1, 1), False),
 ]
 
 
@@ -105,6 +110,43 @@ def test_conv_fwd_dgrad_wgrad(dev, case):
     assert wm.grad is None and bm.grad is None
     assert rel(wm._mvae_main_grad - 0.5, wr.grad) < CONV_TOL
     assert float((bm._mvae_main_grad.cpu().double() - 0.25 - db_ref).abs().max()) < 1e-5 * scale
+
+
+def test_split_bf16_layout(dev):
+    """mvae_split_bf16: per 4 fp32 values hi0..hi3 lo0..lo3 (bf16), hi = RNE(x), lo = RNE(x - hi)."""
+    from medvae_disentangled_multimodal_amd import _lib
+    x = torch.randn(4096, generator=torch.Generator().manual_seed(3)) * 10.0
+    xd = x.to(dev)
+    y = torch.empty(4096 * 4, dtype=torch.uint8, device=dev)
+    _lib.call("mvae_split_bf16", xd.data_ptr(), y.data_ptr(), 4096, torch.cuda.current_stream().cuda_stream)
+    hl = y.view(torch.bfloat16).view(-1, 2, 4).cpu()
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    assert torch.equal(hl[:, 0].flatten(), hi) and torch.equal(hl[:, 1].flatten(), lo)
+    assert float(((hi.float() + lo.float()) - x).abs().max() / x.abs().max()) < 2 ** -15
+
+
+@pytest.mark.parametrize("split", [0, 1])
+def test_weight_prep_split_layouts(dev, split):
+    """Weight re-layouts with split output equal the fp32 re-layout split afterwards."""
+    from medvae_disentangled_multimodal_amd import _lib
+    g = torch.Generator().manual_seed(11)
+    co, ci = 64, 32
+    w = cl(torch.randn(co, ci, 3, 3, generator=g), dev)
+    st = torch.cuda.current_stream().cuda_stream
+    for name, n_out, args in (("mvae_conv_weight_transpose", 9 * ci * co, (co, 3, 3, ci)),
+                              ("mvae_conv_weight_upsample_dgrad", 16 * ci * co, (co, ci)),
+                              ("mvae_conv_weight_upsample_fwd", 16 * ci * co, (co, ci))):
+        ref = torch.empty(n_out, device=dev)
+        _lib.call(name, w.data_ptr(), ref.data_ptr(), *args, 0, st)
+        out = torch.empty(n_out, device=dev)
+        _lib.call(name, w.data_ptr(), out.data_ptr(), *args, split, st)
+        if split:
+            exp = torch.empty(n_out, device=dev)
+            _lib.call("mvae_split_bf16", ref.data_ptr(), exp.data_ptr(), n_out, st)
+            assert torch.equal(out.view(torch.int32), exp.view(torch.int32)), name
+        else:
+            assert torch.equal(out, ref), name
 
 
 def test_upsample_gather_mode_matches_subpixel(dev):

@@ -10,7 +10,7 @@ mkdir -p "$OUT/obj"
 PKG=$ROOT/medvae_disentangled_multimodal_amd/csrc
 pids=()
 for f in "$PKG"/*.hip "$PKG"/errors.cpp; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -w "$@" -c "$f" -o "$OUT/obj/$(basename "$f").o" &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fno-slp-vectorize --offload-arch=gfx950 -w "$@" -c "$f" -o "$OUT/obj/$(basename "$f").o" &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done
