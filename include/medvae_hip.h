@@ -47,6 +47,9 @@ int mvae_get_math_mode(void);
  * mode | MVAE_CONV_WSPLIT: w is pre-split (mvae_split_bf16 layout; cin % 4 == 0) -- the 3xBF16 hi/lo split of
  * the weight operand is done once per step instead of in every workgroup's staging. */
 #define MVAE_CONV_WSPLIT 16
+/* mode | MVAE_CONV_XSPLIT (mode 0, and mvae_conv2d_wgrad_nhwc mode 0): x is pre-split the same way -- the
+ * GroupNorm output written by mvae_group_norm_fwd_nhwc(y_split=1), whose only consumers are convolutions. */
+#define MVAE_CONV_XSPLIT 32
 int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y,
                      int nb, int h, int w_, int cin, int cout, int kh, int kw, int stride, int pad_t,
                      int pad_l, int ho, int wo, int mode, void* stream);
@@ -116,10 +119,12 @@ int mvae_softmax_rows_bwd(const float* y, const float* dy, float* dx, long long 
 /* ---- GroupNorm (+SiLU, +inverted dropout) -------------------------------------------------------
  * Normalize() = nn.GroupNorm(min(32,C), C, eps=1e-6) (encoder_decoder.py:28-33) fused with
  * nonlinearity() (:13-15) and ResnetBlock's nn.Dropout (:163). mean/rstd: [nb*groups].
- * Backward ACCUMULATES into dgamma/dbeta (flat grad buffer). */
+ * Backward ACCUMULATES into dgamma/dbeta (flat grad buffer).
+ * y_split = 1: y is written in the pre-split 3xBF16 operand layout (mvae_split_bf16) for a following
+ * convolution (MVAE_CONV_XSPLIT); the backward never reads y. */
 int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* beta, float* y, float* mean,
                              float* rstd, int nb, int hw, int c, int groups, float eps, int silu,
-                             float drop_p, unsigned long long seed, void* workspace,
+                             float drop_p, unsigned long long seed, int y_split, void* workspace,
                              size_t workspace_bytes, void* stream);
 int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
                              const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta,

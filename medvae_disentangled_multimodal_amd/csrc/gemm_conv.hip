@@ -33,7 +33,9 @@ int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const fl
                      float* y, int nb, int h, int wd, int cin, int cout, int kh, int kw,
                      int stride, int pad_t, int pad_l, int ho, int wo, int mode, void* stream) {
   const bool presplit = (mode & MVAE_CONV_WSPLIT) != 0;
-  mode &= ~MVAE_CONV_WSPLIT;
+  const bool xsplit = (mode & MVAE_CONV_XSPLIT) != 0;
+  mode &= ~(MVAE_CONV_WSPLIT | MVAE_CONV_XSPLIT);
+  if (xsplit && mode != 0) { set_error("conv2d: a pre-split input needs mode 0"); return MVAE_EINVAL; }
   if (nb <= 0 || h <= 0 || wd <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || ho <= 0 || wo <= 0 ||
       stride <= 0 || mode < 0 || mode > 2 || (mode == 2 && (stride & (stride - 1)))) {
     set_error("conv2d: bad geometry");
@@ -49,7 +51,10 @@ int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const fl
   const int chunk = (int)std::min<long long>(nb, MAX_DESC_BYTES / std::max(in_img, out_img));
   hipStream_t st = (hipStream_t)stream;
   const bool v = (cin % 4 == 0) && al16(x) && al16(w);
-  if (presplit && !v) { set_error("conv2d: pre-split weights need cin %% 4 == 0 and 16-B aligned x, w"); return MVAE_EINVAL; }
+  if ((presplit || xsplit) && !v) {
+    set_error("conv2d: pre-split operands need cin %% 4 == 0 and 16-B aligned x, w");
+    return MVAE_EINVAL;
+  }
   int shift = 0;
   while ((1 << shift) < stride) ++shift;
   for (int b0 = 0; b0 < nb; b0 += chunk) {
@@ -68,7 +73,10 @@ int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const fl
     set_gather_magic(a);
     a.stride = stride; a.stride_shift = shift; a.pad_t = pad_t; a.pad_l = pad_l;
     const int cfg = choose_tile(a, v, false);
-    if (presplit) {  // w holds split4_bf16 groups (MVAE_CONV_WSPLIT): no staging split for B
+    if (xsplit) {  // x (and w) hold split4_bf16 groups: no staging split at all
+      if (presplit) launch_big<A_CONV_FWD_SPLIT, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
+      else launch_big<A_CONV_FWD_SPLIT, 4, B_ROWK, 4>(a, st, cfg);
+    } else if (presplit) {  // w holds split4_bf16 groups (MVAE_CONV_WSPLIT): no staging split for B
       if (mode == 0) launch_big<A_CONV_FWD, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
       else if (mode == 1) launch_big<A_CONV_UPS, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
       else launch_big<A_CONV_DGRAD, 4, B_ROWK_SPLIT, 4>(a, st, cfg);

@@ -37,15 +37,19 @@
 namespace mvae {
 
 // operand kinds
-enum { A_ROWK = 0, A_COLM = 1, A_CONV_FWD = 2, A_CONV_UPS = 3, A_CONV_DGRAD = 4, A_CONV_SUBPIX = 5, A_COLM_PIX = 6 };
-enum { B_ROWK = 0, B_COLN = 1, B_WGRAD_FWD = 2, B_WGRAD_UPS = 3, B_WGRAD_SUBPIX = 4, B_ROWK_SPLIT = 5 };
+// *_SPLIT kinds read operands already split into 3xBF16 hi/lo groups in HBM (split4_bf16 layout)
+enum { A_ROWK = 0, A_COLM = 1, A_CONV_FWD = 2, A_CONV_UPS = 3, A_CONV_DGRAD = 4, A_CONV_SUBPIX = 5, A_COLM_PIX = 6,
+       A_CONV_FWD_SPLIT = 7 };
+enum { B_ROWK = 0, B_COLN = 1, B_WGRAD_FWD = 2, B_WGRAD_UPS = 3, B_WGRAD_SUBPIX = 4, B_ROWK_SPLIT = 5,
+       B_WGRAD_FWD_SPLIT = 6 };
 // MODE_SUBPIX: one parity class (ph, pw) of "nearest-x2 upsample then 3x3 conv" as a stride-1 2x2 conv
 // on the low-resolution input whose padding shifts with the parity: pad = pad_t - ph (batch entry
 // bidx = 2*ph + pw carries the class)
 enum { MODE_FWD = 0, MODE_UPS = 1, MODE_DGRAD = 2, MODE_SUBPIX = 3 };
 
 constexpr int BK = 32;
-constexpr int MVAE_CONV_WSPLIT = 16;  // mvae_conv2d_nhwc mode flag: weights hold split4_bf16 groups
+constexpr int MVAE_CONV_WSPLIT = 16;  // conv mode flag: weights hold split4_bf16 groups
+constexpr int MVAE_CONV_XSPLIT = 32;  // conv mode flag: the input activation x holds split4_bf16 groups
 
 // Exact division by a runtime constant d for 0 <= n < 2^31 (Granlund-Montgomery, N = 31):
 // q = (n * m) >> (31 + l), l = ceil(log2 d), m = floor(2^(31+l) / d) + 1 (< 2^32).
@@ -277,7 +281,7 @@ struct LoadRowK {
 };
 
 // ROW image, implicit im2col of an NHWC tensor: element (pixel m, k = (r*S+s)*Cx + c)
-template <int ROWS, int VEC, int NT, int MODE, int PREC>
+template <int ROWS, int VEC, int NT, int MODE, int PREC, bool PRESPLIT = false>
 struct LoadConvA {
   static constexpr bool COL = false;
   static constexpr int RP = NT / 8;
@@ -344,7 +348,10 @@ struct LoadConvA {
     }
   }
   __device__ void store_slot(__bf16* img, int i) {
-    st_split<PREC>(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+    if constexpr (PRESPLIT)
+      st_presplit<PREC>(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+    else
+      st_split<PREC>(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
   }
   __device__ void advance() { k += BK; }
   __device__ void load(const GemmArgs& a) {
@@ -471,7 +478,7 @@ struct LoadColPix {
 
 // COL image for the wgrad B operand: rows n' = (r*S+s)*Cx + c (filter element), k = output pixel.
 // element = X[b][src(oh,ow,r,s)][c], contiguous along c.
-template <int ROWS, int VEC, int NT, int MODE, int PREC>
+template <int ROWS, int VEC, int NT, int MODE, int PREC, bool PRESPLIT = false>
 struct LoadWgradX {
   static constexpr bool COL = true;
   static constexpr int C4 = ROWS / 4;
@@ -537,7 +544,12 @@ struct LoadWgradX {
   __device__ void store_slot(__bf16* img, int i) {
     constexpr int P_ = Img<ROWS, true>::PITCH;
     const int krow = kr + i * (NT / C4);
-    if (krow < BK) st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+    if (krow < BK) {
+      if constexpr (PRESPLIT)
+        st_presplit<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+      else
+        st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+    }
   }
   __device__ void advance() { k += BK; }
   __device__ void load(const GemmArgs& a) {
@@ -586,6 +598,10 @@ template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<4, ROWS, VEC, NT, false, PREC> : LoadWgradX<ROWS, VEC, NT, MODE_SUBPIX, PREC> {};
 template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<5, ROWS, VEC, NT, false, PREC> : LoadRowK<ROWS, VEC, NT, false, PREC, true> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<7, ROWS, VEC, NT, true, PREC> : LoadConvA<ROWS, VEC, NT, MODE_FWD, PREC, true> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<6, ROWS, VEC, NT, false, PREC> : LoadWgradX<ROWS, VEC, NT, MODE_FWD, PREC, true> {};
 
 template <int BM, int BN, int WGM, int WGN, int AK, int VA, int BKIND, int VB, int PREC>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {

@@ -65,7 +65,13 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
                            int wd, int cin, int cout, int kh, int kw, int stride, int pad_t,
                            int pad_l, int ho, int wo, int mode, float* workspace,
                            size_t workspace_bytes, void* stream) {
+  const bool xsplit = (mode & MVAE_CONV_XSPLIT) != 0;  // x holds split4_bf16 groups
+  mode &= ~MVAE_CONV_XSPLIT;
   if (mode != 0 && mode != 1) { set_error("wgrad: mode must be 0 or 1"); return MVAE_EINVAL; }
+  if (xsplit && (mode != 0 || cin % 4 != 0 || !al16(x))) {
+    set_error("wgrad: a pre-split x needs mode 0, cin %% 4 == 0, 16-B alignment");
+    return MVAE_EINVAL;
+  }
   if (nb <= 0 || cin <= 0 || cout <= 0) { set_error("wgrad: bad sizes"); return MVAE_EINVAL; }
   const long long in_img = (long long)h * wd * cin * 4, out_img = (long long)ho * wo * cout * 4;
   if (std::max(in_img, out_img) > MAX_DESC_BYTES || (long long)cout * kh * kw * cin * 4 > MAX_DESC_BYTES) {
@@ -94,7 +100,10 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
     plan_splits(a, cfg, workspace, workspace_bytes - bias_bytes);
     // bias partials live after the split-K partials
     a.bias_ws = dbias ? (float*)((char*)workspace + ((splitk_ws_bytes(a) + 255) & ~(size_t)255)) : nullptr;
-    if (mode == 0) {
+    if (xsplit) {
+      if (va) launch_big<A_COLM, 4, B_WGRAD_FWD_SPLIT, 4>(a, st, cfg);
+      else launch_small<A_COLM, 1, B_WGRAD_FWD_SPLIT, 4>(a, st, cfg);
+    } else if (mode == 0) {
       if (va && vb) launch_big<A_COLM, 4, B_WGRAD_FWD, 4>(a, st, cfg);
       else if (va) launch_small<A_COLM, 4, B_WGRAD_FWD, 1>(a, st, cfg);
       else if (vb) launch_small<A_COLM, 1, B_WGRAD_FWD, 4>(a, st, cfg);

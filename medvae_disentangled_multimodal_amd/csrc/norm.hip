@@ -36,6 +36,7 @@ struct GnArgs {
   float drop_p;
   unsigned long long seed;
   double* ws;  // [nb][chunks][C][2]
+  int y_split;  // forward apply: write y as split4_bf16 groups (the 3xBF16 GEMM operand format)
 };
 
 // Thread mapping shared by the NHWC GroupNorm kernels: a block owns (sample b, chunk of rows); a
@@ -221,7 +222,11 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(GnArgs a, const float* __
               o[k] = (uu >= a.drop_p) ? o[k] / (1.f - a.drop_p) : 0.f;
             }
           }
-          *(float4*)(yp + (long long)r * a.C) = float4{o[0], o[1], o[2], o[3]};
+          const float4 ov{o[0], o[1], o[2], o[3]};
+          if (a.y_split)
+            *(uint4*)(yp + (long long)r * a.C) = split4_bf16(ov);
+          else
+            *(float4*)(yp + (long long)r * a.C) = ov;
         }
       }
     }
@@ -363,8 +368,8 @@ size_t mvae_group_norm_workspace_bytes(int nb, int hw, int c) {
 // y = [dropout](silu?(GroupNorm(x)))  ; saves mean/rstd [nb*groups]
 int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* beta, float* y, float* mean,
                              float* rstd, int nb, int hw, int c, int groups, float eps, int silu,
-                             float drop_p, unsigned long long seed, void* workspace, size_t workspace_bytes,
-                             void* stream) {
+                             float drop_p, unsigned long long seed, int y_split, void* workspace,
+                             size_t workspace_bytes, void* stream) {
   if (nb <= 0 || hw <= 0 || c <= 0 || (c & 3) || groups <= 0 || c % groups) {
     set_error("group_norm: C must be a multiple of 4 and of groups");
     return MVAE_EINVAL;
@@ -384,7 +389,7 @@ int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* be
   hipLaunchKernelGGL(gn_partial_kernel<0>, dim3(a.chunks, nb), dim3(256), 0, st, a);
   hipLaunchKernelGGL(gn_stats_finalize_kernel, dim3(cdiv((long long)nb * groups, 4)), dim3(256), 0, st, a,
                      mean, rstd, scale, shift, eps);
-  a.silu = silu; a.drop_p = drop_p; a.seed = seed;
+  a.silu = silu; a.drop_p = drop_p; a.seed = seed; a.y_split = y_split;
   hipLaunchKernelGGL(gn_apply_kernel, dim3(a.chunks, nb), dim3(256), 0, st, a, scale, shift, y);
   return launch_status();
 }

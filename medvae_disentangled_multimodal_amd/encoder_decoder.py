@@ -74,9 +74,9 @@ class GroupNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(num_channels))
         self.bias = nn.Parameter(torch.zeros(num_channels))
 
-    def forward(self, x, silu: bool = False, drop_p: float = 0.0):
+    def forward(self, x, silu: bool = False, drop_p: float = 0.0, for_conv: bool = False):
         seed = _next_seed() if drop_p > 0.0 else 0
-        return ops.group_norm(x, self.weight, self.bias, self.num_groups, self.eps, silu, drop_p, seed)
+        return ops.group_norm(x, self.weight, self.bias, self.num_groups, self.eps, silu, drop_p, seed, for_conv)
 
 
 def Normalize(in_channels: int, num_groups: int = 32) -> GroupNorm:
@@ -107,9 +107,9 @@ class ResnetBlock(nn.Module):
     def forward(self, x, temb=None):
         if temb is not None:
             raise NotImplementedError("timestep embeddings are not used by the VAE (temb_channels=0)")
-        h = self.conv1(self.norm1(x, silu=True))
+        h = self.conv1(self.norm1(x, silu=True, for_conv=True))
         p = self.dropout.p if self.training else 0.0
-        h = self.norm2(h, silu=True, drop_p=p)
+        h = self.norm2(h, silu=True, drop_p=p, for_conv=True)
         if self.in_channels != self.out_channels:
             x = self.conv_shortcut(x) if self.use_conv_shortcut else self.nin_shortcut(x)
         return self.conv2(h, residual=x)
@@ -215,7 +215,7 @@ class Encoder(nn.Module):
             if i_level != self.num_resolutions - 1:
                 h = lvl.downsample(h)
         h = self.mid.block_2(self.mid.attn_1(self.mid.block_1(h)))
-        return self.conv_out(self.norm_out(h, silu=True))
+        return self.conv_out(self.norm_out(h, silu=True, for_conv=True))
 
 
 class Decoder(nn.Module):
@@ -271,7 +271,7 @@ class Decoder(nn.Module):
                 h = lvl.upsample(h)
         if self.give_pre_end:
             return h
-        h = self.conv_out(self.norm_out(h, silu=True))
+        h = self.conv_out(self.norm_out(h, silu=True, for_conv=True))
         if self.tanh_out:
             h = torch.tanh(h)
         return h

@@ -173,13 +173,14 @@ STRIDE2_CLASSES = os.environ.get("MVAE_NO_STRIDE2_CLASSES") is None
 # the split is done once per step by the weight-prep kernels instead of in every workgroup's staging
 WEIGHT_SPLIT = os.environ.get("MVAE_NO_WEIGHT_SPLIT") is None
 MVAE_CONV_WSPLIT = 16
+MVAE_CONV_XSPLIT = 32
 
 
 def _al16(*ts) -> bool:
     return all(t.data_ptr() % 16 == 0 for t in ts)
 
 
-def conv2d_forward_raw(x, w, b, res, g: ConvGeom):
+def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False):
     n, c, h, wd = x.shape
     co = w.shape[0]
     ho, wo = g.out_hw(h, wd)
@@ -189,6 +190,8 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom):
     alg = ref * 4 / 9 if sub else ref
     st = _stream(x)
     split = WEIGHT_SPLIT and c % 4 == 0 and _al16(x) and not g.pointwise
+    if x_split and (g.pointwise or g.upsample or c % 4 or not _al16(x)):
+        raise RuntimeError("conv2d: a pre-split input needs a non-pointwise, non-upsample conv with cin % 4 == 0")
     wg = w
     if sub:  # tap-summed per-class weights (prepared outside the timed GEMM launch)
         wg = ARENA.get("w4", 16 * co * c * 4, x.device)
@@ -205,7 +208,7 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom):
             _lib.call("mvae_conv2d_upsample_nhwc", x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n,
                       h, wd, c, co, int(split), st)
         else:
-            mode = (1 if g.upsample else 0) | (MVAE_CONV_WSPLIT if split else 0)
+            mode = (1 if g.upsample else 0) | (MVAE_CONV_WSPLIT if split else 0) | (MVAE_CONV_XSPLIT if x_split else 0)
             _lib.call("mvae_conv2d_nhwc", x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n, h, wd, c,
                       co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, mode, st)
     return y
@@ -251,7 +254,7 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom):
     return dx
 
 
-def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None):
+def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool = False):
     """dw (+ db when given and the conv is not pointwise) accumulate with `beta`. Returns True when
     the bias gradient was produced by the fused wgrad kernel."""
     n, c, h, wd = x.shape
@@ -260,11 +263,13 @@ def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None):
     ref = 2.0 * n * ho * wo * co * c * g.kh * g.kw
     alg = ref * 4 / 9 if _subpixel_upsample(g) else ref
     with _timed("conv_wgrad", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
-        return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db)
+        return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db, x_split)
 
 
-def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None):
+def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_split=False):
     st = _stream(dy)
+    if x_split and (g.pointwise or g.upsample):
+        raise RuntimeError("conv2d wgrad: a pre-split input needs a non-pointwise, non-upsample conv")
     if g.pointwise and db is None:
         m = n * h * wd
         nbytes = _lib.query("mvae_gemm_workspace_bytes", co, c, m, 1)
@@ -281,9 +286,9 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None):
         return db is not None
     nbytes = _lib.query("mvae_conv2d_wgrad_workspace_bytes", n, c, co, g.kh, g.kw, ho, wo)
     ws = ARENA.get("ws", nbytes, dy.device)
+    mode = (1 if g.upsample else 0) | (MVAE_CONV_XSPLIT if x_split else 0)
     _lib.call("mvae_conv2d_wgrad_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db), float(beta), n, h, wd,
-              c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, 1 if g.upsample else 0, ws.data_ptr(),
-              ws.numel(), st)
+              c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, mode, ws.data_ptr(), ws.numel(), st)
     return db is not None
 
 
@@ -297,11 +302,15 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, geom: ConvGeom):
         _check(x, "conv input")
+        xs = bool(getattr(x, XSPLIT_ATTR, False))
+        if xs and not x.is_contiguous(memory_format=CL):
+            raise RuntimeError("conv2d: a pre-split input must not be re-laid out")
         x = nhwc(x)
         w = _krsc(weight)
         res = nhwc(residual) if residual is not None else None
-        y = conv2d_forward_raw(x, w, bias, res, geom)
+        y = conv2d_forward_raw(x, w, bias, res, geom, xs)
         ctx.geom = geom
+        ctx.x_split = xs
         ctx.has_bias = bias is not None
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, w)
@@ -322,13 +331,14 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             tgt = _main_grad(ctx.weight_ref)
             btgt = _main_grad(ctx.bias_ref) if want_b else None
+            xs = ctx.x_split
             if tgt is not None and (not want_b or btgt is not None):
-                bias_done = conv2d_wgrad_raw(dy, x, tgt, 1.0, g, btgt)
+                bias_done = conv2d_wgrad_raw(dy, x, tgt, 1.0, g, btgt, x_split=xs)
             elif tgt is not None:
-                conv2d_wgrad_raw(dy, x, tgt, 1.0, g)
+                conv2d_wgrad_raw(dy, x, tgt, 1.0, g, x_split=xs)
             else:
                 dw_ret = torch.empty_like(w, memory_format=CL)
-                conv2d_wgrad_raw(dy, x, dw_ret, 0.0, g)
+                conv2d_wgrad_raw(dy, x, dw_ret, 0.0, g, x_split=xs)
         if ctx.has_bias and ctx.needs_input_grad[2] and not bias_done:
             tgt = _main_grad(ctx.bias_ref)
             n, co, ho, wo = dy.shape
@@ -355,7 +365,8 @@ def conv2d(x, weight, bias, geom: ConvGeom, residual=None):
 # ------------------------------------------------------------------------------------------
 class GroupNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool, drop_p: float, seed: int):
+    def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool, drop_p: float, seed: int,
+                y_split: bool = False):
         _check(x, "group_norm input")
         x = nhwc(x)
         n, c, h, w = x.shape
@@ -366,7 +377,7 @@ class GroupNormFn(torch.autograd.Function):
         ws = ARENA.get("gn", nbytes, x.device)
         _lib.call("mvae_group_norm_fwd_nhwc", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
                   mean.data_ptr(), rstd.data_ptr(), n, h * w, c, groups, float(eps), int(silu), float(drop_p),
-                  int(seed) & 0xFFFFFFFFFFFFFFFF, ws.data_ptr(), ws.numel(), _stream(x))
+                  int(seed) & 0xFFFFFFFFFFFFFFFF, int(y_split), ws.data_ptr(), ws.numel(), _stream(x))
         ctx.save_for_backward(x, gamma, beta, mean, rstd)
         ctx.cfg = (groups, int(silu), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF)
         ctx.gamma_ref, ctx.beta_ref = gamma, beta
@@ -395,11 +406,24 @@ class GroupNormFn(torch.autograd.Function):
             _grad_done(ctx.gamma_ref)
         if ctx.needs_input_grad[2] and db_ret is None:
             _grad_done(ctx.beta_ref)
-        return dx, dg_ret, db_ret, None, None, None, None, None
+        return dx, dg_ret, db_ret, None, None, None, None, None, None
 
 
-def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0):
-    return GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed)
+# Activations handed to a convolution in the pre-split 3xBF16 operand layout carry this attribute
+# (the bytes are bf16 hi/lo pairs, not fp32 values): only Conv2dFn consumes them.
+XSPLIT_ATTR = "_mvae_xsplit"
+ACT_SPLIT = os.environ.get("MVAE_NO_ACT_SPLIT") is None
+
+
+def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0, for_conv=False):
+    """for_conv=True: the caller feeds the result straight into ops.conv2d (3x3/stride-1, C % 4 == 0) -- the
+    output is then written pre-split for the GEMM (GroupNorm -> conv is the ResnetBlock / norm_out pattern,
+    encoder_decoder.py:141-163, :318-328)."""
+    split = bool(for_conv and ACT_SPLIT and x.shape[1] % 4 == 0)
+    y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split)
+    if split:
+        setattr(y, XSPLIT_ATTR, True)
+    return y
 
 
 # ------------------------------------------------------------------------------------------

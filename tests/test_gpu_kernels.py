@@ -149,6 +149,34 @@ def test_weight_prep_split_layouts(dev, split):
             assert torch.equal(out, ref), name
 
 
+@pytest.mark.parametrize("drop", [0.0, 0.25])
+def test_groupnorm_split_output_feeds_conv(dev, drop):
+    """GroupNorm(+SiLU, dropout) written pre-split for a following conv (MVAE_CONV_XSPLIT): the bytes are
+    the split of the fp32 output, and the conv (fwd + weight grad) matches the conv of the fp32 output."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    g = torch.Generator().manual_seed(21)
+    n, c, co, h = 2, 64, 32, 12
+    x = cl(torch.randn(n, c, h, h, generator=g) * 2 + 0.5, dev)
+    gam = (torch.rand(c, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(c, generator=g) * 0.1).to(dev)
+    y32 = ops.group_norm(x, gam, bet, 32, 1e-6, True, drop, 77)
+    ys = ops.group_norm(x, gam, bet, 32, 1e-6, True, drop, 77, for_conv=True)
+    assert getattr(ys, ops.XSPLIT_ATTR, False)
+    exp = torch.empty_like(y32)
+    _lib.call("mvae_split_bf16", y32.data_ptr(), exp.data_ptr(), y32.numel(), torch.cuda.current_stream().cuda_stream)
+    assert torch.equal(ys.view(torch.int32), exp.view(torch.int32))
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1)
+    w = cl(torch.randn(co, c, 3, 3, generator=g) / 24.0, dev)
+    wa, wb = w.clone().requires_grad_(), w.clone().requires_grad_()
+    ya = ops.conv2d(y32, wa, None, geom)
+    yb = ops.conv2d(ys, wb, None, geom)
+    assert rel(yb, ya) < 1e-5
+    gy = torch.randn(ya.shape, generator=g).to(dev).contiguous(memory_format=torch.channels_last)
+    ya.backward(gy)
+    yb.backward(gy)
+    assert rel(wb.grad, wa.grad) < 1e-5
+
+
 def test_upsample_gather_mode_matches_subpixel(dev):
     """The direct gather form of Upsample's conv (mvae_conv2d_nhwc mode 1: 9 taps on the upsampled grid)
     and the sub-pixel form (4 parity classes of 2x2 convs) give the same result."""
