@@ -48,6 +48,23 @@ enum { B_ROWK = 0, B_COLN = 1, B_WGRAD_FWD = 2, B_WGRAD_UPS = 3, B_WGRAD_SUBPIX 
 enum { MODE_FWD = 0, MODE_UPS = 1, MODE_DGRAD = 2, MODE_SUBPIX = 3 };
 
 constexpr int BK = 32;
+// MFMA shape per kernel (template MF): v_mfma_f32_16x16x32_bf16 (MF 16) or v_mfma_f32_32x32x16_bf16
+// (MF 32). Both take the same cycles per FLOP, but on random data the chip holds a higher clock under
+// the 16x16x32 loop: +8-11 % bf16 FLOP/s in this kernel's per-wave structure (tools/micro/mfma_shape.hip),
+// +3-5 % on the conv fwd/dgrad GEMMs. The wgrad / attention GEMMs, whose A operand is a transposed
+// (COL) image, measured 5-7 % faster with 32x32x16 and keep it (mf_of).
+template <int MF> using acc_of = typename std::conditional<MF == 32, f32x16, f32x4>::type;
+template <int MF> constexpr int ks_of() { return BK / (MF == 32 ? 16 : 32); }  // MFMA k-steps per K-tile
+template <int MF> constexpr int nr_of() { return MF == 32 ? 16 : 4; }          // accumulator registers per tile
+// LDS swizzles, conflict-free for the fragment reads of both MFMA shapes:
+//  ROW image: 16-B k-chunk c of row r sits at chunk position c ^ row_swz(r) (the 16x16x32 ds_read_b128
+//             lane groups then hit 16 distinct 4-bank windows; 80-B pitch alone leaves them 2-way)
+//  COL image: column col of k-row kr sits at col ^ col_swz(kr) (the two 16-lane halves of a 16x16x32
+//             ds_read_b64_tr_b16, k-rows 8 apart, land in disjoint bank windows)
+__device__ __forceinline__ int row_swz(int r) { return ((r >> 2) ^ (r >> 3) ^ (r >> 4)) & 1; }
+__device__ __forceinline__ int col_swz(int kr) { return ((kr >> 3) & 1) << 4; }
+// element offset of the 4-element group kc (0..7) of ROW-image row r
+__device__ __forceinline__ int row_off(int r, int kc) { return r * 40 + (((kc >> 1) ^ row_swz(r)) << 3) + ((kc & 1) << 2); }
 constexpr int MVAE_CONV_WSPLIT = 16;  // conv mode flag: weights hold split4_bf16 groups
 constexpr int MVAE_CONV_XSPLIT = 32;  // conv mode flag: the input activation x holds split4_bf16 groups
 
@@ -169,15 +186,30 @@ __device__ __forceinline__ void st_presplit(__bf16* img, int plane, int off, con
   if constexpr (PREC == 3) *(u32x2_t*)(img + plane + off) = u32x2_t{__float_as_uint(v.z), __float_as_uint(v.w)};
 }
 
-// fragment of a 32x32x16 MFMA operand: lane l holds element [row0 + (l&31)][ks*16 + 8*(l>>5) + j]
-template <int ROWS, bool COL>
+// MFMA operand fragment, k-step ks of the K-tile.
+//  32x32x16: lane l holds element [row0 + (l&31)][ks*16 + 8*(l>>5) + j]
+//  16x16x32: lane l holds element [row0 + (l&15)][8*(l>>4) + j]
+template <int ROWS, bool COL, int MF>
 __device__ __forceinline__ bf16x8 read_frag(const __bf16* plane, int row0, int ks, int lane) {
   if constexpr (!COL) {
-    return *(const bf16x8*)(plane + (row0 + (lane & 31)) * 40 + ks * 16 + (lane >> 5) * 8);
+    if constexpr (MF == 32) {
+      const int r = row0 + (lane & 31);
+      return *(const bf16x8*)(plane + r * 40 + (((2 * ks + (lane >> 5)) ^ row_swz(r)) << 3));
+    } else {
+      const int r = row0 + (lane & 15);
+      return *(const bf16x8*)(plane + r * 40 + (((lane >> 4) ^ row_swz(r)) << 3));
+    }
   } else {
     constexpr int P = Img<ROWS, true>::PITCH;
     const int g = lane >> 4, li = lane & 15;
-    const __bf16* p = plane + (ks * 16 + (g >> 1) * 8 + (li >> 2)) * P + row0 + (g & 1) * 16 + 4 * (li & 3);
+    const __bf16* p;
+    if constexpr (MF == 32) {
+      const int kr = ks * 16 + (g >> 1) * 8 + (li >> 2);
+      p = plane + kr * P + ((row0 + (g & 1) * 16 + 4 * (li & 3)) ^ col_swz(kr));
+    } else {
+      const int kr = g * 8 + (li >> 2);
+      p = plane + kr * P + ((row0 + 4 * (li & 3)) ^ col_swz(kr));
+    }
     const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)p);
     const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(p + 4 * P));
     return __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -264,9 +296,9 @@ struct LoadRowK {
   }
   __device__ void store_slot(__bf16* img, int i) {
     if constexpr (PRESPLIT)
-      st_presplit<PREC>(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+      st_presplit<PREC>(img, Img<ROWS, false>::PLANE, row_off(r0 + RP * i, kc), v[i]);
     else
-      st_split<PREC>(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+      st_split<PREC>(img, Img<ROWS, false>::PLANE, row_off(r0 + RP * i, kc), v[i]);
   }
   __device__ void advance() { k += BK; }
   __device__ void load(const GemmArgs& a) {
@@ -349,9 +381,9 @@ struct LoadConvA {
   }
   __device__ void store_slot(__bf16* img, int i) {
     if constexpr (PRESPLIT)
-      st_presplit<PREC>(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+      st_presplit<PREC>(img, Img<ROWS, false>::PLANE, row_off(r0 + RP * i, kc), v[i]);
     else
-      st_split<PREC>(img, Img<ROWS, false>::PLANE, (r0 + RP * i) * 40 + kc * 4, v[i]);
+      st_split<PREC>(img, Img<ROWS, false>::PLANE, row_off(r0 + RP * i, kc), v[i]);
   }
   __device__ void advance() { k += BK; }
   __device__ void load(const GemmArgs& a) {
@@ -401,7 +433,7 @@ struct LoadColK {
     constexpr int P_ = Img<ROWS, true>::PITCH;
     const int krow = kr + i * (NT / C4);
     if (krow < BK) {
-      st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+      st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
       if constexpr (IS_A) {
         bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
       }
@@ -460,7 +492,7 @@ struct LoadColPix {
     constexpr int P_ = Img<ROWS, true>::PITCH;
     const int krow = kr + i * (NT / C4);
     if (krow < BK) {
-      st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+      st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
       bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
     }
   }
@@ -546,9 +578,9 @@ struct LoadWgradX {
     const int krow = kr + i * (NT / C4);
     if (krow < BK) {
       if constexpr (PRESPLIT)
-        st_presplit<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+        st_presplit<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
       else
-        st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + c4 * 4, v[i]);
+        st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
     }
   }
   __device__ void advance() { k += BK; }
@@ -563,16 +595,30 @@ struct LoadWgradX {
   }
 };
 
-// one 32x32x16 product step: 3xBF16 (lo*hi + hi*lo + hi*hi, small terms first) or plain bf16
-template <int PREC>
-__device__ __forceinline__ void mma(f32x16& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
+// one MFMA product step: 3xBF16 (lo*hi + hi*lo + hi*hi, small terms first) or plain bf16
+__device__ __forceinline__ f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <int PREC, typename ACC>
+__device__ __forceinline__ void mma(ACC& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
                                     const bf16x8& bl) {
   if constexpr (PREC == 3) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+    acc = mfma_bf16(al, bh, acc);
+    acc = mfma_bf16(ah, bl, acc);
   }
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+  acc = mfma_bf16(ah, bh, acc);
 }
+// row of accumulator register r (lane's column: lane & (MF-1)) within an MF x MF tile
+template <int MF>
+__device__ __forceinline__ int acc_row(int r, int lane) {
+  if constexpr (MF == 32) return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+  else return 4 * (lane >> 4) + r;
+}
+// MFMA shape of a kernel: 32x32x16 when A is a transposed (COL) image (wgrad, attention backward)
+constexpr int mf_of(int ak) { return (ak == A_COLM || ak == A_COLM_PIX) ? 32 : 16; }
 
 template <int KIND, int ROWS, int VEC, int NT, bool IS_A, int PREC>
 struct Loader;
@@ -606,12 +652,14 @@ struct Loader<6, ROWS, VEC, NT, false, PREC> : LoadWgradX<ROWS, VEC, NT, MODE_FW
 template <int BM, int BN, int WGM, int WGN, int AK, int VA, int BKIND, int VB, int PREC>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   constexpr int NT = 64 * WGM * WGN;
+  constexpr int MF = mf_of(AK), KS = ks_of<MF>(), NR = nr_of<MF>();
+  using acc_t = acc_of<MF>;
   using LA = Loader<AK, BM, VA, NT, true, PREC>;
   using LB = Loader<BKIND, BN, VB, NT, false, PREC>;
   using IA = Img<BM, LA::COL>;
   using IB = Img<BN, LB::COL>;
   constexpr int BUF = IA::SIZE + IB::SIZE;
-  constexpr int TM = BM / WGM / 32, TN = BN / WGN / 32;  // 32x32 MFMA tiles per wave
+  constexpr int TM = BM / WGM / MF, TN = BN / WGN / MF;  // MFMA tiles per wave
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -641,13 +689,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   la.init(a, a.A + bidx * a.sA, m0, kb, tid, bidx);
   lb.init(a, a.B + bidx * a.sB, n0, kb, tid, bidx);
 
-  f32x16 acc[TM][TN];
+  acc_t acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
 
   const int nt = ke > kb ? (ke - kb + BK - 1) / BK : 0;
   // Prologue: tile 0 -> LDS buffer 0, tile 1 -> registers.
@@ -673,18 +721,18 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   auto compute = [&](const __bf16* Ai) {
     const __bf16* Bi = Ai + IA::SIZE;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       bf16x8 bh[TN], bl[TN];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        bh[j] = read_frag<BN, LB::COL>(Bi, brow + j * 32, ks, lane);
-        if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, ks, lane);
+        bh[j] = read_frag<BN, LB::COL, MF>(Bi, brow + j * MF, ks, lane);
+        if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL, MF>(Bi + IB::PLANE, brow + j * MF, ks, lane);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const bf16x8 ah = read_frag<BM, LA::COL>(Ai, arow + i * 32, ks, lane);
+        const bf16x8 ah = read_frag<BM, LA::COL, MF>(Ai, arow + i * MF, ks, lane);
         bf16x8 al{};
-        if constexpr (PREC == 3) al = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow + i * 32, ks, lane);
+        if constexpr (PREC == 3) al = read_frag<BM, LA::COL, MF>(Ai + IA::PLANE, arow + i * MF, ks, lane);
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           mma<PREC>(acc[i][j], ah, al, bh[j], bl[j]);
@@ -694,12 +742,12 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   };
   int t = 0;
 #ifndef MVAE_BLOCK_STAGING
-  // steady state, software-pipelined by hand: the K-tile's 2*TM MFMA steps (one 32-row A fragment
+  // steady state, software-pipelined by hand: the K-tile's KS*TM MFMA steps (one MF-row A fragment
   // x TN B fragments x 3 split products each) each carry a share of the staging work -- split +
   // LDS write of one slot of tile t+1, then the global load of the same slot of tile t+2 -- and
   // prefetch the next step's A fragment. sched_barrier pins that order (the scheduler would
   // otherwise hoist all staging VALU into one block ahead of the MFMAs, idling the MFMA pipe).
-  constexpr int STEPS = 2 * TM;
+  constexpr int STEPS = KS * TM;
   constexpr int NSL = LA::NS + LB::NS;
   // STAG: the wave runs each step's staging share BEFORE its MFMAs instead of after. Given to the
   // second half of the workgroup (waves 4-7 share SIMDs with waves 0-3), it staggers the two waves of
@@ -717,11 +765,11 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
       bf16x8 bh[TN], bl[TN], ah[2], al[2];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        bh[j] = read_frag<BN, LB::COL>(Bi, brow + j * 32, 0, lane);
-        if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, 0, lane);
+        bh[j] = read_frag<BN, LB::COL, MF>(Bi, brow + j * MF, 0, lane);
+        if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL, MF>(Bi + IB::PLANE, brow + j * MF, 0, lane);
       }
-      ah[0] = read_frag<BM, LA::COL>(Ai, arow, 0, lane);
-      if constexpr (PREC == 3) al[0] = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow, 0, lane);
+      ah[0] = read_frag<BM, LA::COL, MF>(Ai, arow, 0, lane);
+      if constexpr (PREC == 3) al[0] = read_frag<BM, LA::COL, MF>(Ai + IA::PLANE, arow, 0, lane);
       auto stage = [&](int st) {
 #pragma unroll
         for (int q = st * NSL / STEPS; q < (st + 1) * NSL / STEPS; ++q) {
@@ -743,18 +791,18 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
         }
         if (st + 1 < STEPS) {
           const int ks1 = (st + 1) / TM, i1 = (st + 1) % TM;
-          ah[cur ^ 1] = read_frag<BM, LA::COL>(Ai, arow + i1 * 32, ks1, lane);
-          if constexpr (PREC == 3) al[cur ^ 1] = read_frag<BM, LA::COL>(Ai + IA::PLANE, arow + i1 * 32, ks1, lane);
+          ah[cur ^ 1] = read_frag<BM, LA::COL, MF>(Ai, arow + i1 * MF, ks1, lane);
+          if constexpr (PREC == 3) al[cur ^ 1] = read_frag<BM, LA::COL, MF>(Ai + IA::PLANE, arow + i1 * MF, ks1, lane);
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           mma<PREC>(acc[i][j], ah[cur], al[cur], bh[j], bl[j]);
         }
-        if (st == TM - 1) {  // B fragments of the second k-half
+        if (KS == 2 && st == TM - 1) {  // B fragments of the second k-half
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
-            bh[j] = read_frag<BN, LB::COL>(Bi, brow + j * 32, 1, lane);
-            if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL>(Bi + IB::PLANE, brow + j * 32, 1, lane);
+            bh[j] = read_frag<BN, LB::COL, MF>(Bi, brow + j * MF, 1, lane);
+            if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL, MF>(Bi + IB::PLANE, brow + j * MF, 1, lane);
           }
         }
         if constexpr (!STAG) stage(st);
@@ -809,19 +857,19 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
     }
   }
 
-  // epilogue: C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  // epilogue: C/D layout of the MFMA tile: col = lane & (MF-1), row = acc_row<MF>(r, lane).
   // Stores go through buffer descriptors: rows/cols outside the matrix are dropped by the hardware.
   if (a.splits > 1) {
     const __amdgpu_buffer_rsrc_t ws =
         make_rsrc(a.ws + ((long long)bidx * a.splits + split) * a.M * a.N, (unsigned)(a.M * a.N * 4u));
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int col = n0 + brow + j * 32 + (lane & 31);
+      const int col = n0 + brow + j * MF + (lane & (MF - 1));
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = m0 + arow + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        for (int r = 0; r < NR; ++r) {
+          const int row = m0 + arow + i * MF + acc_row<MF>(r, lane);
           const bool ok = row < a.M && col < a.N;
           bstore1(ws, ok ? ((unsigned)row * a.N + col) * 4u : OOB, acc[i][j][r]);
         }
@@ -836,13 +884,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   const int par_off = sub_par_off(a, bidx);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int col = n0 + brow + j * 32 + (lane & 31);
+    const int col = n0 + brow + j * MF + (lane & (MF - 1));
     const float bv = bload1(br, col < a.N ? (unsigned)col * 4u : OOB);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + arow + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      for (int r = 0; r < NR; ++r) {
+        const int row = m0 + arow + i * MF + acc_row<MF>(r, lane);
         const bool ok = row < a.M && col < a.N;
         const int orow = remap ? sub_pixel(a, ok ? row : 0, par_off) : row;
         float v = a.alpha * acc[i][j][r] + bv;
