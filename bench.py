@@ -61,6 +61,7 @@ CONFIGS = {
 
 BF16_DENSE_PEAK_TF = 2500.0
 PEAK_3XBF16_TF = BF16_DENSE_PEAK_TF / 3.0
+HBM_PEAK_GBS = 8000.0
 
 
 def _pmc_traffic(config):
@@ -179,8 +180,10 @@ def main():
         mod.fit_step(batches[0], 0)
         torch.cuda.synchronize()
         step_ms = (time.perf_counter() - t1) * 1e3
-        rec = ops.PROFILE
+        rec_all = ops.PROFILE
         ops.PROFILE = None
+        rec = [r for r in rec_all if r[0] not in ops.HBM_TAGS]
+        hbm_rec = [r for r in rec_all if r[0] in ops.HBM_TAGS]
         tot_ms = sum(r[2].elapsed_time(r[3]) for r in rec)
         tot_fl = sum(r[1] for r in rec)
         tot_ref = sum(r[5] for r in rec)
@@ -217,6 +220,22 @@ def main():
                     "gemm_share_of_step": round(tot_ms / step_ms, 3),
                     "by_pass": {k: {"launches": v[0], "ms": round(v[2], 2),
                                     "TFLOP/s": round(v[1] / (v[2] * 1e-3) / 1e12, 1)} for k, v in by.items()}}
+        if hbm_rec:  # the memory-bound GroupNorm(+SiLU) family against the HBM roofline
+            hb = {}
+            for tag, nbytes, s, e, _, _ in hbm_rec:
+                d = hb.setdefault(tag, [0, 0.0, 0.0])
+                d[0] += 1
+                d[1] += nbytes
+                d[2] += s.elapsed_time(e)
+            hms = sum(v[2] for v in hb.values())
+            hby = sum(v[1] for v in hb.values())
+            roofline["hbm_kernels"] = {
+                "bound": "hbm", "kernel": "GroupNorm(+SiLU) fwd / bwd (gn_* kernel chains, all launches)",
+                "achieved": round(hby / (hms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(hby / (hms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms_per_step": round(hms, 2),
+                "bytes_note": "algorithmic bytes: fwd 8 B/elem (read x, write y), bwd 12 B/elem (read x, dy; write dx)",
+                "by_pass": {k: {"launches": v[0], "ms": round(v[2], 2),
+                                "GB/s": round(v[1] / (v[2] * 1e-3) / 1e9, 1)} for k, v in hb.items()}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg["loss"]["type"] == "vae":

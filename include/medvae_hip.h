@@ -119,7 +119,9 @@ int mvae_softmax_rows_bwd(const float* y, const float* dy, float* dx, long long 
 /* ---- GroupNorm (+SiLU, +inverted dropout) -------------------------------------------------------
  * Normalize() = nn.GroupNorm(min(32,C), C, eps=1e-6) (encoder_decoder.py:28-33) fused with
  * nonlinearity() (:13-15) and ResnetBlock's nn.Dropout (:163). mean/rstd: [nb*groups].
- * Backward ACCUMULATES into dgamma/dbeta (flat grad buffer).
+ * Backward ACCUMULATES into dgamma/dbeta (flat grad buffer); dx_add (nullable, [nb][hw][c]) is the
+ * gradient of x from the block's other branch (ResnetBlock / AttnBlock residual, encoder_decoder.py:
+ * 107,170), summed into dx in the same pass (replaces autograd's separate gradient add).
  * y_split = 1: y is written in the pre-split 3xBF16 operand layout (mvae_split_bf16) for a following
  * convolution (MVAE_CONV_XSPLIT); the backward never reads y. */
 int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* beta, float* y, float* mean,
@@ -127,7 +129,8 @@ int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* be
                              float drop_p, unsigned long long seed, int y_split, void* workspace,
                              size_t workspace_bytes, void* stream);
 int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
-                             const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta,
+                             const float* mean, const float* rstd, float* dx, const float* dx_add,
+                             float* dgamma, float* dbeta,
                              int nb, int hw, int c, int groups, int silu, float drop_p,
                              unsigned long long seed, void* workspace, size_t workspace_bytes,
                              void* stream);

@@ -43,7 +43,7 @@ SIGNATURES = {
     "mvae_softmax_rows": (I, [P, P, L, I, P]),
     "mvae_softmax_rows_bwd": (I, [P, P, P, L, I, P]),
     "mvae_group_norm_fwd_nhwc": (I, [P, P, P, P, P, P, I, I, I, I, F, I, F, c_uint64, I, P, Z, P]),
-    "mvae_group_norm_bwd_nhwc": (I, [P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, c_uint64, P, Z, P]),
+    "mvae_group_norm_bwd_nhwc": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, c_uint64, P, Z, P]),
     "mvae_group_norm_workspace_bytes": (Z, [I, I, I]),
     "mvae_reparam_fwd": (I, [P, P, L, P, P, L, I, P]),
     "mvae_reparam_bwd": (I, [P, P, P, L, P, L, I, P]),

@@ -8,6 +8,7 @@
 // results are bitwise reproducible run to run.
 #include "common.h"
 #include <algorithm>
+#include <stdlib.h>
 
 namespace mvae {
 
@@ -37,6 +38,7 @@ struct GnArgs {
   unsigned long long seed;
   double* ws;  // [nb][chunks][C][2]
   int y_split;  // forward apply: write y as split4_bf16 groups (the 3xBF16 GEMM operand format)
+  const float* dx_add;  // backward: optional gradient of the same tensor from another branch, summed into dx
 };
 
 // Thread mapping shared by the NHWC GroupNorm kernels: a block owns (sample b, chunk of rows); a
@@ -259,15 +261,19 @@ __global__ void __launch_bounds__(256) gn_bwd_finalize_kernel(GnArgs a, float* k
   }
 }
 
-// dgamma[c] += sum_{b,chunks} s1 ; dbeta[c] += sum s0   (64 channels x 4 partial lanes per block)
-__global__ void __launch_bounds__(256) gn_param_grad_kernel(GnArgs a, float* dgamma, float* dbeta) {
+// dgamma[c] += sum_{b,chunks} s1 ; dbeta[c] += sum s0. Two fixed-order stages so the reduction over the
+// nb*chunks partial rows runs on many blocks: stage 1, block (channel tile, slice) sums its slice of rows
+// (64 channels x 4 row lanes per block) into part[slice][C][2]; stage 2 sums the slices per channel.
+constexpr int GN_PG_SLICES = 64;
+__global__ void __launch_bounds__(256) gn_param_grad_kernel(GnArgs a, double* __restrict__ part) {
   __shared__ double sh[2][256];
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  const int c = blockIdx.x * 64 + cl, sl = blockIdx.y;
+  const int n = a.nb * a.chunks;
+  const int lo = (int)((long long)n * sl / GN_PG_SLICES), hi = (int)((long long)n * (sl + 1) / GN_PG_SLICES);
   double s0 = 0, s1 = 0;
   if (c < a.C) {
-    const int n = a.nb * a.chunks;
-    for (int i = rg; i < n; i += 4) {
+    for (int i = lo + rg; i < hi; i += 4) {
       const double* w = a.ws + ((long long)i * a.C + c) * 2;
       s0 += w[0];
       s1 += w[1];
@@ -277,11 +283,23 @@ __global__ void __launch_bounds__(256) gn_param_grad_kernel(GnArgs a, float* dga
   sh[1][threadIdx.x] = s1;
   __syncthreads();
   if (rg == 0 && c < a.C) {
-    s0 = sh[0][cl] + sh[0][cl + 64] + sh[0][cl + 128] + sh[0][cl + 192];
-    s1 = sh[1][cl] + sh[1][cl + 64] + sh[1][cl + 128] + sh[1][cl + 192];
-    if (dgamma) dgamma[c] += (float)s1;
-    if (dbeta) dbeta[c] += (float)s0;
+    double* o = part + ((long long)sl * a.C + c) * 2;
+    o[0] = sh[0][cl] + sh[0][cl + 64] + sh[0][cl + 128] + sh[0][cl + 192];
+    o[1] = sh[1][cl] + sh[1][cl + 64] + sh[1][cl + 128] + sh[1][cl + 192];
   }
+}
+
+__global__ void __launch_bounds__(256) gn_param_final_kernel(int C, const double* __restrict__ part,
+                                                              float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0, s1 = 0;
+  for (int sl = 0; sl < GN_PG_SLICES; ++sl) {
+    s0 += part[((long long)sl * C + c) * 2];
+    s1 += part[((long long)sl * C + c) * 2 + 1];
+  }
+  if (dgamma) dgamma[c] += (float)s1;
+  if (dbeta) dbeta[c] += (float)s0;
 }
 
 __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __restrict__ k1,
@@ -339,6 +357,10 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
             }
             o[e] = d * q1[e] + xs[e] * q2[e] + q3[e];
           }
+          if (a.dx_add) {  // the other branch's gradient of x (ResnetBlock / AttnBlock residual): summed here
+            const float4 ad = *(const float4*)(a.dx_add + off);
+            o[0] += ad.x; o[1] += ad.y; o[2] += ad.z; o[3] += ad.w;
+          }
           *(float4*)(op + (long long)r * a.C) = float4{o[0], o[1], o[2], o[3]};
         }
       }
@@ -347,9 +369,16 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
   }
 }
 
+static int gn_target_blocks() {
+  static int v = [] {
+    const char* e = getenv("MVAE_GN_BLOCKS");  // experiment knob: target grid size of the streaming kernels
+    return e ? std::max(64, atoi(e)) : 1024;
+  }();
+  return v;
+}
 static int gn_chunks(int nb, int hw) {
   int chunks = 1;
-  while ((long long)nb * chunks < 1024 && hw / (chunks * 2) >= 16) chunks *= 2;
+  while ((long long)nb * chunks < gn_target_blocks() && hw / (chunks * 2) >= 16) chunks *= 2;
   return chunks;
 }
 
@@ -362,7 +391,9 @@ extern "C" {
 size_t mvae_group_norm_workspace_bytes(int nb, int hw, int c) {
   const int ch = gn_chunks(nb, hw);
   // fp64 partials + 3 float arrays of nb*C (scale/shift or k1) + 2 of nb*C (k2/k3 upper bound)
-  return (size_t)nb * ch * c * 2 * sizeof(double) + (size_t)nb * c * 5 * sizeof(float) + 256;
+  // + the parameter-gradient slice partials [GN_PG_SLICES][C][2] fp64
+  return (size_t)nb * ch * c * 2 * sizeof(double) + (size_t)nb * c * 5 * sizeof(float) + 256 +
+         (size_t)GN_PG_SLICES * c * 2 * sizeof(double) + 256;
 }
 
 // y = [dropout](silu?(GroupNorm(x)))  ; saves mean/rstd [nb*groups]
@@ -394,9 +425,10 @@ int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* be
   return launch_status();
 }
 
-// dx = d/dx of the fused forward; dgamma/dbeta are ACCUMULATED (+=) when non-null.
+// dx = d/dx of the fused forward [+ dx_add when non-null]; dgamma/dbeta are ACCUMULATED (+=) when non-null.
 int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
-                             const float* mean, const float* rstd, float* dx, float* dgamma, float* dbeta,
+                             const float* mean, const float* rstd, float* dx, const float* dx_add,
+                             float* dgamma, float* dbeta,
                              int nb, int hw, int c, int groups, int silu, float drop_p,
                              unsigned long long seed, void* workspace, size_t workspace_bytes, void* stream) {
   if (nb <= 0 || hw <= 0 || c <= 0 || (c & 3) || groups <= 0 || c % groups) {
@@ -409,7 +441,7 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
   }
   hipStream_t st = (hipStream_t)stream;
   GnArgs a{};
-  a.x = x; a.dy = dy; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta;
+  a.x = x; a.dy = dy; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta; a.dx_add = dx_add;
   a.nb = nb; a.hw = hw; a.C = c; a.G = groups; a.silu = silu; a.drop_p = drop_p; a.seed = seed;
   a.chunks = gn_chunks(nb, hw);
   a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
@@ -420,8 +452,12 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
   hipLaunchKernelGGL(gn_partial_kernel<1>, dim3(a.chunks, nb), dim3(256), 0, st, a);
   hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(cdiv((long long)nb * groups, 4)), dim3(256), 0, st, a, k1,
                      k2, k3);
-  if (dgamma || dbeta)
-    hipLaunchKernelGGL(gn_param_grad_kernel, dim3(cdiv(c, 64)), dim3(256), 0, st, a, dgamma, dbeta);
+  if (dgamma || dbeta) {
+    double* part = (double*)(((uintptr_t)(k3 + (size_t)nb * c) + 255) & ~(uintptr_t)255);
+    hipLaunchKernelGGL(gn_param_grad_kernel, dim3(cdiv(c, 64), GN_PG_SLICES), dim3(256), 0, st, a, part);
+    hipLaunchKernelGGL(gn_param_final_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st, c, (const double*)part, dgamma,
+                       dbeta);
+  }
   hipLaunchKernelGGL(gn_dx_kernel, dim3(a.chunks, nb), dim3(256), 0, st, a, k1, k2, k3, dx);
   return launch_status();
 }

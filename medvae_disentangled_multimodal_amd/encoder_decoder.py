@@ -61,8 +61,8 @@ class Conv2d(nn.Module):
             bound = 1 / math.sqrt(fan_in) if fan_in > 0 else 0
             nn.init.uniform_(self.bias, -bound, bound)
 
-    def forward(self, x, residual=None, geom: Optional[ConvGeom] = None):
-        return ops.conv2d(x, self.weight, self.bias, geom or self.geom, residual)
+    def forward(self, x, residual=None, geom: Optional[ConvGeom] = None, res_sink=None, x_sink=None):
+        return ops.conv2d(x, self.weight, self.bias, geom or self.geom, residual, res_sink, x_sink)
 
 
 class GroupNorm(nn.Module):
@@ -74,9 +74,10 @@ class GroupNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(num_channels))
         self.bias = nn.Parameter(torch.zeros(num_channels))
 
-    def forward(self, x, silu: bool = False, drop_p: float = 0.0, for_conv: bool = False):
+    def forward(self, x, silu: bool = False, drop_p: float = 0.0, for_conv: bool = False, grad_sink=None):
         seed = _next_seed() if drop_p > 0.0 else 0
-        return ops.group_norm(x, self.weight, self.bias, self.num_groups, self.eps, silu, drop_p, seed, for_conv)
+        return ops.group_norm(x, self.weight, self.bias, self.num_groups, self.eps, silu, drop_p, seed, for_conv,
+                              grad_sink)
 
 
 def Normalize(in_channels: int, num_groups: int = 32) -> GroupNorm:
@@ -107,12 +108,15 @@ class ResnetBlock(nn.Module):
     def forward(self, x, temb=None):
         if temb is not None:
             raise NotImplementedError("timestep embeddings are not used by the VAE (temb_channels=0)")
-        h = self.conv1(self.norm1(x, silu=True, for_conv=True))
+        # x's two gradient branches (norm1 and the residual / shortcut) are summed inside norm1's backward
+        sink = ops.GradSink() if torch.is_grad_enabled() and x.requires_grad else None
+        h = self.conv1(self.norm1(x, silu=True, for_conv=True, grad_sink=sink))
         p = self.dropout.p if self.training else 0.0
         h = self.norm2(h, silu=True, drop_p=p, for_conv=True)
         if self.in_channels != self.out_channels:
-            x = self.conv_shortcut(x) if self.use_conv_shortcut else self.nin_shortcut(x)
-        return self.conv2(h, residual=x)
+            sc = self.conv_shortcut if self.use_conv_shortcut else self.nin_shortcut
+            return self.conv2(h, residual=sc(x, x_sink=sink))
+        return self.conv2(h, residual=x, res_sink=sink)
 
 
 class AttnBlock(nn.Module):
@@ -126,9 +130,10 @@ class AttnBlock(nn.Module):
         self.proj_out = Conv2d(in_channels, in_channels, 1)
 
     def forward(self, x):
-        h = self.norm(x)
+        sink = ops.GradSink() if torch.is_grad_enabled() and x.requires_grad else None
+        h = self.norm(x, grad_sink=sink)
         o = ops.attention_core(self.q(h), self.k(h), self.v(h))
-        return self.proj_out(o, residual=x)
+        return self.proj_out(o, residual=x, res_sink=sink)
 
 
 def make_attn(in_channels: int, attn_type: str = "vanilla") -> nn.Module:

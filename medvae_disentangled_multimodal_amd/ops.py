@@ -65,8 +65,10 @@ ARENA = _Arena()
 
 # Optional live kernel timing (bench.py): when PROFILE is a list, every implicit-GEMM launch is
 # bracketed by HIP events on the current stream and recorded as
-# (tag, algorithmic_flops, start, end, shape) -- shape = the launch's problem tuple.
+# (tag, algorithmic_flops, start, end, shape) -- shape = the launch's problem tuple. The HBM-bound
+# GroupNorm launches are recorded the same way under HBM_TAGS with algorithmic BYTES in the work slot.
 PROFILE = None
+HBM_TAGS = ("gn_fwd", "gn_bwd")
 
 
 class _timed:
@@ -298,9 +300,37 @@ def bias_grad_raw(dy2d_ptr, rows, n, out, beta, device, stream):
     _lib.call("mvae_bias_grad", dy2d_ptr, rows, n, n, out.data_ptr(), float(beta), ws.data_ptr(), ws.numel(), stream)
 
 
+class GradSink:
+    """Side channel for the two gradient branches of a block input x (ResnetBlock: norm1(x) and the
+    residual / nin_shortcut(x), encoder_decoder.py:141-170; AttnBlock: norm(x) and the residual, :83-107).
+    The residual-side op's backward (the producer: Conv2dFn's residual passthrough or the nin_shortcut
+    dgrad) parks its gradient here instead of returning it, and the GroupNorm backward of norm1 (the
+    consumer) sums it into dx inside gn_dx -- no separate autograd add over the activation. If the
+    consumer runs first (engine order), it marks the sink closed and the producer returns its gradient
+    normally, so the result is correct in either order."""
+    __slots__ = ("g", "closed")
+
+    def __init__(self):
+        self.g = None
+        self.closed = False
+
+    def park(self, g) -> bool:
+        # one producer per sink and backward pass: a gradient still parked here is left over from a pass
+        # that never reached the consumer (a partial torch.autograd.grad) and is replaced
+        if self.closed:
+            return False
+        self.g = g
+        return True
+
+    def take(self):
+        g, self.g = self.g, None
+        self.closed = g is None
+        return g
+
+
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, geom: ConvGeom):
+    def forward(ctx, x, weight, bias, residual, geom: ConvGeom, res_sink=None, x_sink=None):
         _check(x, "conv input")
         xs = bool(getattr(x, XSPLIT_ATTR, False))
         if xs and not x.is_contiguous(memory_format=CL):
@@ -316,6 +346,7 @@ class Conv2dFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.weight_ref = weight
         ctx.bias_ref = bias
+        ctx.res_sink, ctx.x_sink = res_sink, x_sink
         return y
 
     @staticmethod
@@ -326,6 +357,8 @@ class Conv2dFn(torch.autograd.Function):
         dx = dw_ret = db_ret = dres = None
         if ctx.needs_input_grad[0]:
             dx = conv2d_dgrad_raw(dy, w, x.shape, g)
+            if ctx.x_sink is not None and ctx.x_sink.park(dx):
+                dx = None
         bias_done = False
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
@@ -349,15 +382,17 @@ class Conv2dFn(torch.autograd.Function):
                 bias_grad_raw(dy.data_ptr(), n * ho * wo, co, db_ret, 0.0, dy.device, _stream(dy))
         if ctx.has_res and ctx.needs_input_grad[3]:
             dres = dy
+            if ctx.res_sink is not None and ctx.res_sink.park(dy):
+                dres = None
         if ctx.needs_input_grad[1] and dw_ret is None:
             _grad_done(ctx.weight_ref)
         if want_b and db_ret is None:
             _grad_done(ctx.bias_ref)
-        return dx, dw_ret, db_ret, dres, None
+        return dx, dw_ret, db_ret, dres, None, None, None
 
 
-def conv2d(x, weight, bias, geom: ConvGeom, residual=None):
-    return Conv2dFn.apply(x, weight, bias, residual, geom)
+def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink=None):
+    return Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink)
 
 
 # ------------------------------------------------------------------------------------------
@@ -366,7 +401,7 @@ def conv2d(x, weight, bias, geom: ConvGeom, residual=None):
 class GroupNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool, drop_p: float, seed: int,
-                y_split: bool = False):
+                y_split: bool = False, grad_sink=None):
         _check(x, "group_norm input")
         x = nhwc(x)
         n, c, h, w = x.shape
@@ -375,12 +410,14 @@ class GroupNormFn(torch.autograd.Function):
         rstd = torch.empty_like(mean)
         nbytes = _lib.query("mvae_group_norm_workspace_bytes", n, h * w, c)
         ws = ARENA.get("gn", nbytes, x.device)
-        _lib.call("mvae_group_norm_fwd_nhwc", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
-                  mean.data_ptr(), rstd.data_ptr(), n, h * w, c, groups, float(eps), int(silu), float(drop_p),
-                  int(seed) & 0xFFFFFFFFFFFFFFFF, int(y_split), ws.data_ptr(), ws.numel(), _stream(x))
+        with _timed("gn_fwd", 8.0 * x.numel(), (n, c, h * w)):  # algorithmic HBM bytes: read x, write y
+            _lib.call("mvae_group_norm_fwd_nhwc", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
+                      mean.data_ptr(), rstd.data_ptr(), n, h * w, c, groups, float(eps), int(silu), float(drop_p),
+                      int(seed) & 0xFFFFFFFFFFFFFFFF, int(y_split), ws.data_ptr(), ws.numel(), _stream(x))
         ctx.save_for_backward(x, gamma, beta, mean, rstd)
         ctx.cfg = (groups, int(silu), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF)
         ctx.gamma_ref, ctx.beta_ref = gamma, beta
+        ctx.grad_sink = grad_sink
         return y
 
     @staticmethod
@@ -399,14 +436,20 @@ class GroupNormFn(torch.autograd.Function):
             db = db_ret = torch.zeros(c, device=x.device, dtype=torch.float32)
         nbytes = _lib.query("mvae_group_norm_workspace_bytes", n, h * w, c)
         ws = ARENA.get("gn", nbytes, x.device)
-        _lib.call("mvae_group_norm_bwd_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
-                  mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(dg), _ptr(db), n, h * w, c, groups, silu,
-                  drop_p, seed, ws.data_ptr(), ws.numel(), _stream(x))
+        add = ctx.grad_sink.take() if ctx.grad_sink is not None else None
+        if add is not None:
+            add = nhwc(add)
+            if add.shape != x.shape or add.dtype != torch.float32:
+                raise RuntimeError("group_norm backward: parked branch gradient has the wrong shape")
+        with _timed("gn_bwd", 12.0 * x.numel(), (n, c, h * w)):  # algorithmic HBM bytes: read x, dy; write dx
+            _lib.call("mvae_group_norm_bwd_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                      mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(add), _ptr(dg), _ptr(db), n, h * w, c,
+                      groups, silu, drop_p, seed, ws.data_ptr(), ws.numel(), _stream(x))
         if ctx.needs_input_grad[1] and dg_ret is None:
             _grad_done(ctx.gamma_ref)
         if ctx.needs_input_grad[2] and db_ret is None:
             _grad_done(ctx.beta_ref)
-        return dx, dg_ret, db_ret, None, None, None, None, None, None
+        return dx, dg_ret, db_ret, None, None, None, None, None, None, None
 
 
 # Activations handed to a convolution in the pre-split 3xBF16 operand layout carry this attribute
@@ -415,12 +458,12 @@ XSPLIT_ATTR = "_mvae_xsplit"
 ACT_SPLIT = os.environ.get("MVAE_NO_ACT_SPLIT") is None
 
 
-def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0, for_conv=False):
+def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0, for_conv=False, grad_sink=None):
     """for_conv=True: the caller feeds the result straight into ops.conv2d (3x3/stride-1, C % 4 == 0) -- the
     output is then written pre-split for the GEMM (GroupNorm -> conv is the ResnetBlock / norm_out pattern,
     encoder_decoder.py:141-163, :318-328)."""
     split = bool(for_conv and ACT_SPLIT and x.shape[1] % 4 == 0)
-    y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split)
+    y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink)
     if split:
         setattr(y, XSPLIT_ATTR, True)
     return y
@@ -811,7 +854,7 @@ class BatchNormFn(torch.autograd.Function):
             _grad_done(ctx.gamma_ref)
         if ctx.needs_input_grad[2] and db_ret is None:
             _grad_done(ctx.beta_ref)
-        return dx, dg_ret, db_ret, None, None, None, None, None, None
+        return dx, dg_ret, db_ret, None, None, None, None, None, None, None
 
 
 def batch_norm(x, gamma, beta, run_mean, run_var, training, momentum=0.1, eps=1e-5, slope=-1.0):

@@ -340,3 +340,37 @@ def test_multi_tensor_adam_matches_torch(dev):
             opt.step()
         for p, r in zip(flat.params, ref):
             assert rel(p, r) < 1e-6
+
+
+@pytest.mark.parametrize("cin,cout,attn", [(64, 64, False), (64, 128, False), (64, 64, True)])
+def test_block_input_gradient_branches_summed_in_groupnorm(dev, cin, cout, attn):
+    """ResnetBlock (identity residual and nin_shortcut) and AttnBlock: the residual-side gradient of the
+    block input is parked in a GradSink and summed inside norm1's GroupNorm backward; the input gradient
+    must equal the float64 torch functional reference (encoder_decoder.py:68-170)."""
+    from medvae_disentangled_multimodal_amd import encoder_decoder as E
+    torch.manual_seed(3)
+    blk = (E.AttnBlock(cin) if attn else E.ResnetBlock(in_channels=cin, out_channels=cout)).to(dev)
+    x = torch.randn(2, cin, 8, 8)
+    xd = cl(x, dev).requires_grad_(True)
+    y = blk(xd)
+    gy = torch.randn(y.shape)
+    y.backward(cl(gy, dev))
+    P = {k: v.detach().double().cpu() for k, v in blk.state_dict().items()}
+    xr = x.double().requires_grad_(True)
+    if attn:
+        h = F.group_norm(xr, 32, P["norm.weight"], P["norm.bias"], eps=1e-6)
+        q, k, v = (F.conv2d(h, P[f"{n}.weight"], P[f"{n}.bias"]) for n in "qkv")
+        b, c, hh, ww = q.shape
+        w_ = torch.softmax(torch.bmm(q.reshape(b, c, -1).permute(0, 2, 1), k.reshape(b, c, -1)) * c ** -0.5, dim=2)
+        o = torch.bmm(v.reshape(b, c, -1), w_.permute(0, 2, 1)).reshape(b, c, hh, ww)
+        yr = xr + F.conv2d(o, P["proj_out.weight"], P["proj_out.bias"])
+    else:
+        h = F.silu(F.group_norm(xr, 32, P["norm1.weight"], P["norm1.bias"], eps=1e-6))
+        h = F.conv2d(h, P["conv1.weight"], P["conv1.bias"], padding=1)
+        h = F.silu(F.group_norm(h, 32, P["norm2.weight"], P["norm2.bias"], eps=1e-6))
+        h = F.conv2d(h, P["conv2.weight"], P["conv2.bias"], padding=1)
+        sc = xr if cin == cout else F.conv2d(xr, P["nin_shortcut.weight"], P["nin_shortcut.bias"])
+        yr = sc + h
+    yr.backward(gy.double())
+    assert rel(y, yr) < CONV_TOL
+    assert rel(xd.grad, xr.grad) < 1e-3

@@ -100,3 +100,16 @@ def test_distributed_sampler_semantics():
     import numpy as np
     assert standardize_labels(np.array([[3], [1]])).tolist() == [3, 1]
     assert standardize_labels(np.array([[0, 1, 1], [0, 0, 0]])).tolist() == [1, 0]
+
+
+def test_grad_sink_park_take_semantics():
+    """GradSink (ops.py): producer parks, consumer takes; a consumer that ran first closes the sink so
+    the producer returns its gradient to autograd instead (correct in either engine order)."""
+    from medvae_disentangled_multimodal_amd import ops
+    s = ops.GradSink()
+    g = torch.ones(3)
+    assert s.park(g) and s.take() is g and s.g is None and not s.closed
+    s2 = ops.GradSink()
+    assert s2.take() is None and s2.closed and not s2.park(g)
+    s3 = ops.GradSink()  # stale park (partial backward) is replaced by the next pass's gradient
+    assert s3.park(torch.zeros(3)) and s3.park(g) and s3.take() is g
