@@ -62,6 +62,16 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
                            int wo, int mode, float* workspace, size_t workspace_bytes, void* stream);
 size_t mvae_conv2d_wgrad_workspace_bytes(int nb, int cin, int cout, int kh, int kw, int ho, int wo);
 
+/* Weight (+ bias) gradient of a 3x3 / stride-1 / pad-1 conv with 1 <= cout <= 4 (Decoder.conv_out,
+ * src/models/encoder_decoder.py:418-419): each x element read once and scattered into its 9 taps
+ * (a cout-row implicit GEMM would stream the 9x im2col for 3 useful rows). Same contract as
+ * mvae_conv2d_wgrad_nhwc (dw = beta*dw + ..., dbias optional); x_split = 1: x holds split4_bf16 groups
+ * (x = hi + lo). cin % 4 == 0, x 16-B aligned. Deterministic (fixed-order partials). */
+int mvae_conv2d_wgrad_small_cout_nhwc(const float* dy, const float* x, float* dw, float* dbias, float beta, int nb,
+                                      int h, int w_, int cin, int cout, int x_split, void* workspace,
+                                      size_t workspace_bytes, void* stream);
+size_t mvae_conv2d_wgrad_small_cout_workspace_bytes(int nb, int cin);
+
 /* Input gradient of a stride-2 conv (Downsample, encoder_decoder.py:184-188) by dx parity class: each
  * class is a dense stride-1 conv of dy [nb][ho][wo][cout] with its own <= 2x2 taps of wt [cin][kh][kw][cout]
  * (mvae_conv_weight_transpose), written interleaved into dx [nb][h][w_][cin] (h, w_ even): the useful

@@ -909,15 +909,15 @@ __global__ void splitk_reduce_kernel(GemmArgs a);
 // ------------------------------------------------------------------------------------------
 // host-side dispatch
 // ------------------------------------------------------------------------------------------
-enum { T256x256 = 0, T256x128 = 1, T128x256 = 2, T128x128 = 3, T64x64 = 4 };
+enum { T256x256 = 0, T256x128 = 1, T128x256 = 2, T128x128 = 3, T64x64 = 4, T128x16 = 5 };
 
 // process-wide GEMM arithmetic (mvae_set_math_mode): 3xBF16 fp32 emulation (default) or bf16
 enum { MATH_3XBF16 = 0, MATH_BF16 = 1 };
 int math_mode();
 
 inline long long tiles_of(int cfg, const GemmArgs& a) {
-  static const int TM_[] = {256, 256, 128, 128, 64};
-  static const int TN_[] = {256, 128, 256, 128, 64};
+  static const int TM_[] = {256, 256, 128, 128, 64, 128};
+  static const int TN_[] = {256, 128, 256, 128, 64, 16};
   return (long long)cdiv(a.M, TM_[cfg]) * cdiv(a.N, TN_[cfg]) * a.batch;
 }
 
@@ -943,6 +943,9 @@ inline int choose_tile(const GemmArgs& a, bool allow_big, bool can_split) {
   const int ov = tile_override();
   if (ov >= 0 && ov <= 4 && (allow_big || ov >= T128x128)) return ov;
   const long long ms = max_splits_of(a, can_split);
+  // skinny N (Decoder.conv_out forward, cout 3; Encoder.conv_in input gradient, cin 6): 128x16 tiles on
+  // 2 waves instead of 64-wide tiles that are 95 % padding
+  if (allow_big && a.N <= 16 && tiles_of(T128x16, a) >= 512) return T128x16;
   if (allow_big) {
     if (tiles_of(T256x256, a) * ms >= 240 && a.M > 128 && a.N > 128) return T256x256;
     if (a.N <= 128 && tiles_of(T256x128, a) * ms >= 240 && a.M > 128) return T256x128;
@@ -955,12 +958,12 @@ inline int choose_tile(const GemmArgs& a, bool allow_big, bool can_split) {
 template <int CFG, int AK, int VA, int BKIND, int VB>
 void launch_cfg(GemmArgs& a, hipStream_t st) {
   constexpr int BM = CFG == T256x256 || CFG == T256x128 ? 256 : CFG == T64x64 ? 64 : 128;
-  constexpr int BN = CFG == T256x256 || CFG == T128x256 ? 256 : CFG == T64x64 ? 64 : 128;
+  constexpr int BN = CFG == T256x256 || CFG == T128x256 ? 256 : CFG == T64x64 ? 64 : CFG == T128x16 ? 16 : 128;
   constexpr int WGM = CFG == T256x128 ? 4 : 2;
 #ifdef MVAE_W4
   constexpr int WGN = CFG == T128x256 ? 4 : 2;  // 256x256 on 4 waves (128x128 per wave)
 #else
-  constexpr int WGN = (CFG == T256x256 || CFG == T128x256) ? 4 : 2;
+  constexpr int WGN = (CFG == T256x256 || CFG == T128x256) ? 4 : CFG == T128x16 ? 1 : 2;
 #endif
   a.tiles_m = cdiv(a.M, BM);
   a.tiles_n = cdiv(a.N, BN);
@@ -978,6 +981,10 @@ void launch_big(GemmArgs& a, hipStream_t st, int cfg) {
     case T256x128: launch_cfg<T256x128, AK, VA, BKIND, VB>(a, st); break;
     case T128x256: launch_cfg<T128x256, AK, VA, BKIND, VB>(a, st); break;
     case T128x128: launch_cfg<T128x128, AK, VA, BKIND, VB>(a, st); break;
+    case T128x16:  // 16-wide tiles need the 16x16x32 MFMA shape
+      if constexpr (mf_of(AK) == 16) launch_cfg<T128x16, AK, VA, BKIND, VB>(a, st);
+      else launch_cfg<T64x64, AK, VA, BKIND, VB>(a, st);
+      break;
     default: launch_cfg<T64x64, AK, VA, BKIND, VB>(a, st); break;
   }
 }

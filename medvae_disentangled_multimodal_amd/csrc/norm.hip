@@ -12,6 +12,10 @@
 
 namespace mvae {
 
+#ifndef GN_UNROLL
+#define GN_UNROLL 4  // rows in flight per thread in the streaming GroupNorm kernels
+#endif
+
 // counter-based hash -> uniform [0,1) for the dropout mask (recomputed in backward, never stored)
 __device__ __forceinline__ float hash_uniform(unsigned long long seed, unsigned long long idx) {
   unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
@@ -83,17 +87,17 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(GnArgs a) {
       const float* xp = a.x + sbase + mp.c4 * 4;
       const float* dp = a.dy + sbase + mp.c4 * 4;
       int row = mp.row_lo + mp.rph;
-      for (; row < mp.row_hi; row += 4 * mp.rpar) {
-        float4 xv[4], dv[4];
+      for (; row < mp.row_hi; row += GN_UNROLL * mp.rpar) {
+        float4 xv[GN_UNROLL], dv[GN_UNROLL];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < GN_UNROLL; ++u) {
           const int r = row + u * mp.rpar;
           const bool ok = r < mp.row_hi;
           xv[u] = ok ? *(const float4*)(xp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
           if (KIND == 1) dv[u] = ok ? *(const float4*)(dp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < GN_UNROLL; ++u) {
           const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
           if (KIND == 0) {
 #pragma unroll
@@ -203,15 +207,15 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(GnArgs a, const float* __
       const float4 sh = *(const float4*)(shift + (long long)b * a.C + mp.c4 * 4);
       const float* xp = a.x + sbase + mp.c4 * 4;
       float* yp = y + sbase + mp.c4 * 4;
-      for (int row = mp.row_lo + mp.rph; row < mp.row_hi; row += 4 * mp.rpar) {
-        float4 xv[4];
+      for (int row = mp.row_lo + mp.rph; row < mp.row_hi; row += GN_UNROLL * mp.rpar) {
+        float4 xv[GN_UNROLL];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < GN_UNROLL; ++u) {
           const int r = row + u * mp.rpar;
           xv[u] = r < mp.row_hi ? *(const float4*)(xp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < GN_UNROLL; ++u) {
           const int r = row + u * mp.rpar;
           if (r >= mp.row_hi) continue;
           float o[4] = {xv[u].x * sc.x + sh.x, xv[u].y * sc.y + sh.y, xv[u].z * sc.z + sh.z, xv[u].w * sc.w + sh.w};
@@ -326,17 +330,17 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
       const float* xp = a.x + sbase + mp.c4 * 4;
       const float* dp = a.dy + sbase + mp.c4 * 4;
       float* op = dx + sbase + mp.c4 * 4;
-      for (int row = mp.row_lo + mp.rph; row < mp.row_hi; row += 4 * mp.rpar) {
-        float4 xv[4], dv[4];
+      for (int row = mp.row_lo + mp.rph; row < mp.row_hi; row += GN_UNROLL * mp.rpar) {
+        float4 xv[GN_UNROLL], dv[GN_UNROLL];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < GN_UNROLL; ++u) {
           const int r = row + u * mp.rpar;
           const bool ok = r < mp.row_hi;
           xv[u] = ok ? *(const float4*)(xp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
           dv[u] = ok ? *(const float4*)(dp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < GN_UNROLL; ++u) {
           const int r = row + u * mp.rpar;
           if (r >= mp.row_hi) continue;
           const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};

@@ -174,6 +174,7 @@ STRIDE2_CLASSES = os.environ.get("MVAE_NO_STRIDE2_CLASSES") is None
 # weight operands handed to the GEMM pre-split into 3xBF16 hi/lo pairs (include/medvae_hip.h MVAE_CONV_WSPLIT):
 # the split is done once per step by the weight-prep kernels instead of in every workgroup's staging
 WEIGHT_SPLIT = os.environ.get("MVAE_NO_WEIGHT_SPLIT") is None
+SMALL_COUT_WGRAD = os.environ.get("MVAE_NO_SMALL_COUT_WGRAD") is None
 MVAE_CONV_WSPLIT = 16
 MVAE_CONV_XSPLIT = 32
 
@@ -280,6 +281,14 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         _lib.call("mvae_gemm_strided_batched", 1, 0, co, c, m, 1.0, dy.data_ptr(), co, 0, x.data_ptr(), c, 0,
                   float(beta), dw.data_ptr(), c, 0, 1, None, None, 0, 0, ws.data_ptr(), ws.numel(), st)
         return False
+    if (SMALL_COUT_WGRAD and co <= 4 and c % 4 == 0 and not g.upsample and g.kh == 3 and g.kw == 3 and g.stride == 1
+            and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and _al16(x)):
+        # Decoder.conv_out (cout 3): x read once, scattered into its 9 taps (no 9x im2col stream)
+        nbytes = _lib.query("mvae_conv2d_wgrad_small_cout_workspace_bytes", n, c)
+        ws = ARENA.get("ws", nbytes, dy.device)
+        _lib.call("mvae_conv2d_wgrad_small_cout_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db),
+                  float(beta), n, h, wd, c, co, int(x_split), ws.data_ptr(), ws.numel(), st)
+        return db is not None
     if _subpixel_upsample(g):
         nbytes = _lib.query("mvae_conv2d_wgrad_upsample_workspace_bytes", n, h, wd, c, co)
         ws = ARENA.get("ws", nbytes, dy.device)

@@ -61,6 +61,9 @@ CONV_CASES = [
     (2, 16, 32, 16, 16, 4, 2, (1, 1, 1, 1), False),
     (2, 32, 16, 8, 8, 1, 2, (0, 0, 0, 0), False),
     (2, 6, 8, 8, 8, 3, 2, (0, 0, 1, 1), False),
+    # skinny-N 128x16 tiles (>= 512 tiles): conv_out forward (cout 3), conv_in input gradient (cin 6)
+    (64, 64, 3, 32, 32, 3, 1, (1, 1, 1, 1), False),
+    (64, 6, 64, 32, 32, 3, 1, (1, 1, 1, 1), False),
 ]
 
 
@@ -149,13 +152,14 @@ def test_weight_prep_split_layouts(dev, split):
             assert torch.equal(out, ref), name
 
 
-@pytest.mark.parametrize("drop", [0.0, 0.25])
-def test_groupnorm_split_output_feeds_conv(dev, drop):
+@pytest.mark.parametrize("drop,co", [(0.0, 32), (0.25, 32), (0.0, 3)])
+def test_groupnorm_split_output_feeds_conv(dev, drop, co):
     """GroupNorm(+SiLU, dropout) written pre-split for a following conv (MVAE_CONV_XSPLIT): the bytes are
-    the split of the fp32 output, and the conv (fwd + weight grad) matches the conv of the fp32 output."""
+    the split of the fp32 output, and the conv (fwd + weight grad) matches the conv of the fp32 output
+    (co = 3: Decoder.conv_out, whose weight gradient runs on the small-cout kernel)."""
     from medvae_disentangled_multimodal_amd import _lib, ops
     g = torch.Generator().manual_seed(21)
-    n, c, co, h = 2, 64, 32, 12
+    n, c, h = 2, 64, 12
     x = cl(torch.randn(n, c, h, h, generator=g) * 2 + 0.5, dev)
     gam = (torch.rand(c, generator=g) + 0.5).to(dev)
     bet = (torch.randn(c, generator=g) * 0.1).to(dev)
