@@ -30,7 +30,17 @@ __global__ void __launch_bounds__(256) mt_chunk_stats_kernel(MtArgs a) {
   const int len = a.chunk_len[ch];
   double acc = 0;
   int badf = 0;
-  for (int i = threadIdx.x; i < len; i += blockDim.x) {
+  const int body = (s & 3) == 0 ? (len & ~3) : 0;
+  for (int i = threadIdx.x * 4; i < body; i += blockDim.x * 4) {
+    const float4 g4 = *(const float4*)(a.g + s + i);
+    const float xs[4] = {g4.x * a.gscale, g4.y * a.gscale, g4.z * a.gscale, g4.w * a.gscale};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (!isfinite(xs[e])) badf = 1;
+      acc += (double)xs[e] * xs[e];
+    }
+  }
+  for (int i = body + threadIdx.x; i < len; i += blockDim.x) {
     const float x = a.g[s + i] * a.gscale;
     if (!isfinite(x)) badf = 1;
     acc += (double)x * x;
@@ -97,7 +107,35 @@ __global__ void __launch_bounds__(256) mt_adam_kernel(MtArgs a, float lr, float 
   const float bc2_sqrt = (float)sqrt(bc2);
   const float decay = (float)(1.0 - (double)lr * (double)wd);
   const float w = 1.f - b1;
-  for (int i = threadIdx.x; i < len; i += blockDim.x) {
+  // one element of the update (torch.optim.Adam/AdamW single-tensor arithmetic, in its operation order)
+  auto upd = [&](float g, float& p, float& m, float& v) -> float {
+    g = zero ? 0.f : g * a.gscale;
+    g = g * coef;
+    const float gout = g;
+    if (decoupled) p = p * decay;
+    else if (wd != 0.f) g = g + wd * p;
+    m = (w < 0.5f) ? m + w * (g - m) : g - (g - m) * (1.f - w);
+    v = v * b2 + (1.f - b2) * g * g;
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    p = p + (-step_size) * (m / denom);
+    return gout;
+  };
+  // 16-B body (flat-buffer tensors are 16-B aligned), scalar tail
+  const int body = (s & 3) == 0 ? (len & ~3) : 0;
+  for (int i = threadIdx.x * 4; i < body; i += blockDim.x * 4) {
+    const long long e = s + i;
+    float4 g4 = *(const float4*)(a.g + e), p4 = *(const float4*)(a.p + e);
+    float4 m4 = *(const float4*)(a.m + e), v4 = *(const float4*)(a.v + e);
+    g4.x = upd(g4.x, p4.x, m4.x, v4.x);
+    g4.y = upd(g4.y, p4.y, m4.y, v4.y);
+    g4.z = upd(g4.z, p4.z, m4.z, v4.z);
+    g4.w = upd(g4.w, p4.w, m4.w, v4.w);
+    *(float4*)(a.g + e) = g4;
+    *(float4*)(a.p + e) = p4;
+    *(float4*)(a.m + e) = m4;
+    *(float4*)(a.v + e) = v4;
+  }
+  for (int i = body + threadIdx.x; i < len; i += blockDim.x) {
     const long long e = s + i;
     float g = zero ? 0.f : a.g[e] * a.gscale;
     g = g * coef;
