@@ -110,6 +110,7 @@ struct GemmArgs {
   // [2Ho][2Wo = sub_w2] image: 4m - 2j + ph*sub_w2 + pw, class (ph, pw) = bidx + sub_par
   int sub_w2 = 0, sub_par = 0;
   int out_remap = 0;  // epilogue writes C row sub_pixel(m) (conv outputs); else row m
+  int vec_epi = 0;    // set by launch_cfg: 16-B epilogue through LDS is legal (see gemm3x_kernel)
 };
 
 // full-resolution pixel of class-grid pixel m (see GemmArgs::sub_w2)
@@ -155,6 +156,10 @@ __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, unsigned off) 
 }
 __device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+}
+__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, unsigned off, const float4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(
+      u32x4_t{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)}, r, off, 0, 0);
 }
 
 template <int ROWS, bool COL>
@@ -857,6 +862,58 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
     }
   }
 
+  // 16-B epilogue (16x16x32 kernels, one split, plain row order, N / ldc / ldr multiples of 4): each wave
+  // stages half of its accumulator block at a time in LDS (free after the main loop) as fp32 rows and
+  // re-reads them as float4 runs of the row, so bias / residual / beta*C / the store move whole 16-B
+  // groups along C's contiguous channel dimension instead of 4-B scalars in 64-B pieces.
+  if constexpr (MF == 16 && TM % 2 == 0) {
+    if (a.vec_epi) {
+      constexpr int WR = BM / WGM, WC = BN / WGN, HR = WR / 2, PE = WC + 4;
+      static_assert((NT / 64) * HR * PE * 4 <= 4 * BUF, "epilogue staging exceeds the LDS");
+      constexpr int C4 = WC / 4, RPI = 64 / C4;  // float4 per staged row, rows per wave instruction
+      float* stg = (float*)lds + wid * HR * PE;
+      const __amdgpu_buffer_rsrc_t cr = make_rsrc(a.C + bidx * a.sC, a.c_bytes);
+      const bool has_res = a.res != nullptr;
+      const __amdgpu_buffer_rsrc_t rr = make_rsrc(has_res ? a.res + bidx * a.sR : a.C, has_res ? a.r_bytes : 0u);
+      const int c4 = lane % C4, rsub = lane / C4;
+      const int col = n0 + brow + c4 * 4;
+      float4 bv{0.f, 0.f, 0.f, 0.f};
+      if (a.bias != nullptr && col < a.N) bv = *(const float4*)(a.bias + col);
+      __syncthreads();  // every wave's last fragment reads are done: the LDS is free
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int i = 0; i < TM / 2; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+              stg[(i * 16 + acc_row<MF>(r, lane)) * PE + j * 16 + (lane & 15)] = acc[pass * (TM / 2) + i][j][r];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < HR / RPI; ++k) {
+          const int lr = k * RPI + rsub;
+          const float4 s4 = *(const float4*)(stg + lr * PE + c4 * 4);
+          const int row = m0 + arow + pass * HR + lr;
+          const bool ok = row < a.M && col < a.N;
+          const unsigned co = ok ? ((unsigned)row * (unsigned)a.ldc + col) * 4u : OOB;
+          float4 v{a.alpha * s4.x + bv.x, a.alpha * s4.y + bv.y, a.alpha * s4.z + bv.z, a.alpha * s4.w + bv.w};
+          if (has_res) {
+            const float4 r4 = bload4(rr, ok ? ((unsigned)row * (unsigned)a.ldr + col) * 4u : OOB);
+            v.x += r4.x; v.y += r4.y; v.z += r4.z; v.w += r4.w;
+          }
+          if (a.beta != 0.f) {
+            const float4 c4v = bload4(cr, co);
+            v.x += a.beta * c4v.x; v.y += a.beta * c4v.y; v.z += a.beta * c4v.z; v.w += a.beta * c4v.w;
+          }
+          bstore4(cr, co, v);
+        }
+        __syncthreads();
+      }
+      return;
+    }
+  }
+
   // epilogue: C/D layout of the MFMA tile: col = lane & (MF-1), row = acc_row<MF>(r, lane).
   // Stores go through buffer descriptors: rows/cols outside the matrix are dropped by the hardware.
   if (a.splits > 1) {
@@ -955,6 +1012,12 @@ inline int choose_tile(const GemmArgs& a, bool allow_big, bool can_split) {
   return T64x64;
 }
 
+inline bool al16(const void* p);
+inline bool vec_epi_disabled() {
+  static int v = getenv("MVAE_NO_VEC_EPI") != nullptr;  // experiment knob: scalar epilogue everywhere
+  return v != 0;
+}
+
 template <int CFG, int AK, int VA, int BKIND, int VB>
 void launch_cfg(GemmArgs& a, hipStream_t st) {
   constexpr int BM = CFG == T256x256 || CFG == T256x128 ? 256 : CFG == T64x64 ? 64 : 128;
@@ -967,6 +1030,9 @@ void launch_cfg(GemmArgs& a, hipStream_t st) {
 #endif
   a.tiles_m = cdiv(a.M, BM);
   a.tiles_n = cdiv(a.N, BN);
+  a.vec_epi = a.splits == 1 && !a.out_remap && (a.N & 3) == 0 && (a.ldc & 3) == 0 && (a.sC & 3) == 0 && al16(a.C) &&
+              (!a.res || ((a.ldr & 3) == 0 && (a.sR & 3) == 0 && al16(a.res))) && (!a.bias || al16(a.bias)) &&
+              !vec_epi_disabled();
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splits);
   if (math_mode() == MATH_BF16)
     hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, 1>), grid, dim3(64 * WGM * WGN), 0, st, a);
