@@ -53,6 +53,14 @@ int mvae_get_math_mode(void);
 int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y,
                      int nb, int h, int w_, int cin, int cout, int kh, int kw, int stride, int pad_t,
                      int pad_l, int ho, int wo, int mode, void* stream);
+/* mvae_conv2d_nhwc that also emits, from the GEMM epilogue, the GroupNorm statistics of y for the
+ * Normalize that consumes it (ResnetBlock conv1 -> norm2, block output -> next norm1, ...,
+ * encoder_decoder.py:141-170): gn_part = [nb*ho*wo/32][cout/4][2] fp64 {sum y, sum y^2} over 32 pixels
+ * x 4 channels (see mvae_group_norm_fwd_part_nhwc). Needs ho*wo % 32 == 0, cout % 4 == 0, 16-B aligned
+ * y / residual / bias, cin % 4 == 0. */
+int mvae_conv2d_gnstats_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y,
+                             int nb, int h, int w_, int cin, int cout, int kh, int kw, int stride, int pad_t,
+                             int pad_l, int ho, int wo, int mode, double* gn_part, void* stream);
 
 /* Weight gradient of mvae_conv2d_nhwc (modes 0/1): dw = beta*dw + sum_pixels dy (x) x, and (if dbias
  * is non-null) the bias gradient dbias = beta*dbias + sum_pixels dy, computed from the same staged dy.
@@ -145,6 +153,13 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
                              unsigned long long seed, void* workspace, size_t workspace_bytes,
                              void* stream);
 size_t mvae_group_norm_workspace_bytes(int nb, int hw, int c);
+/* mvae_group_norm_fwd_nhwc from the statistics the producing convolution emitted
+ * (mvae_conv2d_gnstats_nhwc, part = [nb*hw/32][c/4][2] fp64): skips the statistics pass over x.
+ * hw % 32 == 0, (c / groups) % 4 == 0. */
+int mvae_group_norm_fwd_part_nhwc(const float* x, const double* part, const float* gamma, const float* beta, float* y,
+                                  float* mean, float* rstd, int nb, int hw, int c, int groups, float eps, int silu,
+                                  float drop_p, unsigned long long seed, int y_split, void* workspace,
+                                  size_t workspace_bytes, void* stream);
 
 /* ---- reparameterization / KL / reconstruction ---------------------------------------------------
  * BaseVAE.reparameterize (src/models/base_vae.py:83-87) with explicit eps; mu/logvar are channel

@@ -29,9 +29,37 @@ extern "C" {
 //   mode 2: transposed gather: y[oh] += x[(oh + pad - r)/stride] * w[r] (dgrad of a strided conv;
 //           stride must be a power of two)
 // y[n][ho][wo][cout] = sum + bias[cout] + residual[n][ho][wo][cout]
+static int conv2d_impl(const float* x, const float* w, const float* bias, const float* residual, float* y, int nb,
+                       int h, int wd, int cin, int cout, int kh, int kw, int stride, int pad_t, int pad_l, int ho,
+                       int wo, int mode, double* gn_part, void* stream);
+
 int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const float* residual,
                      float* y, int nb, int h, int wd, int cin, int cout, int kh, int kw,
                      int stride, int pad_t, int pad_l, int ho, int wo, int mode, void* stream) {
+  return conv2d_impl(x, w, bias, residual, y, nb, h, wd, cin, cout, kh, kw, stride, pad_t, pad_l, ho, wo, mode,
+                     nullptr, stream);
+}
+
+// mvae_conv2d_nhwc that also emits the GroupNorm statistics of y for the Normalize that follows
+// (gn_part: [nb*ho*wo/32][cout/4][2] fp64 {sum, sum of squares}); needs ho*wo % 32 == 0, cout % 4 == 0,
+// 16-B aligned y / residual / bias.
+int mvae_conv2d_gnstats_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y,
+                             int nb, int h, int wd, int cin, int cout, int kh, int kw, int stride, int pad_t,
+                             int pad_l, int ho, int wo, int mode, double* gn_part, void* stream) {
+  if (gn_part == nullptr || (ho * wo) % 32 != 0 || cout % 4 != 0 || !al16(y) || (residual && !al16(residual)) ||
+      (bias && !al16(bias)) || vec_epi_disabled()) {
+    set_error("conv2d_gnstats: needs ho*wo %% 32 == 0, cout %% 4 == 0, 16-B aligned outputs");
+    return MVAE_EINVAL;
+  }
+  return conv2d_impl(x, w, bias, residual, y, nb, h, wd, cin, cout, kh, kw, stride, pad_t, pad_l, ho, wo, mode,
+                     gn_part, stream);
+}
+
+}  // extern "C"
+
+static int conv2d_impl(const float* x, const float* w, const float* bias, const float* residual, float* y, int nb,
+                       int h, int wd, int cin, int cout, int kh, int kw, int stride, int pad_t, int pad_l, int ho,
+                       int wo, int mode, double* gn_part, void* stream) {
   const bool presplit = (mode & MVAE_CONV_WSPLIT) != 0;
   const bool xsplit = (mode & MVAE_CONV_XSPLIT) != 0;
   mode &= ~(MVAE_CONV_WSPLIT | MVAE_CONV_XSPLIT);
@@ -72,7 +100,12 @@ int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const fl
     a.perm_rs = (v && cin % BK == 0 && kh * kw > 1 && kperm_enabled()) ? kh * kw : 1;
     set_gather_magic(a);
     a.stride = stride; a.stride_shift = shift; a.pad_t = pad_t; a.pad_l = pad_l;
+    a.gn_part = gn_part ? gn_part + (long long)b0 * (ho * wo / 32) * (cout / 4) * 2 : nullptr;
     const int cfg = choose_tile(a, v, false);
+    if (gn_part && !v) {
+      set_error("conv2d_gnstats: needs the vector (16-B) operand path");
+      return MVAE_EINVAL;
+    }
     if (xsplit) {  // x (and w) hold split4_bf16 groups: no staging split at all
       if (presplit) launch_big<A_CONV_FWD_SPLIT, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
       else launch_big<A_CONV_FWD_SPLIT, 4, B_ROWK, 4>(a, st, cfg);
@@ -95,6 +128,8 @@ int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const fl
   }
   return MVAE_OK;
 }
+
+extern "C" {
 
 // Input gradient of a stride-2 convolution (Downsample, encoder_decoder.py:184-188) by parity class:
 // dx pixel (2m+p, 2j+q) only receives the taps r with r = p + pad_t (mod 2) (and likewise s), so each

@@ -111,6 +111,9 @@ struct GemmArgs {
   int sub_w2 = 0, sub_par = 0;
   int out_remap = 0;  // epilogue writes C row sub_pixel(m) (conv outputs); else row m
   int vec_epi = 0;    // set by launch_cfg: 16-B epilogue through LDS is legal (see gemm3x_kernel)
+  // GroupNorm statistics of the output for the following Normalize (16-B epilogue only): per 32-row block
+  // and 4-channel group, {sum y, sum y^2} in fp64 at gn_part[((row/32) * (N/4) + col/4) * 2]
+  double* gn_part = nullptr;
 };
 
 // full-resolution pixel of class-grid pixel m (see GemmArgs::sub_w2)
@@ -879,6 +882,11 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
       const int col = n0 + brow + c4 * 4;
       float4 bv{0.f, 0.f, 0.f, 0.f};
       if (a.bias != nullptr && col < a.N) bv = *(const float4*)(a.bias + col);
+      constexpr int NSB = WR / 32;  // 32-row blocks of the wave's rows (GroupNorm statistics)
+      double st0[NSB], st1[NSB];
+#pragma unroll
+      for (int q = 0; q < NSB; ++q) st0[q] = st1[q] = 0.0;
+      const bool want_stats = a.gn_part != nullptr;
       __syncthreads();  // every wave's last fragment reads are done: the LDS is free
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
@@ -907,8 +915,30 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
             v.x += a.beta * c4v.x; v.y += a.beta * c4v.y; v.z += a.beta * c4v.z; v.w += a.beta * c4v.w;
           }
           bstore4(cr, co, v);
+          if (want_stats && ok) {
+            const int q = (pass * HR + k * RPI) / 32;  // compile-time: RPI divides 32
+            st0[q] += ((double)v.x + (double)v.y) + ((double)v.z + (double)v.w);
+            st1[q] += ((double)v.x * v.x + (double)v.y * v.y) + ((double)v.z * v.z + (double)v.w * v.w);
+          }
         }
         __syncthreads();
+      }
+      if (want_stats) {  // fixed xor-tree over the lanes of one column group (the RPI row lanes)
+#pragma unroll
+        for (int q = 0; q < NSB; ++q) {
+          double s0 = st0[q], s1 = st1[q];
+#pragma unroll
+          for (int o = C4; o < 64; o <<= 1) {
+            s0 += __shfl_xor(s0, o, 64);
+            s1 += __shfl_xor(s1, o, 64);
+          }
+          const int row0 = m0 + arow + q * 32;
+          if (rsub == 0 && row0 < a.M && col < a.N) {
+            double* gp = a.gn_part + ((long long)(row0 >> 5) * (a.N >> 2) + (col >> 2)) * 2;
+            gp[0] = s0;
+            gp[1] = s1;
+          }
+        }
       }
       return;
     }

@@ -195,6 +195,40 @@ __global__ void __launch_bounds__(256) gn_stats_finalize_kernel(GnArgs a, float*
   }
 }
 
+// Same finalize from the statistics the producing convolution's epilogue emitted
+// (mvae_conv2d_gnstats_nhwc: part[(row/32) * (C/4) + c/4] = {sum, sum sq} over 32 rows x 4 channels)
+__global__ void __launch_bounds__(256) gn_stats_finalize_part_kernel(GnArgs a, const double* __restrict__ part,
+                                                                     float* mean, float* rstd, float* scale,
+                                                                     float* shift, float eps) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (i >= a.nb * a.G) return;
+  const int b = i / a.G, g = i - b * a.G;
+  const int cpg = a.C / a.G, q4 = cpg >> 2, c4n = a.C >> 2, sbn = a.hw >> 5;
+  double s0 = 0, s1 = 0;
+  for (int j = lane; j < sbn * q4; j += 64) {  // fixed order per lane, then a fixed wave tree
+    const int sb = j / q4, c4 = g * q4 + (j - sb * q4);
+    const double* w = part + ((long long)(b * sbn + sb) * c4n + c4) * 2;
+    s0 += w[0];
+    s1 += w[1];
+  }
+  s0 = wave_sum_d(s0);
+  s1 = wave_sum_d(s1);
+  const double n = (double)a.hw * cpg;
+  const double mu = s0 / n;
+  double var = s1 / n - mu * mu;
+  if (var < 0) var = 0;
+  const float rs = (float)(1.0 / sqrt(var + (double)eps));
+  if (lane == 0) {
+    mean[i] = (float)mu;
+    rstd[i] = rs;
+  }
+  for (int c = g * cpg + lane; c < (g + 1) * cpg; c += 64) {
+    const float sc = rs * a.gamma[c];
+    scale[b * a.C + c] = sc;
+    shift[b * a.C + c] = a.beta[c] - (float)mu * sc;
+  }
+}
+
 // y = [dropout](silu?(x*scale + shift))
 __global__ void __launch_bounds__(256) gn_apply_kernel(GnArgs a, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, float* __restrict__ y) {
@@ -423,6 +457,35 @@ int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* be
   float* shift = scale + (size_t)nb * c;
   hipLaunchKernelGGL(gn_partial_kernel<0>, dim3(a.chunks, nb), dim3(256), 0, st, a);
   hipLaunchKernelGGL(gn_stats_finalize_kernel, dim3(cdiv((long long)nb * groups, 4)), dim3(256), 0, st, a,
+                     mean, rstd, scale, shift, eps);
+  a.silu = silu; a.drop_p = drop_p; a.seed = seed; a.y_split = y_split;
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(a.chunks, nb), dim3(256), 0, st, a, scale, shift, y);
+  return launch_status();
+}
+
+// Forward from the statistics emitted by the producing convolution (mvae_conv2d_gnstats_nhwc): no
+// statistics pass over x.
+int mvae_group_norm_fwd_part_nhwc(const float* x, const double* part, const float* gamma, const float* beta, float* y,
+                                  float* mean, float* rstd, int nb, int hw, int c, int groups, float eps, int silu,
+                                  float drop_p, unsigned long long seed, int y_split, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  if (nb <= 0 || hw <= 0 || c <= 0 || (c & 3) || groups <= 0 || c % groups || (c / groups) % 4 || hw % 32) {
+    set_error("group_norm_part: needs hw %% 32 == 0 and channels per group %% 4 == 0");
+    return MVAE_EINVAL;
+  }
+  if (workspace_bytes < mvae_group_norm_workspace_bytes(nb, hw, c)) {
+    set_error("group_norm_part: workspace too small");
+    return MVAE_EWORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  GnArgs a{};
+  a.x = x; a.gamma = gamma; a.beta = beta; a.nb = nb; a.hw = hw; a.C = c; a.G = groups;
+  a.chunks = gn_chunks(nb, hw);
+  a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
+  a.ws = (double*)workspace;
+  float* scale = (float*)((char*)workspace + (size_t)nb * a.chunks * c * 2 * sizeof(double));
+  float* shift = scale + (size_t)nb * c;
+  hipLaunchKernelGGL(gn_stats_finalize_part_kernel, dim3(cdiv((long long)nb * groups, 4)), dim3(256), 0, st, a, part,
                      mean, rstd, scale, shift, eps);
   a.silu = silu; a.drop_p = drop_p; a.seed = seed; a.y_split = y_split;
   hipLaunchKernelGGL(gn_apply_kernel, dim3(a.chunks, nb), dim3(256), 0, st, a, scale, shift, y);

@@ -61,8 +61,10 @@ class Conv2d(nn.Module):
             bound = 1 / math.sqrt(fan_in) if fan_in > 0 else 0
             nn.init.uniform_(self.bias, -bound, bound)
 
-    def forward(self, x, residual=None, geom: Optional[ConvGeom] = None, res_sink=None, x_sink=None):
-        return ops.conv2d(x, self.weight, self.bias, geom or self.geom, residual, res_sink, x_sink)
+    def forward(self, x, residual=None, geom: Optional[ConvGeom] = None, res_sink=None, x_sink=None,
+                gn_stats: bool = False):
+        # gn_stats: the output feeds a Normalize; its statistics come out of the conv's epilogue
+        return ops.conv2d(x, self.weight, self.bias, geom or self.geom, residual, res_sink, x_sink, gn_stats)
 
 
 class GroupNorm(nn.Module):
@@ -110,13 +112,13 @@ class ResnetBlock(nn.Module):
             raise NotImplementedError("timestep embeddings are not used by the VAE (temb_channels=0)")
         # x's two gradient branches (norm1 and the residual / shortcut) are summed inside norm1's backward
         sink = ops.GradSink() if torch.is_grad_enabled() and x.requires_grad else None
-        h = self.conv1(self.norm1(x, silu=True, for_conv=True, grad_sink=sink))
+        h = self.conv1(self.norm1(x, silu=True, for_conv=True, grad_sink=sink), gn_stats=True)
         p = self.dropout.p if self.training else 0.0
         h = self.norm2(h, silu=True, drop_p=p, for_conv=True)
         if self.in_channels != self.out_channels:
             sc = self.conv_shortcut if self.use_conv_shortcut else self.nin_shortcut
-            return self.conv2(h, residual=sc(x, x_sink=sink))
-        return self.conv2(h, residual=x, res_sink=sink)
+            return self.conv2(h, residual=sc(x, x_sink=sink), gn_stats=True)
+        return self.conv2(h, residual=x, res_sink=sink, gn_stats=True)
 
 
 class AttnBlock(nn.Module):
@@ -153,7 +155,7 @@ class Downsample(nn.Module):
         self.geom = ConvGeom(3, 3, 2, 0, 0, 1, 1)
 
     def forward(self, x):
-        return self.conv(x, geom=self.geom)
+        return self.conv(x, geom=self.geom, gn_stats=True)
 
 
 class Upsample(nn.Module):
@@ -210,7 +212,7 @@ class Encoder(nn.Module):
         self.conv_out = Conv2d(block_in, 2 * z_channels if double_z else z_channels, 3, 1, 1)
 
     def forward(self, x):
-        h = self.conv_in(x)
+        h = self.conv_in(x, gn_stats=True)
         for i_level in range(self.num_resolutions):
             lvl = self.down[i_level]
             for i_block in range(self.num_res_blocks):
@@ -264,7 +266,7 @@ class Decoder(nn.Module):
         self.conv_out = Conv2d(block_in, out_ch, 3, 1, 1)
 
     def forward(self, z):
-        h = self.conv_in(z)
+        h = self.conv_in(z, gn_stats=True)
         h = self.mid.block_2(self.mid.attn_1(self.mid.block_1(h)))
         for i_level in reversed(range(self.num_resolutions)):
             lvl = self.up[i_level]

@@ -183,7 +183,9 @@ def _al16(*ts) -> bool:
     return all(t.data_ptr() % 16 == 0 for t in ts)
 
 
-def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False):
+def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part=None):
+    """gn_part (fp64 [n*ho*wo/32 * cout/4 * 2]): also emit the GroupNorm statistics of y from the GEMM
+    epilogue (mvae_conv2d_gnstats_nhwc; only on the plain implicit-GEMM path -- the caller checks)."""
     n, c, h, wd = x.shape
     co = w.shape[0]
     ho, wo = g.out_hw(h, wd)
@@ -212,8 +214,12 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False):
                       h, wd, c, co, int(split), st)
         else:
             mode = (1 if g.upsample else 0) | (MVAE_CONV_WSPLIT if split else 0) | (MVAE_CONV_XSPLIT if x_split else 0)
-            _lib.call("mvae_conv2d_nhwc", x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n, h, wd, c,
-                      co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, mode, st)
+            if gn_part is not None:
+                _lib.call("mvae_conv2d_gnstats_nhwc", x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(),
+                          n, h, wd, c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, mode, gn_part.data_ptr(), st)
+            else:
+                _lib.call("mvae_conv2d_nhwc", x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n, h, wd,
+                          c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, mode, st)
     return y
 
 
@@ -339,7 +345,7 @@ class GradSink:
 
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, geom: ConvGeom, res_sink=None, x_sink=None):
+    def forward(ctx, x, weight, bias, residual, geom: ConvGeom, res_sink=None, x_sink=None, gn_part=None):
         _check(x, "conv input")
         xs = bool(getattr(x, XSPLIT_ATTR, False))
         if xs and not x.is_contiguous(memory_format=CL):
@@ -347,7 +353,7 @@ class Conv2dFn(torch.autograd.Function):
         x = nhwc(x)
         w = _krsc(weight)
         res = nhwc(residual) if residual is not None else None
-        y = conv2d_forward_raw(x, w, bias, res, geom, xs)
+        y = conv2d_forward_raw(x, w, bias, res, geom, xs, gn_part)
         ctx.geom = geom
         ctx.x_split = xs
         ctx.has_bias = bias is not None
@@ -397,11 +403,30 @@ class Conv2dFn(torch.autograd.Function):
             _grad_done(ctx.weight_ref)
         if want_b and db_ret is None:
             _grad_done(ctx.bias_ref)
-        return dx, dw_ret, db_ret, dres, None, None, None
+        return dx, dw_ret, db_ret, dres, None, None, None, None
 
 
-def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink=None):
-    return Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink)
+# The GroupNorm statistics of a conv output emitted by its GEMM epilogue travel with the output tensor
+# (with its version counter: an in-place change before the GroupNorm invalidates them).
+GN_PART_ATTR = "_mvae_gn_part"
+GN_FUSED_STATS = os.environ.get("MVAE_NO_GN_FUSED") is None and os.environ.get("MVAE_NO_VEC_EPI") is None
+
+
+def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink=None, gn_stats: bool = False):
+    """gn_stats=True: the output feeds a Normalize (encoder_decoder.py:28-33) -- emit its statistics from the
+    conv's epilogue so the GroupNorm skips its statistics pass (plain implicit-GEMM convs only)."""
+    part = None
+    if gn_stats and GN_FUSED_STATS and not geom.pointwise and not _subpixel_upsample(geom) and x.shape[1] % 4 == 0:
+        n, _, h, w = x.shape
+        ho, wo = geom.out_hw(h, w)
+        co = weight.shape[0]
+        if (ho * wo) % 32 == 0 and co % 4 == 0 and _al16(x, weight) and (bias is None or _al16(bias)) and (
+                residual is None or _al16(residual)):
+            part = torch.empty(n * ho * wo // 32 * (co // 4) * 2, device=x.device, dtype=torch.float64)
+    y = Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink, part)
+    if part is not None:
+        setattr(y, GN_PART_ATTR, (part, y._version))
+    return y
 
 
 # ------------------------------------------------------------------------------------------
@@ -410,7 +435,7 @@ def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink
 class GroupNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool, drop_p: float, seed: int,
-                y_split: bool = False, grad_sink=None):
+                y_split: bool = False, grad_sink=None, part=None):
         _check(x, "group_norm input")
         x = nhwc(x)
         n, c, h, w = x.shape
@@ -420,9 +445,15 @@ class GroupNormFn(torch.autograd.Function):
         nbytes = _lib.query("mvae_group_norm_workspace_bytes", n, h * w, c)
         ws = ARENA.get("gn", nbytes, x.device)
         with _timed("gn_fwd", 8.0 * x.numel(), (n, c, h * w)):  # algorithmic HBM bytes: read x, write y
-            _lib.call("mvae_group_norm_fwd_nhwc", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
-                      mean.data_ptr(), rstd.data_ptr(), n, h * w, c, groups, float(eps), int(silu), float(drop_p),
-                      int(seed) & 0xFFFFFFFFFFFFFFFF, int(y_split), ws.data_ptr(), ws.numel(), _stream(x))
+            if part is not None:  # statistics from the producing conv's epilogue: no pass over x for them
+                _lib.call("mvae_group_norm_fwd_part_nhwc", x.data_ptr(), part.data_ptr(), gamma.data_ptr(),
+                          beta.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), n, h * w, c, groups,
+                          float(eps), int(silu), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, int(y_split),
+                          ws.data_ptr(), ws.numel(), _stream(x))
+            else:
+                _lib.call("mvae_group_norm_fwd_nhwc", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
+                          mean.data_ptr(), rstd.data_ptr(), n, h * w, c, groups, float(eps), int(silu), float(drop_p),
+                          int(seed) & 0xFFFFFFFFFFFFFFFF, int(y_split), ws.data_ptr(), ws.numel(), _stream(x))
         ctx.save_for_backward(x, gamma, beta, mean, rstd)
         ctx.cfg = (groups, int(silu), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF)
         ctx.gamma_ref, ctx.beta_ref = gamma, beta
@@ -458,7 +489,7 @@ class GroupNormFn(torch.autograd.Function):
             _grad_done(ctx.gamma_ref)
         if ctx.needs_input_grad[2] and db_ret is None:
             _grad_done(ctx.beta_ref)
-        return dx, dg_ret, db_ret, None, None, None, None, None, None, None
+        return dx, dg_ret, db_ret, None, None, None, None, None, None, None, None
 
 
 # Activations handed to a convolution in the pre-split 3xBF16 operand layout carry this attribute
@@ -472,7 +503,14 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
     output is then written pre-split for the GEMM (GroupNorm -> conv is the ResnetBlock / norm_out pattern,
     encoder_decoder.py:141-163, :318-328)."""
     split = bool(for_conv and ACT_SPLIT and x.shape[1] % 4 == 0)
-    y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink)
+    part = getattr(x, GN_PART_ATTR, None)
+    if part is not None:
+        delattr(x, GN_PART_ATTR)  # consumed once; frees the statistics with the next allocation cycle
+        h, w = x.shape[2], x.shape[3]
+        ok = part[1] == x._version and (h * w) % 32 == 0 and (x.shape[1] // groups) % 4 == 0 and \
+            x.shape[1] % groups == 0 and x.is_contiguous(memory_format=CL)
+        part = part[0] if ok else None
+    y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink, part)
     if split:
         setattr(y, XSPLIT_ATTR, True)
     return y

@@ -378,3 +378,34 @@ def test_block_input_gradient_branches_summed_in_groupnorm(dev, cin, cout, attn)
     yr.backward(gy.double())
     assert rel(y, yr) < CONV_TOL
     assert rel(xd.grad, xr.grad) < 1e-3
+
+
+@pytest.mark.parametrize("n,c,co,h,res", [(4, 64, 128, 16, False), (8, 128, 256, 8, True), (16, 256, 256, 32, True)])
+def test_conv_epilogue_groupnorm_statistics(dev, n, c, co, h, res):
+    """conv2d(gn_stats=True) emits {sum, sum sq} per 32 pixels x 4 channels from the GEMM epilogue and the
+    following GroupNorm(+SiLU) finalizes from them (no statistics pass): same output as the two-pass
+    GroupNorm of the same conv output; an in-place change of the conv output drops the statistics."""
+    from medvae_disentangled_multimodal_amd import ops
+    g = torch.Generator().manual_seed(7)
+    x = cl(torch.randn(n, c, h, h, generator=g), dev)
+    w = cl(torch.randn(co, c, 3, 3, generator=g) / math.sqrt(9 * c), dev)
+    b = (torch.randn(co, generator=g) * 0.3 + 0.5).to(dev)
+    r = cl(torch.randn(n, co, h, h, generator=g), dev) if res else None
+    gam = (torch.rand(co, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(co, generator=g) * 0.1).to(dev)
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1)
+    y0 = ops.conv2d(x, w, b, geom, residual=r)
+    y1 = ops.conv2d(x, w, b, geom, residual=r, gn_stats=True)
+    assert getattr(y1, ops.GN_PART_ATTR, None) is not None
+    assert torch.equal(y0, y1)
+    ref = ops.group_norm(y0, gam, bet, 32, 1e-6, True)
+    out = ops.group_norm(y1, gam, bet, 32, 1e-6, True)
+    assert not hasattr(y1, ops.GN_PART_ATTR)
+    assert rel(out, ref) < 1e-5
+    # against float64 torch as well
+    t = F.silu(F.group_norm(y0.double().cpu(), 32, gam.double().cpu(), bet.double().cpu(), eps=1e-6))
+    assert rel(out, t) < 1e-5
+    y2 = ops.conv2d(x, w, b, geom, residual=r, gn_stats=True)
+    y2.mul_(2.0)  # stale statistics must not be used
+    assert rel(ops.group_norm(y2, gam, bet, 32, 1e-6, True),
+               F.silu(F.group_norm(y2.double().cpu(), 32, gam.double().cpu(), bet.double().cpu(), eps=1e-6))) < 1e-5
