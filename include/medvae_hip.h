@@ -62,6 +62,17 @@ int mvae_conv2d_gnstats_nhwc(const float* x, const float* w, const float* bias, 
                              int nb, int h, int w_, int cin, int cout, int kh, int kw, int stride, int pad_t,
                              int pad_l, int ho, int wo, int mode, double* gn_part, void* stream);
 
+/* Input gradient of a stride-1 conv (mode 2 of mvae_conv2d_nhwc, wt = [cin][kh][kw][cout]) whose input was
+ * y = silu?(GroupNorm(gn_x)) (ResnetBlock norm1/norm2 -> conv1/conv2, norm_out -> conv_out;
+ * encoder_decoder.py:141-163, :318-328): the GEMM epilogue also emits the GroupNorm backward partials
+ * part = [nb*h*w/32][cin][2] fp64 {sum dyn, sum dyn*xhat}, dyn = dx*silu'(.), consumed by
+ * mvae_group_norm_bwd_part_nhwc. Replaces the reduction half of GroupNorm's backward
+ * (aten::native_group_norm_backward). No dropout in between; h*w % 32 == 0, (cin/groups) % 4 == 0. */
+int mvae_conv2d_dgrad_gnbwd_nhwc(const float* dy, const float* wt, float* dx, int nb, int ho, int wo, int cout,
+                                 int cin, int kh, int kw, int pad_t, int pad_l, int h, int w_, int w_split,
+                                 const float* gn_x, const float* mean, const float* rstd, const float* gamma,
+                                 const float* beta, int groups, int silu, double* part, void* stream);
+
 /* Weight gradient of mvae_conv2d_nhwc (modes 0/1): dw = beta*dw + sum_pixels dy (x) x, and (if dbias
  * is non-null) the bias gradient dbias = beta*dbias + sum_pixels dy, computed from the same staged dy.
  * Replaces the weight/bias half of aten::convolution_backward for the convolutions above. */
@@ -153,6 +164,12 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
                              unsigned long long seed, void* workspace, size_t workspace_bytes,
                              void* stream);
 size_t mvae_group_norm_workspace_bytes(int nb, int hw, int c);
+/* mvae_group_norm_bwd_nhwc (drop_p = 0) from the partials of mvae_conv2d_dgrad_gnbwd_nhwc: no reduction
+ * pass over x and dy. hw % 32 == 0. */
+int mvae_group_norm_bwd_part_nhwc(const float* x, const float* dy, const double* part, const float* gamma,
+                                  const float* beta, const float* mean, const float* rstd, float* dx,
+                                  const float* dx_add, float* dgamma, float* dbeta, int nb, int hw, int c, int groups,
+                                  int silu, void* workspace, size_t workspace_bytes, void* stream);
 /* mvae_group_norm_fwd_nhwc from the statistics the producing convolution emitted
  * (mvae_conv2d_gnstats_nhwc, part = [nb*hw/32][c/4][2] fp64): skips the statistics pass over x.
  * hw % 32 == 0, (c / groups) % 4 == 0. */

@@ -27,6 +27,7 @@ SIGNATURES = {
     "mvae_get_math_mode": (I, []),
     "mvae_conv2d_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P]),
     "mvae_conv2d_gnstats_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P]),
+    "mvae_conv2d_dgrad_gnbwd_nhwc": (I, [P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P, P, I, I, P, P]),
     "mvae_conv2d_wgrad_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),
     "mvae_conv2d_wgrad_workspace_bytes": (Z, [I, I, I, I, I, I, I]),
     "mvae_conv2d_wgrad_small_cout_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, I, P, Z, P]),
@@ -48,6 +49,7 @@ SIGNATURES = {
     "mvae_group_norm_fwd_nhwc": (I, [P, P, P, P, P, P, I, I, I, I, F, I, F, c_uint64, I, P, Z, P]),
     "mvae_group_norm_fwd_part_nhwc": (I, [P, P, P, P, P, P, P, I, I, I, I, F, I, F, c_uint64, I, P, Z, P]),
     "mvae_group_norm_bwd_nhwc": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, c_uint64, P, Z, P]),
+    "mvae_group_norm_bwd_part_nhwc": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P, Z, P]),
     "mvae_group_norm_workspace_bytes": (Z, [I, I, I]),
     "mvae_reparam_fwd": (I, [P, P, L, P, P, L, I, P]),
     "mvae_reparam_bwd": (I, [P, P, P, L, P, L, I, P]),

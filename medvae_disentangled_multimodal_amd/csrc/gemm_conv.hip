@@ -29,9 +29,17 @@ extern "C" {
 //   mode 2: transposed gather: y[oh] += x[(oh + pad - r)/stride] * w[r] (dgrad of a strided conv;
 //           stride must be a power of two)
 // y[n][ho][wo][cout] = sum + bias[cout] + residual[n][ho][wo][cout]
+// GroupNorm backward link of an input-gradient conv (GemmArgs::gnb_part): the conv's input was
+// silu?(GroupNorm(x)) with these saved statistics and affine parameters
+struct GnBwdLink {
+  const float* x;
+  const float *mean, *rstd, *gamma, *beta;
+  int groups, silu;
+  double* part;
+};
 static int conv2d_impl(const float* x, const float* w, const float* bias, const float* residual, float* y, int nb,
                        int h, int wd, int cin, int cout, int kh, int kw, int stride, int pad_t, int pad_l, int ho,
-                       int wo, int mode, double* gn_part, void* stream);
+                       int wo, int mode, double* gn_part, void* stream, const GnBwdLink* gnb = nullptr);
 
 int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const float* residual,
                      float* y, int nb, int h, int wd, int cin, int cout, int kh, int kw,
@@ -55,11 +63,36 @@ int mvae_conv2d_gnstats_nhwc(const float* x, const float* w, const float* bias, 
                      gn_part, stream);
 }
 
+// Input gradient of a stride-1 conv (mode 2 of mvae_conv2d_nhwc: dy [nb][ho][wo][cout] -> dx [nb][h][wd][cin],
+// wt = [cin][kh][kw][cout]) whose input was y = silu?(GroupNorm(gn_x)) (ResnetBlock norm1/norm2 -> conv,
+// encoder_decoder.py:141-163; norm_out -> conv_out): the epilogue also emits the GroupNorm backward partials
+// part = [nb*h*wd/32][cin][2] fp64 {sum dyn, sum dyn*xhat} (dyn = dx * silu'(.)) for
+// mvae_group_norm_bwd_part_nhwc. No dropout between the GroupNorm and the conv. Needs h*wd % 32 == 0,
+// (cin / groups) % 4 == 0, 16-B aligned dx and gn_x.
+int mvae_conv2d_dgrad_gnbwd_nhwc(const float* dy, const float* wt, float* dx, int nb, int ho, int wo, int cout,
+                                 int cin, int kh, int kw, int pad_t, int pad_l, int h, int wd, int w_split,
+                                 const float* gn_x, const float* mean, const float* rstd, const float* gamma,
+                                 const float* beta, int groups, int silu, double* part, void* stream) {
+  if (part == nullptr || gn_x == nullptr || mean == nullptr || rstd == nullptr || gamma == nullptr ||
+      beta == nullptr || groups <= 0 || cin % groups || (cin / groups) % 4 || (h * wd) % 32 || !al16(dx) ||
+      !al16(gn_x) || vec_epi_disabled()) {
+    set_error("conv2d_dgrad_gnbwd: needs h*w %% 32 == 0, channels per group %% 4 == 0, 16-B aligned dx / x");
+    return MVAE_EINVAL;
+  }
+  if (cout % 4 || !al16(dy) || !al16(wt)) {
+    set_error("conv2d_dgrad_gnbwd: needs the vector (16-B) operand path (cout %% 4 == 0, aligned dy / wt)");
+    return MVAE_EINVAL;
+  }
+  const GnBwdLink link{gn_x, mean, rstd, gamma, beta, groups, silu, part};
+  return conv2d_impl(dy, wt, nullptr, nullptr, dx, nb, ho, wo, cout, cin, kh, kw, 1, pad_t, pad_l, h, wd,
+                     2 | (w_split ? MVAE_CONV_WSPLIT : 0), nullptr, stream, &link);
+}
+
 }  // extern "C"
 
 static int conv2d_impl(const float* x, const float* w, const float* bias, const float* residual, float* y, int nb,
                        int h, int wd, int cin, int cout, int kh, int kw, int stride, int pad_t, int pad_l, int ho,
-                       int wo, int mode, double* gn_part, void* stream) {
+                       int wo, int mode, double* gn_part, void* stream, const GnBwdLink* gnb) {
   const bool presplit = (mode & MVAE_CONV_WSPLIT) != 0;
   const bool xsplit = (mode & MVAE_CONV_XSPLIT) != 0;
   mode &= ~(MVAE_CONV_WSPLIT | MVAE_CONV_XSPLIT);
@@ -101,8 +134,17 @@ static int conv2d_impl(const float* x, const float* w, const float* bias, const 
     set_gather_magic(a);
     a.stride = stride; a.stride_shift = shift; a.pad_t = pad_t; a.pad_l = pad_l;
     a.gn_part = gn_part ? gn_part + (long long)b0 * (ho * wo / 32) * (cout / 4) * 2 : nullptr;
+    if (gnb) {
+      const int hw = ho * wo;
+      a.gnb_part = gnb->part + (long long)b0 * (hw / 32) * cout * 2;
+      a.gnb_x = gnb->x + (long long)b0 * (out_img / 4);
+      a.gnb_mean = gnb->mean + (long long)b0 * gnb->groups;
+      a.gnb_rstd = gnb->rstd + (long long)b0 * gnb->groups;
+      a.gnb_gamma = gnb->gamma; a.gnb_beta = gnb->beta;
+      a.gnb_hw = hw; a.gnb_G = gnb->groups; a.gnb_cpg = cout / gnb->groups; a.gnb_silu = gnb->silu;
+    }
     const int cfg = choose_tile(a, v, false);
-    if (gn_part && !v) {
+    if ((gn_part || gnb) && !v) {
       set_error("conv2d_gnstats: needs the vector (16-B) operand path");
       return MVAE_EINVAL;
     }

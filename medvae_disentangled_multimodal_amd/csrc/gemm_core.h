@@ -114,6 +114,15 @@ struct GemmArgs {
   // GroupNorm statistics of the output for the following Normalize (16-B epilogue only): per 32-row block
   // and 4-channel group, {sum y, sum y^2} in fp64 at gn_part[((row/32) * (N/4) + col/4) * 2]
   double* gn_part = nullptr;
+  // GroupNorm BACKWARD partials (16-B epilogue only): when C is the input gradient of a conv whose input was
+  // y = silu?(GroupNorm(x)), emit per 32-row block and channel {sum dyn, sum dyn * xhat} (fp64) at
+  // gnb_part[((row/32) * N + col) * 2], dyn = C * silu'(.) -- the sums the GroupNorm backward would
+  // otherwise re-read C and x for (norm.hip gn_partial_kernel<1>, no dropout). x is [M][N] like C.
+  double* gnb_part = nullptr;
+  const float* gnb_x = nullptr;
+  const float *gnb_mean = nullptr, *gnb_rstd = nullptr;  // [nb * G]
+  const float *gnb_gamma = nullptr, *gnb_beta = nullptr;  // [N]
+  int gnb_hw = 1, gnb_cpg = 1, gnb_G = 1, gnb_silu = 0;
 };
 
 // full-resolution pixel of class-grid pixel m (see GemmArgs::sub_w2)
@@ -887,6 +896,45 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 #pragma unroll
       for (int q = 0; q < NSB; ++q) st0[q] = st1[q] = 0.0;
       const bool want_stats = a.gn_part != nullptr;
+      // GroupNorm backward partials (GemmArgs::gnb_part): per-channel, per 32-row block; a pass holds whole
+      // blocks when HR >= 32 (flushed per pass), else one block spans both passes (flushed at the end)
+      const bool want_gnb = a.gnb_part != nullptr;
+      constexpr int QP = HR >= 32 ? HR / 32 : 1;
+      double gs0[QP][4], gs1[QP][4];
+      float ggm[4] = {0.f, 0.f, 0.f, 0.f}, gbt[4] = {0.f, 0.f, 0.f, 0.f};
+      const __amdgpu_buffer_rsrc_t xr = make_rsrc(want_gnb ? a.gnb_x + bidx * a.sC : a.C, want_gnb ? a.c_bytes : 0u);
+      if (want_gnb && col < a.N) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ggm[e] = a.gnb_gamma[col + e];
+          gbt[e] = a.gnb_beta[col + e];
+        }
+      }
+      auto gnb_reset = [&]() {
+#pragma unroll
+        for (int q = 0; q < QP; ++q)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) gs0[q][e] = gs1[q][e] = 0.0;
+      };
+      auto gnb_flush = [&](int q, int row0) {  // fixed xor-tree over the RPI row lanes of one column group
+        double s0[4], s1[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s0[e] = gs0[q][e];
+          s1[e] = gs1[q][e];
+#pragma unroll
+          for (int o = C4; o < 64; o <<= 1) {
+            s0[e] += __shfl_xor(s0[e], o, 64);
+            s1[e] += __shfl_xor(s1[e], o, 64);
+          }
+        }
+        if (rsub == 0 && row0 < a.M && col < a.N) {
+          double* gp = a.gnb_part + ((long long)(row0 >> 5) * a.N + col) * 2;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) *(double2*)(gp + 2 * e) = double2{s0[e], s1[e]};
+        }
+      };
+      gnb_reset();
       __syncthreads();  // every wave's last fragment reads are done: the LDS is free
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
@@ -920,6 +968,31 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
             st0[q] += ((double)v.x + (double)v.y) + ((double)v.z + (double)v.w);
             st1[q] += ((double)v.x * v.x + (double)v.y * v.y) + ((double)v.z * v.z + (double)v.w * v.w);
           }
+          if (want_gnb && ok) {  // same float arithmetic as gn_partial_kernel<1>
+            const int q = HR >= 32 ? (k * RPI) / 32 : 0;
+            const float4 x4 = bload4(xr, co);
+            const int bg = (row / a.gnb_hw) * a.gnb_G + col / a.gnb_cpg;
+            const float mu = a.gnb_mean[bg], rs = a.gnb_rstd[bg];
+            const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+            const float vs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float d = vs[e];
+              const float xh = (xs[e] - mu) * rs;
+              if (a.gnb_silu) {
+                const float yn = xh * ggm[e] + gbt[e];
+                const float sg = sigmoid_f(yn);
+                d = d * sg * (1.f + yn * (1.f - sg));
+              }
+              gs0[q][e] += d;
+              gs1[q][e] += (double)d * xh;
+            }
+          }
+        }
+        if (want_gnb && (HR >= 32 || pass == 1)) {
+#pragma unroll
+          for (int q = 0; q < QP; ++q) gnb_flush(q, m0 + arow + (HR >= 32 ? pass * HR + q * 32 : 0));
+          gnb_reset();
         }
         __syncthreads();
       }

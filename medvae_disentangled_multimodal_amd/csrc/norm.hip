@@ -529,6 +529,46 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
   return launch_status();
 }
 
+// Backward from the partials emitted by the input-gradient conv that consumed this GroupNorm's output
+// (mvae_conv2d_dgrad_gnbwd_nhwc, part = [nb*hw/32][c][2] fp64 {sum dyn, sum dyn*xhat}): no partial pass over
+// x and dy. No dropout (the fused conv epilogue does not apply a mask).
+int mvae_group_norm_bwd_part_nhwc(const float* x, const float* dy, const double* part, const float* gamma,
+                                  const float* beta, const float* mean, const float* rstd, float* dx,
+                                  const float* dx_add, float* dgamma, float* dbeta, int nb, int hw, int c, int groups,
+                                  int silu, void* workspace, size_t workspace_bytes, void* stream) {
+  if (nb <= 0 || hw <= 0 || c <= 0 || (c & 3) || groups <= 0 || c % groups || hw % 32 || part == nullptr) {
+    set_error("group_norm_bwd_part: needs hw %% 32 == 0 and C %% 4 == 0");
+    return MVAE_EINVAL;
+  }
+  if (workspace_bytes < mvae_group_norm_workspace_bytes(nb, hw, c)) {
+    set_error("group_norm_bwd_part: workspace too small");
+    return MVAE_EWORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  GnArgs a{};
+  a.x = x; a.dy = dy; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta; a.dx_add = dx_add;
+  a.nb = nb; a.hw = hw; a.C = c; a.G = groups; a.silu = silu; a.drop_p = 0.f; a.seed = 0;
+  a.chunks = gn_chunks(nb, hw);
+  a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
+  float* k1 = (float*)((char*)workspace + (size_t)nb * a.chunks * c * 2 * sizeof(double));
+  float* k2 = k1 + (size_t)nb * c;
+  float* k3 = k2 + (size_t)nb * c;
+  GnArgs ap = a;  // the reductions run over the conv's 32-row blocks
+  ap.ws = const_cast<double*>(part);
+  ap.chunks = hw / 32;
+  ap.rows_per_chunk = 32;
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(cdiv((long long)nb * groups, 4)), dim3(256), 0, st, ap, k1,
+                     k2, k3);
+  if (dgamma || dbeta) {
+    double* pg = (double*)(((uintptr_t)(k3 + (size_t)nb * c) + 255) & ~(uintptr_t)255);
+    hipLaunchKernelGGL(gn_param_grad_kernel, dim3(cdiv(c, 64), GN_PG_SLICES), dim3(256), 0, st, ap, pg);
+    hipLaunchKernelGGL(gn_param_final_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st, c, (const double*)pg, dgamma,
+                       dbeta);
+  }
+  hipLaunchKernelGGL(gn_dx_kernel, dim3(a.chunks, nb), dim3(256), 0, st, a, k1, k2, k3, dx);
+  return launch_status();
+}
+
 }  // extern "C"
 
 // ------------------------------------------------------------------------------------------

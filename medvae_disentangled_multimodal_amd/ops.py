@@ -223,7 +223,9 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
     return y
 
 
-def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom):
+def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None):
+    """gn_link (GnBwdLink): the conv's input was silu?(GroupNorm(x)) -- also emit that GroupNorm's backward
+    partials from the GEMM epilogue (mvae_conv2d_dgrad_gnbwd_nhwc) into gn_link.part when the launch allows it."""
     n, c, h, wd = x_shape
     co = w.shape[0]
     _, _, ho, wo = dy.shape
@@ -231,6 +233,19 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom):
     st = _stream(dy)
     flops = 2.0 * n * ho * wo * co * c * g.kh * g.kw  # reference count
     shp = (n, c, h, wd, co, g.kh, g.stride, g.upsample)
+    if gn_link is not None and gn_link.usable(dx) and not g.pointwise and not g.upsample and g.stride == 1 and \
+            co % 4 == 0 and _al16(dy, dx):
+        split = WEIGHT_SPLIT
+        wt = ARENA.get("wt", c * g.kh * g.kw * co * 4, dy.device)
+        _lib.call("mvae_conv_weight_transpose", w.data_ptr(), wt.data_ptr(), co, g.kh, g.kw, c, int(split), st)
+        part = torch.empty(n * h * wd // 32 * c * 2, device=dy.device, dtype=torch.float64)
+        L = gn_link
+        with _timed("conv_dgrad", flops, shp):
+            _lib.call("mvae_conv2d_dgrad_gnbwd_nhwc", dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, ho, wo, co, c,
+                      g.kh, g.kw, g.pad_t, g.pad_l, h, wd, int(split), L.x.data_ptr(), L.mean.data_ptr(),
+                      L.rstd.data_ptr(), L.gamma.data_ptr(), L.beta.data_ptr(), L.groups, L.silu, part.data_ptr(), st)
+        L.part, L.dx = part, dx
+        return dx
     if g.pointwise:
         # dx[m][c] = sum_n dy[m][n] W[n][c]  (W stored [K=cout][N=cin])
         with _timed("conv_dgrad", flops, shp):
@@ -345,7 +360,8 @@ class GradSink:
 
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, geom: ConvGeom, res_sink=None, x_sink=None, gn_part=None):
+    def forward(ctx, x, weight, bias, residual, geom: ConvGeom, res_sink=None, x_sink=None, gn_part=None,
+                gn_link=None):
         _check(x, "conv input")
         xs = bool(getattr(x, XSPLIT_ATTR, False))
         if xs and not x.is_contiguous(memory_format=CL):
@@ -362,6 +378,7 @@ class Conv2dFn(torch.autograd.Function):
         ctx.weight_ref = weight
         ctx.bias_ref = bias
         ctx.res_sink, ctx.x_sink = res_sink, x_sink
+        ctx.gn_link = gn_link
         return y
 
     @staticmethod
@@ -370,8 +387,11 @@ class Conv2dFn(torch.autograd.Function):
         g = ctx.geom
         dy = nhwc(dy)
         dx = dw_ret = db_ret = dres = None
+        link = ctx.gn_link
+        if link is not None:
+            link.part = link.dx = None  # partials of an earlier pass are never reused
         if ctx.needs_input_grad[0]:
-            dx = conv2d_dgrad_raw(dy, w, x.shape, g)
+            dx = conv2d_dgrad_raw(dy, w, x.shape, g, link if ctx.x_sink is None else None)
             if ctx.x_sink is not None and ctx.x_sink.park(dx):
                 dx = None
         bias_done = False
@@ -403,7 +423,7 @@ class Conv2dFn(torch.autograd.Function):
             _grad_done(ctx.weight_ref)
         if want_b and db_ret is None:
             _grad_done(ctx.bias_ref)
-        return dx, dw_ret, db_ret, dres, None, None, None, None
+        return dx, dw_ret, db_ret, dres, None, None, None, None, None
 
 
 # The GroupNorm statistics of a conv output emitted by its GEMM epilogue travel with the output tensor
@@ -423,7 +443,10 @@ def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink
         if (ho * wo) % 32 == 0 and co % 4 == 0 and _al16(x, weight) and (bias is None or _al16(bias)) and (
                 residual is None or _al16(residual)):
             part = torch.empty(n * ho * wo // 32 * (co // 4) * 2, device=x.device, dtype=torch.float64)
-    y = Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink, part)
+    link = getattr(x, GN_BWD_ATTR, None)
+    if link is not None and not link.matches(x):
+        link = None
+    y = Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink, part, link)
     if part is not None:
         setattr(y, GN_PART_ATTR, (part, y._version))
     return y
@@ -432,10 +455,46 @@ def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink
 # ------------------------------------------------------------------------------------------
 # GroupNorm (+SiLU, +dropout)
 # ------------------------------------------------------------------------------------------
+# A GroupNorm output that feeds exactly one convolution carries a GnBwdLink: the conv's input-gradient GEMM
+# emits the GroupNorm backward partials from its epilogue (mvae_conv2d_dgrad_gnbwd_nhwc) and the GroupNorm
+# backward then skips its reduction pass over x and dy (mvae_group_norm_bwd_part_nhwc).
+GN_BWD_ATTR = "_mvae_gn_bwd_link"
+GN_BWD_FUSED = os.environ.get("MVAE_NO_GN_BWD_FUSED") is None and os.environ.get("MVAE_NO_VEC_EPI") is None
+
+
+class GnBwdLink:
+    __slots__ = ("x", "gamma", "beta", "mean", "rstd", "groups", "silu", "y_ref", "y_version", "part", "dx")
+
+    def __init__(self, groups: int, silu: bool):
+        self.groups, self.silu = groups, int(silu)
+        self.x = self.gamma = self.beta = self.mean = self.rstd = None
+        self.y_ref = self.y_version = self.part = self.dx = None
+
+    def bind_output(self, y):
+        self.y_ref, self.y_version = y.data_ptr(), y._version
+
+    def matches(self, x) -> bool:  # the conv input is still the GroupNorm's untouched output
+        return self.x is not None and x.data_ptr() == self.y_ref and x._version == self.y_version
+
+    def usable(self, dx) -> bool:
+        n, c, h, w = dx.shape
+        return (self.x is not None and tuple(self.x.shape) == (n, c, h, w) and (h * w) % 32 == 0 and
+                c % self.groups == 0 and (c // self.groups) % 4 == 0 and _al16(self.x))
+
+    def take(self, dy):
+        """The emitted partials, if they were computed from exactly this gradient tensor."""
+        part, dx = self.part, self.dx
+        self.part = self.dx = None
+        if part is None or dx is None or dy.data_ptr() != dx.data_ptr() or dy.shape != dx.shape or \
+                not dy.is_contiguous(memory_format=CL):
+            return None
+        return part
+
+
 class GroupNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool, drop_p: float, seed: int,
-                y_split: bool = False, grad_sink=None, part=None):
+                y_split: bool = False, grad_sink=None, part=None, link=None):
         _check(x, "group_norm input")
         x = nhwc(x)
         n, c, h, w = x.shape
@@ -458,6 +517,9 @@ class GroupNormFn(torch.autograd.Function):
         ctx.cfg = (groups, int(silu), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF)
         ctx.gamma_ref, ctx.beta_ref = gamma, beta
         ctx.grad_sink = grad_sink
+        ctx.link = link
+        if link is not None:
+            link.x, link.gamma, link.beta, link.mean, link.rstd = x, gamma, beta, mean, rstd
         return y
 
     @staticmethod
@@ -481,15 +543,22 @@ class GroupNormFn(torch.autograd.Function):
             add = nhwc(add)
             if add.shape != x.shape or add.dtype != torch.float32:
                 raise RuntimeError("group_norm backward: parked branch gradient has the wrong shape")
+        gpart = ctx.link.take(dy) if ctx.link is not None and drop_p == 0.0 else None
         with _timed("gn_bwd", 12.0 * x.numel(), (n, c, h * w)):  # algorithmic HBM bytes: read x, dy; write dx
-            _lib.call("mvae_group_norm_bwd_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
-                      mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(add), _ptr(dg), _ptr(db), n, h * w, c,
-                      groups, silu, drop_p, seed, ws.data_ptr(), ws.numel(), _stream(x))
+            if gpart is not None:  # reduction half emitted by the consuming conv's input-gradient GEMM
+                _lib.call("mvae_group_norm_bwd_part_nhwc", x.data_ptr(), dy.data_ptr(), gpart.data_ptr(),
+                          gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                          _ptr(add), _ptr(dg), _ptr(db), n, h * w, c, groups, silu, ws.data_ptr(), ws.numel(),
+                          _stream(x))
+            else:
+                _lib.call("mvae_group_norm_bwd_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                          mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(add), _ptr(dg), _ptr(db), n, h * w,
+                          c, groups, silu, drop_p, seed, ws.data_ptr(), ws.numel(), _stream(x))
         if ctx.needs_input_grad[1] and dg_ret is None:
             _grad_done(ctx.gamma_ref)
         if ctx.needs_input_grad[2] and db_ret is None:
             _grad_done(ctx.beta_ref)
-        return dx, dg_ret, db_ret, None, None, None, None, None, None, None, None
+        return dx, dg_ret, db_ret, None, None, None, None, None, None, None, None, None
 
 
 # Activations handed to a convolution in the pre-split 3xBF16 operand layout carry this attribute
@@ -510,9 +579,13 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
         ok = part[1] == x._version and (h * w) % 32 == 0 and (x.shape[1] // groups) % 4 == 0 and \
             x.shape[1] % groups == 0 and x.is_contiguous(memory_format=CL)
         part = part[0] if ok else None
-    y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink, part)
+    link = GnBwdLink(groups, silu) if (for_conv and GN_BWD_FUSED and drop_p == 0.0 and x.requires_grad) else None
+    y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink, part, link)
     if split:
         setattr(y, XSPLIT_ATTR, True)
+    if link is not None:
+        link.bind_output(y)
+        setattr(y, GN_BWD_ATTR, link)
     return y
 
 

@@ -409,3 +409,63 @@ def test_conv_epilogue_groupnorm_statistics(dev, n, c, co, h, res):
     y2.mul_(2.0)  # stale statistics must not be used
     assert rel(ops.group_norm(y2, gam, bet, 32, 1e-6, True),
                F.silu(F.group_norm(y2.double().cpu(), 32, gam.double().cpu(), bet.double().cpu(), eps=1e-6))) < 1e-5
+
+
+@pytest.mark.parametrize("n,c,co,h,silu", [(4, 64, 128, 16, True), (8, 256, 64, 8, True), (2, 128, 32, 32, False),
+                                           (16, 256, 256, 32, True)])
+def test_groupnorm_backward_partials_from_conv_dgrad(dev, n, c, co, h, silu):
+    """GroupNorm(+SiLU) -> conv: the conv's input-gradient GEMM emits the GroupNorm backward partials
+    (mvae_conv2d_dgrad_gnbwd_nhwc) and the GroupNorm backward skips its reduction pass
+    (mvae_group_norm_bwd_part_nhwc). dx / dgamma / dbeta / dW equal the unfused path (1e-5) and float64
+    torch autograd (1e-4); the fused kernels actually ran (the link's partials were consumed)."""
+    from medvae_disentangled_multimodal_amd import ops
+    g = torch.Generator().manual_seed(11 + c)
+    x0 = torch.randn(n, c, h, h, generator=g) * 1.5 + 0.3
+    gam0 = torch.rand(c, generator=g) + 0.5
+    bet0 = torch.randn(c, generator=g) * 0.1
+    w0 = torch.randn(co, c, 3, 3, generator=g) / math.sqrt(9 * c)
+    gy = torch.randn(n, co, h, h, generator=g)
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1)
+
+    def run(fused):
+        prev = ops.GN_BWD_FUSED
+        ops.GN_BWD_FUSED = fused
+        try:
+            x = cl(x0, dev).requires_grad_()
+            gam, bet = gam0.to(dev).requires_grad_(), bet0.to(dev).requires_grad_()
+            w = cl(w0, dev).requires_grad_()
+            y = ops.group_norm(x, gam, bet, 32, 1e-6, silu, for_conv=True)
+            link = getattr(y, ops.GN_BWD_ATTR, None)
+            assert (link is not None) == fused
+            out = ops.conv2d(y, w, None, geom)
+            seen = []
+            if fused:
+                orig = ops._lib.call
+
+                def spy(name, *args):
+                    seen.append(name)
+                    return orig(name, *args)
+                ops._lib.call = spy
+            try:
+                out.backward(cl(gy, dev))
+            finally:
+                if fused:
+                    ops._lib.call = orig
+            if fused:
+                assert "mvae_conv2d_dgrad_gnbwd_nhwc" in seen and "mvae_group_norm_bwd_part_nhwc" in seen
+                assert "mvae_group_norm_bwd_nhwc" not in seen
+            return x.grad, gam.grad, bet.grad, w.grad
+        finally:
+            ops.GN_BWD_FUSED = prev
+
+    fz, un = run(True), run(False)
+    for a, b in zip(fz, un):
+        assert rel(a, b) < 1e-5
+    xr = x0.double().requires_grad_()
+    gr, br, wr = gam0.double().requires_grad_(), bet0.double().requires_grad_(), w0.double().requires_grad_()
+    yr = F.group_norm(xr, 32, gr, br, eps=1e-6)
+    if silu:
+        yr = F.silu(yr)
+    F.conv2d(yr, wr, None, 1, 1).backward(gy.double())
+    for a, b in zip(fz, (xr.grad, gr.grad, br.grad, wr.grad)):
+        assert rel(a, b) < 1e-4
