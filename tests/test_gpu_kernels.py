@@ -411,14 +411,22 @@ def test_conv_epilogue_groupnorm_statistics(dev, n, c, co, h, res):
                F.silu(F.group_norm(y2.double().cpu(), 32, gam.double().cpu(), bet.double().cpu(), eps=1e-6))) < 1e-5
 
 
-@pytest.mark.parametrize("n,c,co,h,silu", [(4, 64, 128, 16, True), (8, 256, 64, 8, True), (2, 128, 32, 32, False),
-                                           (16, 256, 256, 32, True)])
+@pytest.mark.parametrize("n,c,co,h,silu", [
+    (4, 64, 128, 16, True),     # 2 channels per group: not eligible, the two-pass backward must run
+    (8, 256, 64, 8, True), (2, 128, 32, 32, False), (16, 256, 256, 32, True),
+    (2, 256, 256, 64, True),    # c4 level 0 (64x64, C=256)
+    (2, 512, 512, 32, True),    # c4 level 1
+    (2, 1024, 1024, 16, True),  # c4 level 2
+    (2, 2048, 2048, 8, True),   # c4 level 3 / mid
+    (4, 128, 128, 28, True),    # c2 level 0 (28x28: 784 % 32 == 16, not eligible)
+])
 def test_groupnorm_backward_partials_from_conv_dgrad(dev, n, c, co, h, silu):
     """GroupNorm(+SiLU) -> conv: the conv's input-gradient GEMM emits the GroupNorm backward partials
     (mvae_conv2d_dgrad_gnbwd_nhwc) and the GroupNorm backward skips its reduction pass
-    (mvae_group_norm_bwd_part_nhwc). dx / dgamma / dbeta / dW equal the unfused path (1e-5) and float64
-    torch autograd (1e-4); the fused kernels actually ran (the link's partials were consumed)."""
+    (mvae_group_norm_bwd_part_nhwc) -- exactly when the shape is eligible (H*W % 32 == 0 and C/G % 4 == 0).
+    dx / dgamma / dbeta / dW equal the unfused path (1e-5) and float64 torch autograd (1e-4)."""
     from medvae_disentangled_multimodal_amd import ops
+    eligible = (h * h) % 32 == 0 and (c // 32) % 4 == 0
     g = torch.Generator().manual_seed(11 + c)
     x0 = torch.randn(n, c, h, h, generator=g) * 1.5 + 0.3
     gam0 = torch.rand(c, generator=g) + 0.5
@@ -451,9 +459,12 @@ def test_groupnorm_backward_partials_from_conv_dgrad(dev, n, c, co, h, silu):
             finally:
                 if fused:
                     ops._lib.call = orig
-            if fused:
+            if fused and eligible:
                 assert "mvae_conv2d_dgrad_gnbwd_nhwc" in seen and "mvae_group_norm_bwd_part_nhwc" in seen
                 assert "mvae_group_norm_bwd_nhwc" not in seen
+            elif fused:
+                assert "mvae_conv2d_dgrad_gnbwd_nhwc" not in seen and "mvae_group_norm_bwd_part_nhwc" not in seen
+                assert "mvae_group_norm_bwd_nhwc" in seen
             return x.grad, gam.grad, bet.grad, w.grad
         finally:
             ops.GN_BWD_FUSED = prev
