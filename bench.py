@@ -8,8 +8,10 @@ AdamW lr 1e-4 betas (0.5, 0.999) wd 1e-5, gradient clip 1.0 -- configs/training/
 forward + VAE loss + backward + [gradient all-reduce] + non-finite zeroing + clip + AdamW.
 Synthetic MedMNIST-shaped data resident in HBM (x = randint(0,256)/255*2-1, random one-hot of 12).
 
-    python bench.py [--gpus N --steps K --warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL all-reduce)
+    python bench.py [--gpus N --steps K --warmup W --config c4|c5|c2|c3]
+        N > 1 without a launcher: bench.py spawns N rank processes itself (before anything touches
+        the GPU), one per GPU, RCCL ("nccl") process group over 127.0.0.1
+    torchrun --nproc-per-node N bench.py --gpus N ...   (the same, launched externally)
 
 Rank 0 prints ONE JSON line (value = images/s over all ranks, max-over-ranks timing), with
   roofline:     the implicit-GEMM MFMA kernel family, live HIP-event timing of every launch in one
@@ -23,6 +25,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -52,12 +56,23 @@ CONFIGS = {
                loss=dict(type="lpips_discriminator", perceptual_factor=1.0, kl_factor=1e-5,
                          discriminator_iter_start=10000, allow_synthetic_lpips=True, lpips_net="vgg")),
     # BASELINE config 2: path_beta_vae at 28x28x3 with the 3-level ch_mult, bs 256
-    "c2": dict(cls="BetaVAE", res=28, batch=256,
+    "c2": dict(cls="BetaVAE", res=28, batch=256, cpu_batch=16,
                kwargs=dict(input_channels=3, latent_dim=128, hidden_channels=128, ch_mult=(1, 2, 4),
                            num_res_blocks=2, attn_resolutions=[16], dropout=0.0, resolution=28, beta=6.0),
                opt=dict(type="adamw", lr=1e-4, weight_decay=1e-4, betas=[0.9, 0.999]), clip=1.0,
                loss=dict(type="vae", recon_loss_type="mse", kl_weight=6.0, recon_weight=1.0)),
+    # BASELINE config 3: disentangled_multi_modal_cvae_quick (configs/model/disentangled_conditional_vae_quick.yaml,
+    # configs/experiment/disentangled_multi_modal_cvae_quick.yaml: Adam lr 5e-4, clip 0.5, dropout 0.1), bs 512,
+    # a mixed batch of the 5 modalities (1-channel images zero-padded to 3 by the collate)
+    "c3": dict(cls="DisentangledConditionalVAE", res=28, batch=512, cpu_batch=512,
+               kwargs=dict(num_modalities=5, shared_latent_dim=8, modality_latent_dim=8, hidden_channels=32,
+                           ch_mult=(1, 2, 4), num_res_blocks=1, attn_resolutions=[], dropout=0.1, resolution=28,
+                           modality_separation_weight=0.1, contrastive_weight=0.05),
+               opt=dict(type="adam", lr=5e-4, weight_decay=0.0, betas=[0.9, 0.999]), clip=0.5,
+               loss=dict(type="disentangled_vae", recon_loss_type="mse", kl_weight=1.0, recon_weight=1.0,
+                         separation_weight=0.1, contrastive_weight=0.05)),
 }
+METRIC_C4 = "training images/sec (whole node) + ELBO parity, multimodal CVAE 64\u00d764 bs=256"
 
 BF16_DENSE_PEAK_TF = 2500.0
 PEAK_3XBF16_TF = BF16_DENSE_PEAK_TF / 3.0
@@ -81,9 +96,16 @@ def _pmc_traffic(config):
 
 def make_batch(cfg, device, gen):
     B, r = cfg["batch"], cfg["res"]
-    C = cfg["kwargs"]["input_channels"]
+    C = cfg["kwargs"].get("input_channels", 3)
     x = torch.randint(0, 256, (B, C, r, r), generator=gen, device=device).float() / 255 * 2 - 1
     labels = torch.zeros(B, 1, dtype=torch.long, device=device)
+    if cfg["cls"] == "DisentangledConditionalVAE":
+        # modality ids 0..4 (medmnist_data.py:138-152); gray modalities 0 / 3 zero-padded to 3 channels (:16-72)
+        idx = torch.randint(0, 5, (B,), generator=gen, device=device)
+        gray = (idx == 0) | (idx == 3)
+        x[:, 1:] = torch.where(gray.view(B, 1, 1, 1), torch.zeros_like(x[:, 1:]), x[:, 1:])
+        oh = torch.nn.functional.one_hot(idx, 12).float()
+        return (x, labels, oh, idx)
     if cfg["cls"] == "ConditionalVAE":
         idx = torch.randint(0, 12, (B,), generator=gen, device=device)
         oh = torch.nn.functional.one_hot(idx, 12).float()
@@ -93,17 +115,21 @@ def make_batch(cfg, device, gen):
 
 def cpu_baseline(cfg, seconds_budget=20.0):
     """Time the CPU oracle (oracle/torch_ref.py: the reference algorithm, pinned by the golden tests)
-    on a bounded sample: one training step (fwd+loss+bwd+clip+AdamW) at batch 2."""
+    on a bounded sample: training steps (fwd+loss+bwd+clip+Adam/AdamW) at the config's `cpu_batch`
+    (default 2) on the host's torch threads."""
     from oracle import torch_ref as R
     threads = torch.get_num_threads()
     a = R.make_arch(cfg["cls"], dict(cfg["kwargs"]))
     g = torch.Generator().manual_seed(0)
     P = {k: torch.randn(s, generator=g) * 0.02 for k, s in R.param_shapes(a)}
-    bs = 2
+    bs = cfg.get("cpu_batch", 2)
     x = torch.randint(0, 256, (bs, a.input_channels, a.resolution, a.resolution), generator=g).float() / 255 * 2 - 1
     cond = None
     if a.cls == "ConditionalVAE":
         cond = torch.nn.functional.one_hot(torch.randint(0, 12, (bs,), generator=g), 12).float()
+    elif a.cls == "DisentangledConditionalVAE":
+        cond = torch.randint(0, 5, (bs,), generator=g)
+        x[:, 1:] = torch.where(((cond == 0) | (cond == 3)).view(bs, 1, 1, 1), torch.zeros_like(x[:, 1:]), x[:, 1:])
     eps = torch.randn(bs, a.latent_dim, a.enc_res, a.enc_res, generator=g)
     t0 = time.perf_counter()
     steps = 0
@@ -113,9 +139,45 @@ def cpu_baseline(cfg, seconds_budget=20.0):
         if time.perf_counter() - t0 > seconds_budget / 2 or steps >= 3:
             break
     dt = (time.perf_counter() - t0) / steps
-    return {"value": round(bs / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+    return {"value": round(bs / dt, 4), "unit": "images/s", "cores": threads, "host_nproc": os.cpu_count(),
+            "kind": "port",
             "sample": f"{steps} oracle training step(s) at batch {bs} of the same model (fp32, CPU), "
                       f"{dt:.2f} s/step"}
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, cmd=None) -> int:
+    """`bench.py --gpus N` without an external launcher: start N rank processes of this script (fresh
+    interpreters -- this parent never touches the GPU), one per GPU, with torchrun's environment
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT). Rank 0 prints the JSON line.
+    Returns the first non-zero child exit code (the other ranks are then stopped)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen(cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            c = p.poll()
+            if c is None:
+                continue
+            pending.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
 
 
 def main():
@@ -129,6 +191,12 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--detail", action="store_true", help="per-shape GEMM launch timings on stderr")
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
 
     import medvae_disentangled_multimodal_amd as M
     from medvae_disentangled_multimodal_amd import ddp, ops
@@ -238,22 +306,23 @@ def main():
                                 "GB/s": round(v[1] / (v[2] * 1e-3) / 1e9, 1)} for k, v in hb.items()}}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg["loss"]["type"] == "vae":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg["loss"]["type"] in ("vae", "disentangled_vae"):
         cpu = cpu_baseline(cfg)
 
     if rank == 0:
         imgs = cfg["batch"] * world * args.steps
-        out = {"metric": "training images/sec (whole node), multimodal CVAE 64x64 bs=256/GPU"
-               if args.config == "c4" else f"training images/sec, config {args.config}",
+        out = {"metric": METRIC_C4 if args.config == "c4" else
+               f"training images/sec (whole node), config {args.config}",
                "value": round(imgs / dt, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": ("bf16 (bf16-mixed: bf16 MFMA operands, fp32 accumulate/activations)" if bf16
                                                      else "fp32 (3xBF16 MFMA, fp32 accumulate)"),
                "data": "synthetic (MedMNIST-shaped, resident in HBM; random-init weights)",
-               "config": {"workload": f"{cfg['cls']} {cfg['res']}x{cfg['res']}x{cfg['kwargs']['input_channels']} "
+               "config": {"workload": f"{cfg['cls']} {cfg['res']}x{cfg['res']}x{cfg['kwargs'].get('input_channels', 3)} "
                                       f"train step (fwd+loss+bwd+clip+AdamW)", "model": cfg["cls"],
                           "params": nparams, "global_batch": cfg["batch"] * world, "per_gpu_batch": cfg["batch"],
-                          "resolution": cfg["res"], "parallelism": f"dp{world}"},
+                          "resolution": cfg["res"], "parallelism": f"dp{world}", "rccl_world_size": world,
+                          "backend": dist.get_backend() if world > 1 else None},
                "loss": round(loss_v, 6), "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -126,6 +126,14 @@ class DataParallel:
         g = self.module.flat.grad[lo:hi]
         self._works.append(dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
+    def any_across_ranks(self, flags: torch.Tensor) -> torch.Tensor:
+        """Element-wise OR of a small bool vector over all ranks (same call order on every rank)."""
+        if self.world == 1:
+            return flags
+        v = flags.to(torch.int32)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=self.group)
+        return v > 0
+
     def allreduce_flat(self, flat):
         """Synchronous bucketed all-reduce of another flat gradient buffer (the discriminator's)."""
         if self.world == 1:

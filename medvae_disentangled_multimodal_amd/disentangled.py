@@ -19,11 +19,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.distributions import Normal
 
+from . import ops
 from .encoder_decoder import Conv2d
 from .vae import BaseVAE, _posterior, _prior
-
-MODALITY_BUCKETS = 16  # device-side bucket count for separation-loss centroids (ids must be < 16)
-
 
 def _nan_to_zero(t):
     return torch.where(torch.isnan(t), torch.zeros_like(t), t)
@@ -148,10 +146,18 @@ class DisentangledConditionalVAE(BaseVAE):
         return z_full.view(z_full.shape[0], spatial, r, r)
 
     def modality_separation_loss(self, z: torch.Tensor, modality_indices: torch.Tensor) -> torch.Tensor:
+        """-mean pdist of the centroids of every distinct (unclamped) modality id, :305-349. The ids of
+        `torch.unique` become segment numbers of the sorted ids (any id value, no host sync): B segment
+        slots, of which the first (#distinct) are present."""
         _, zm = self.partition_latent(z)
-        idx = modality_indices.to(z.device).long()
-        nb = MODALITY_BUCKETS
-        oh = (idx[:, None] == torch.arange(nb, device=z.device)[None, :]).to(zm.dtype)  # [B, nb]
+        idx = modality_indices.to(z.device).long().view(-1)
+        nb = idx.shape[0]
+        srt, perm = torch.sort(idx, stable=True)
+        new = torch.ones_like(srt, dtype=torch.bool)
+        new[1:] = srt[1:] != srt[:-1]
+        seg = torch.empty_like(idx)
+        seg[perm] = torch.cumsum(new.long(), 0) - 1
+        oh = (seg[:, None] == torch.arange(nb, device=z.device)[None, :]).to(zm.dtype)  # [B, B]
         cnt = oh.sum(0)
         present = cnt > 0
         cent = (oh.t() @ zm) / cnt.clamp_min(1.0)[:, None]
@@ -187,8 +193,9 @@ class DisentangledConditionalVAE(BaseVAE):
         z = self.reparameterize(mu, logvar, eps=eps)
         hint = 1 if x.shape[1] == 1 else max(self.modality_channels.values())
         rec = self._decode_routed(z, modality_indices, hint)
-        sep = self.modality_separation_loss(z, modality_indices)
-        con = self.contrastive_loss(z, modality_indices)
+        # gated terms: a NaN/Inf value drops the term's gradient (DisentangledVAELoss replaces it by 0, :540-550)
+        sep = ops.finite_gated(lambda zz: self.modality_separation_loss(zz, modality_indices), z)
+        con = ops.finite_gated(lambda zz: self.contrastive_loss(zz, modality_indices), z)
         std = torch.clamp(torch.exp(0.5 * logvar), min=1e-6, max=10.0)
         out = {"reconstruction": rec, "mean": mu, "logvar": logvar, "mu": mu, "z": z,
                "prior": _prior(mu, std), "posterior": _posterior(mu, logvar, std),

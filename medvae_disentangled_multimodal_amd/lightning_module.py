@@ -255,6 +255,10 @@ class VAELightningModule(_Base):
             self._param_mod = torch.tensor([self.model.parameter_modality(n) for n in f.names],
                                            dtype=torch.long, device=f.device)
         present = self.model.modality_presence(self._usage.to(f.device))
+        if self.process_group is not None:
+            # a head used on ANY rank receives the averaged gradient on every rank: the mask (clip norm, Adam
+            # update and step count) must be the same everywhere or the replicas drift apart
+            present = self.process_group.any_across_ranks(present)
         pm = self._param_mod
         used = (pm == -1) | ((pm >= 0) & present[pm.clamp_min(0)])
         return used.to(torch.int32)

@@ -45,7 +45,8 @@ class VAELoss(nn.Module):
 
 
 def _finite_or_zero(v: torch.Tensor) -> torch.Tensor:
-    # device-side replacement of the reference's `if isnan(v).any(): v = 0` (no host sync)
+    # device-side replacement of the reference's `if isnan(v).any(): v = 0` (no host sync); the term's own
+    # gradient is gated by ops.finite_gated where it is computed, so a non-finite term contributes nothing
     return torch.where(torch.isfinite(v), v, torch.zeros_like(v))
 
 
@@ -62,8 +63,10 @@ class DisentangledVAELoss(nn.Module):
         self.separation_weight, self.contrastive_weight = separation_weight, contrastive_weight
 
     def forward(self, outputs: Dict[str, torch.Tensor], targets: torch.Tensor) -> Dict[str, torch.Tensor]:
-        recon = _finite_or_zero(_recon(self.recon_loss_type, outputs["reconstruction"], targets))
-        kl = _finite_or_zero(ops.kl_closed_form_sum(outputs["mu"], outputs["logvar"], targets.numel()))
+        kind, n = self.recon_loss_type, targets.numel()
+        recon = _finite_or_zero(ops.finite_gated(lambda r, t: _recon(kind, r, t), outputs["reconstruction"], targets))
+        kl = _finite_or_zero(ops.finite_gated(lambda m, lv: ops.kl_closed_form_sum(m, lv, n), outputs["mu"],
+                                              outputs["logvar"]))
         sep = _finite_or_zero(outputs["separation_loss"])
         con = _finite_or_zero(outputs["contrastive_loss"])
         total = (self.recon_weight * recon + self.kl_weight * kl + self.separation_weight * sep +

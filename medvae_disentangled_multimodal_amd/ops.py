@@ -771,6 +771,43 @@ class ReconFn(torch.autograd.Function):
         return da, None, None
 
 
+class _FiniteGateFn(torch.autograd.Function):
+    """v = fn(*inputs); backward recomputes fn under autograd and hands back its input gradients only if v
+    was finite (device-side flag, no host sync). This is the reference's `if isnan(v) or isinf(v): v =
+    tensor(0.)` (disentangled_conditional_vae.py:528-550): a non-finite term is cut out of the graph, so
+    its backward can never inject 0*inf = NaN into the shared encoder gradients."""
+
+    @staticmethod
+    def forward(ctx, fn, *inputs):
+        v = fn(*inputs)
+        ctx.fn = fn
+        ctx.ok = torch.isfinite(v).all()
+        ctx.save_for_backward(*inputs)
+        return v
+
+    @staticmethod
+    def backward(ctx, g):
+        ins = ctx.saved_tensors
+        need = ctx.needs_input_grad[1:]
+        with torch.enable_grad():
+            req = [t.detach().requires_grad_(bool(n)) for t, n in zip(ins, need)]
+            v = ctx.fn(*req)
+            want = [r for r in req if r.requires_grad]
+            got = list(torch.autograd.grad(v, want, g, allow_unused=True)) if want else []
+        out = []
+        for r in req:
+            gr = got.pop(0) if r.requires_grad else None
+            if gr is not None:
+                gr = torch.where(ctx.ok, gr, torch.zeros((), device=gr.device, dtype=gr.dtype))
+            out.append(gr)
+        return (None, *out)
+
+
+def finite_gated(fn, *inputs):
+    """fn(*inputs) as a loss term whose gradient is dropped when its value is NaN/Inf."""
+    return _FiniteGateFn.apply(fn, *inputs)
+
+
 def mse_mean(a, b):
     return ReconFn.apply(a, b, 1)
 

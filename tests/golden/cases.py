@@ -63,6 +63,46 @@ CASES = {
         optimizer=dict(type="adam", lr=5e-4, weight_decay=0.0, betas=[0.9, 0.999]),
         clip=0.5,
     ),
+    # ---- full BASELINE architectures at small batch (the production fast paths: 256x256 GEMM tiles,
+    # GroupNorm statistics / backward fused into the GEMM epilogues (H*W % 32 == 0, C/G % 4 == 0),
+    # sub-pixel Upsample at >= 512 channels, many-split wgrad, 1024/2048-channel attention).
+    # Config 4 exactly (configs/experiment/multi_modal_cvae.yaml + model.resolution=64, loss vae,
+    # configs/training/advanced.yaml optimizer): 927 M parameters.
+    "cvae_c4_full": dict(
+        cls="ConditionalVAE",
+        kwargs=dict(input_channels=3, latent_dim=256, hidden_channels=256, ch_mult=[1, 2, 4, 8],
+                    num_res_blocks=2, attn_resolutions=[16], dropout=0.0, resolution=64,
+                    condition_method="concat"),
+        batch=2, cond="onehot", full=True,
+        loss=dict(type="vae", recon_loss_type="mse", kl_weight=1.0, recon_weight=1.0),
+        optimizer=dict(type="adamw", lr=1e-4, weight_decay=1e-5, betas=[0.5, 0.999]),
+        clip=1.0,
+    ),
+    # Config 2 exactly (path_beta_vae, 3-level ch_mult at 28x28x3; mid attention only).
+    "beta_c2_full": dict(
+        cls="BetaVAE",
+        kwargs=dict(input_channels=3, latent_dim=128, hidden_channels=128, ch_mult=[1, 2, 4],
+                    num_res_blocks=2, attn_resolutions=[16], dropout=0.0, resolution=28, beta=6.0),
+        batch=2, cond="none", full=True,
+        loss=dict(type="vae", recon_loss_type="mse", kl_weight=6.0, recon_weight=1.0),
+        optimizer=dict(type="adamw", lr=1e-4, weight_decay=1e-4, betas=[0.9, 0.999]),
+        clip=1.0,
+    ),
+    # Config 3 architecture (disentangled_multi_modal_cvae_quick) at B=16: every modality, repeated
+    # modalities, and out-of-range ids 7, 9 and 17 (routing clamps them to 4; the separation loss keeps
+    # each as its own centroid, so ids >= 16 must work too).
+    "dis_c3_b16": dict(
+        cls="DisentangledConditionalVAE",
+        kwargs=dict(num_modalities=5, shared_latent_dim=8, modality_latent_dim=8,
+                    hidden_channels=32, ch_mult=[1, 2, 4], num_res_blocks=1, attn_resolutions=[],
+                    dropout=0.0, resolution=28, modality_separation_weight=0.1,
+                    contrastive_weight=0.05),
+        batch=16, cond="idx", idx=[0, 1, 2, 3, 4, 7, 1, 0, 17, 3, 2, 4, 4, 9, 1, 0],
+        loss=dict(type="disentangled_vae", recon_loss_type="mse", kl_weight=1.0,
+                  recon_weight=1.0, separation_weight=0.1, contrastive_weight=0.05),
+        optimizer=dict(type="adam", lr=5e-4, weight_decay=0.0, betas=[0.9, 0.999]),
+        clip=0.5,
+    ),
 }
 
 MODALITY_CHANNELS = {0: 1, 1: 3, 2: 3, 3: 1, 4: 3}
@@ -80,4 +120,12 @@ FULL_GRADS = {
     "dis_c3": ["modality_input_projectors.0.weight", "modality_output_projectors.3.weight",
                "modality_decoders.4.0.weight", "modality_decoders.1.2.bias",
                "encoder.conv_in.weight"],
+    "cvae_c4_full": ["condition_proj.0.bias", "encoder.conv_in.weight", "decoder.conv_out.weight",
+                     "decoder.conv_out.bias", "encoder.mid.attn_1.norm.weight", "decoder.up.3.block.0.norm1.bias",
+                     "encoder.norm_out.weight"],
+    "beta_c2_full": ["encoder.conv_in.weight", "decoder.conv_out.weight", "decoder.mid.attn_1.proj_out.bias",
+                     "encoder.down.1.block.0.nin_shortcut.weight", "decoder.up.0.block.2.norm2.weight"],
+    "dis_c3_b16": ["modality_input_projectors.0.weight", "modality_output_projectors.3.weight",
+                   "modality_decoders.4.0.weight", "modality_decoders.1.2.bias", "modality_decoders.2.2.weight",
+                   "encoder.conv_in.weight"],
 }

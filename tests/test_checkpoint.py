@@ -55,3 +55,42 @@ def test_checkpoint_roundtrip_and_torch_format():
         assert torch.equal(F._view(b.optimizer.exp_avg_sq, off, pb), F._view(a.optimizer.exp_avg_sq, off, pa))
     assert torch.equal(b.optimizer.steps, a.optimizer.steps)
     assert b.global_step_count == 7
+
+
+def test_checkpoint_lpips_discriminator_roundtrip():
+    """config-5 / adversarial objective: the criterion's state (LPIPS network, NLayerDiscriminator weights and
+    BatchNorm buffers) is written as `criterion.*` and the discriminator's Adam as optimizer_states[1]; both
+    round-trip."""
+    def make(seed):
+        torch.manual_seed(seed)
+        model = M.BaseVAE(**KW)
+        loss = {"type": "lpips_discriminator", "allow_synthetic_lpips": True, "lpips_net": "alex",
+                "discriminator": {"input_nc": 3, "ndf": 8, "n_layers": 2}}
+        mod = M.VAELightningModule(model, {"type": "adam", "lr": 2e-4}, {"type": "none"}, loss)
+        mod.configure_optimizers()
+        return mod
+
+    a = make(0)
+    with torch.no_grad():
+        for n, b in a.criterion.discriminator.named_buffers():
+            if b.is_floating_point():
+                b.uniform_(0.5, 1.5)
+    a.optimizer_d.exp_avg.normal_()
+    a.optimizer_d.exp_avg_sq.uniform_()
+    a.optimizer_d.steps.fill_(3)
+    ck = checkpoint.lightning_checkpoint(a)
+    keys = list(ck["state_dict"])
+    assert any(k.startswith("criterion.discriminator.") and k.endswith("running_mean") for k in keys)
+    assert any(k.startswith("criterion.perceptual_loss.") for k in keys)
+    assert len(ck["optimizer_states"]) == 2
+    ref_d = torch.optim.Adam(a.criterion.discriminator.parameters(), lr=1.0)
+    ref_d.load_state_dict(ck["optimizer_states"][1])  # torch's own format
+    b = make(9)
+    checkpoint.load_checkpoint(b, ck)
+    assert torch.equal(b.flat_d.data, a.flat_d.data)
+    for (ka, va), (kb, vb) in zip(a.criterion.state_dict().items(), b.criterion.state_dict().items()):
+        assert ka == kb and torch.equal(va, vb), ka
+    assert torch.equal(b.optimizer_d.steps, a.optimizer_d.steps)
+    from medvae_disentangled_multimodal_amd.optim import FlatParameters as F
+    for pa, pb, off in zip(a.flat_d.params, b.flat_d.params, a.flat_d.offsets):
+        assert torch.equal(F._view(b.optimizer_d.exp_avg, off, pb), F._view(a.optimizer_d.exp_avg, off, pa))

@@ -87,3 +87,56 @@ def test_dp_overlapped_allreduce_matches_global_batch():
     ref = mod.flat.grad.cpu().double()
     got = r0["grad"].double()
     assert float((got - ref).norm() / ref.norm()) < 1e-3
+
+
+DKW = dict(num_modalities=5, shared_latent_dim=8, modality_latent_dim=8, hidden_channels=32, ch_mult=(1, 2),
+           num_res_blocks=1, attn_resolutions=[], dropout=0.0, resolution=16)
+
+
+def _worker_modalities(rank, world, init_file, out_file):
+    """Rank 0 sees modalities {0, 1}, rank 1 sees {2, 3, 4}: every head is used on exactly one rank."""
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    import medvae_disentangled_multimodal_amd as M
+    from medvae_disentangled_multimodal_amd import ddp
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    model = M.DisentangledConditionalVAE(**DKW).to(dev)
+    mod = M.VAELightningModule(model, {"type": "adam", "lr": 5e-4}, {"type": "none"},
+                               {"type": "disentangled_vae"}, gradient_clip_val=0.5)
+    mod.configure_optimizers()
+    ddp.DataParallel(mod, bucket_bytes=64 << 10)
+    g = torch.Generator().manual_seed(11 + rank)
+    idx = torch.tensor([0, 1, 0, 1] if rank == 0 else [2, 3, 4, 2])
+    x = torch.rand(4, 3, 16, 16, generator=g) * 2 - 1
+    eps = torch.randn(4, 16, 8, 8, generator=g)
+    oh = torch.nn.functional.one_hot(idx, 12).float()
+    batch = (x.to(dev), torch.zeros(4, 1, dtype=torch.long, device=dev), oh.to(dev), idx.to(dev))
+    for step in range(2):
+        mod.fit_step(batch, step, eps=eps.to(dev))
+    torch.cuda.synchronize()
+    torch.save({"params": mod.flat.data.cpu(), "used": mod._used_mask().cpu(),
+                "steps": mod.optimizer.steps.cpu()}, f"{out_file}.{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_rank_dependent_modalities_keep_replicas_identical():
+    """the per-modality parameter mask (clip norm / Adam update / step count) is OR-ed over ranks, so
+    parameters stay bitwise identical when ranks see different modalities."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    with tempfile.TemporaryDirectory() as d:
+        init_file = os.path.join(d, "init")
+        out = os.path.join(d, "out")
+        ctx = mp.get_context("spawn")
+        procs = [ctx.Process(target=_worker_modalities, args=(r, 2, init_file, out)) for r in range(2)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=300)
+        assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+        r0 = torch.load(f"{out}.0", weights_only=True)
+        r1 = torch.load(f"{out}.1", weights_only=True)
+    assert torch.equal(r0["used"], r1["used"]) and bool(r0["used"].bool().all()) is False  # embedding unused
+    assert torch.equal(r0["steps"], r1["steps"])
+    assert torch.equal(r0["params"], r1["params"])

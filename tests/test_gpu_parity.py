@@ -10,6 +10,7 @@ gradients of every parameter through their sum of squares, selected gradients/pa
 The index routing of the disentangled model is exact (selection, no arithmetic).
 """
 import json
+import math
 import os
 
 import pytest
@@ -88,7 +89,14 @@ def test_training_step_matches_reference(name):
     mod.optimizer.step(used=used)
     torch.cuda.synchronize()
     tn = float(mod.optimizer.last_total_norm)
-    assert abs(tn - float(data["clip.total_norm"])) < TOL * float(data["clip.total_norm"])
+    # The global norm of the reference's own gradients, summed in float64 from the fixture's per-tensor sums of
+    # squares. torch's CPU fp32 clip_grad_norm_ (the fixture's clip.total_norm) accumulates in fp32 and drifts
+    # from it by 1.1e-3 at the 927 M-parameter c4 architecture (9.7718 vs 9.7828; float64 oracle: 9.78283),
+    # so the exact norm is the target and the fp32 value is held to 2x the budget.
+    exact = math.sqrt(sum(float(data[f"gradsum.{k}"][1]) for k in has))
+    report["clip.total_norm_vs_exact"] = abs(tn - exact) / exact
+    assert abs(tn - exact) < TOL * exact
+    assert abs(tn - float(data["clip.total_norm"])) < 2 * TOL * float(data["clip.total_norm"])
     # (a) the fused step equals torch.optim applied to OUR gradients (per-tensor non-finite zeroing,
     #     global clip, Adam/AdamW, params without a gradient skipped)
     used_l = used.tolist() if used is not None else [1] * len(names)
