@@ -274,6 +274,36 @@ size_t mvae_batch_norm_workspace_bytes(long long rows, int c);
 int mvae_leaky_relu_fwd(const float* x, float* y, float slope, long long n, void* stream);
 int mvae_leaky_relu_bwd(const float* y, const float* dy, float* dx, float slope, long long n, void* stream);
 
+/* ---- disentangled modality routing (DisentangledConditionalVAE) ------------------------------------------
+ * Replaces the reference's per-sample Python loops (src/models/disentangled_conditional_vae.py:137-169 encode,
+ * :255-301 decode): ONE launch per batch; each sample reads its modality id idx[b] (int64, device; ids >= nm
+ * use modality nm-1 like :142-146 / :260-265) and runs only that modality's layers. c (max channels) must be 3
+ * (the reference's channel map {0:1, 1:3, 2:3, 3:1, 4:3}); nm <= 8; the image must fit the LDS tiles
+ * ((4*(h+2)*(w+2) + h*w) * c * 4 bytes <= 160 KiB). Parameter tables are HOST arrays of device pointers.
+ * Weight gradients accumulate (+=) into the grad_table slots (per-sample partials, fixed-order per-modality
+ * reduction: deterministic); NULL slots are skipped.
+ *
+ * heads: table[6*m + {0..5}] = {w1, b1, w2, b2, pw, pb} of modality_decoders.m.0 / .m.2 (conv3x3 c->c, KRSC)
+ * and modality_output_projectors.m (1x1 c->1; NULL/NULL for colour modalities). rec / drec [nb][h][w][c];
+ * out / dout [nb][h][w][out_c]: the projector output (1 channel) or the head's first out_c channels,
+ * zero-padded to out_c channels (:283-299). */
+int mvae_modality_heads_fwd(const float* rec, const long long* idx, int nb, int h, int w, int c, int nm,
+                            const void* const* table, int out_c, float* out, void* stream);
+int mvae_modality_heads_bwd(const float* rec, const long long* idx, int nb, int h, int w, int c, int nm,
+                            const void* const* table, int out_c, const float* dout, float* drec,
+                            void* const* grad_table, void* workspace, size_t ws_bytes, void* stream);
+size_t mvae_modality_heads_workspace_bytes(int nb, int c);
+/* input routing: routed[b] = nan_to_zero(proj_m(nan_to_zero(x[b][..][0]))) when table[2*m] (1x1 conv 1->c
+ * weight, table[2*m+1] its bias) is set, else nan_to_zero(x[b][..][0..c)) (channels past cx read as 0).
+ * x [nb][hw][cx], routed / drouted [nb][hw][c]; the backward produces the projector weight gradients only
+ * (x is data). */
+int mvae_modality_route_in_fwd(const float* x, int cx, const long long* idx, int nb, int hw, int c, int nm,
+                               const void* const* table, float* routed, void* stream);
+int mvae_modality_route_in_bwd(const float* x, int cx, const long long* idx, int nb, int hw, int c, int nm,
+                               const void* const* table, const float* drouted, void* const* grad_table,
+                               void* workspace, size_t ws_bytes, void* stream);
+size_t mvae_modality_route_in_workspace_bytes(int nb, int c);
+
 #ifdef __cplusplus
 }
 #endif

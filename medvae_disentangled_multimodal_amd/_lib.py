@@ -78,6 +78,12 @@ SIGNATURES = {
     "mvae_batch_norm_workspace_bytes": (Z, [L, I]),
     "mvae_leaky_relu_fwd": (I, [P, P, F, L, P]),
     "mvae_leaky_relu_bwd": (I, [P, P, P, F, L, P]),
+    "mvae_modality_heads_fwd": (I, [P, P, I, I, I, I, I, P, I, P, P]),
+    "mvae_modality_heads_bwd": (I, [P, P, I, I, I, I, I, P, I, P, P, P, P, Z, P]),
+    "mvae_modality_heads_workspace_bytes": (Z, [I, I]),
+    "mvae_modality_route_in_fwd": (I, [P, I, P, I, I, I, I, P, P, P]),
+    "mvae_modality_route_in_bwd": (I, [P, I, P, I, I, I, I, P, P, P, P, Z, P]),
+    "mvae_modality_route_in_workspace_bytes": (Z, [I, I]),
 }
 
 

@@ -828,7 +828,22 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
       __syncthreads();
     }
   };
+#ifndef MVAE_NO_PRIO
+  // the second-dispatched half of the workgroup loses every VALU arbitration to its SIMD partner: one static
+  // priority raise for it (no per-segment flips): wgrad +1-3 %, fwd / dgrad within noise (tools/ab.sh)
+  if (NT >= 512 && wid >= (NT / 64) / 2) __builtin_amdgcn_s_setprio(1);
+#endif
+#ifdef MVAE_STAG
+  if (NT >= 512 && wid >= (NT / 64) / 2)
+    kloop(std::true_type{});
+  else
     kloop(std::false_type{});
+#else
+    kloop(std::false_type{});
+#endif
+#ifndef MVAE_NO_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
 #else
   for (; t + 2 < nt; ++t) {  // block staging: all of tile t+1's staging, then tile t's MFMAs
     __bf16* nb = lds + ((t & 1) ^ 1) * BUF;

@@ -2,9 +2,11 @@
 (reference: src/models/disentangled_conditional_vae.py:14-482).
 
 The reference routes every sample through a Python loop (`.item()` per sample, per-sample conv
-launches: :137-169, :255-301). Here the routing is batched and stays on the device: the per-modality
-input projectors and decoder heads run over the whole batch on the HIP conv kernel and each sample
-picks its modality's result with an exact index select (bit-exact routing, no host sync).
+launches: :137-169, :255-301). Here the routing is batched and stays on the device: ONE launch routes
+the batch through the input projectors and ONE through the modality heads (csrc/routing.hip): each
+sample reads its modality id on the device and runs only that modality's layers (no host sync, no
+work on the other heads). Images too large for the kernels' LDS tiles use the grouped form: every
+head over the whole batch on the HIP conv kernel, then an exact per-sample index select.
 Semantics kept: out-of-range indices clamp to the last modality (:142-146, :258-265), 1-channel
 modalities use only channel 0 of the (collate-padded) input, NaN scrubbing (:132-191), mu/logvar clamp
 to [-10, 10] (:409-412), `partition_latent`'s NCHW flatten order (:195-206), separation loss over the
@@ -12,6 +14,7 @@ sorted unique (unclamped) modality ids (:305-349), masked InfoNCE contrastive lo
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -22,6 +25,10 @@ from torch.distributions import Normal
 from . import ops
 from .encoder_decoder import Conv2d
 from .vae import BaseVAE, _posterior, _prior
+
+# batched per-sample routing kernels (csrc/routing.hip); MVAE_NO_ROUTING=1 selects the grouped-conv form
+ROUTING_KERNELS = os.environ.get("MVAE_NO_ROUTING") is None
+
 
 def _nan_to_zero(t):
     return torch.where(torch.isnan(t), torch.zeros_like(t), t)
@@ -82,11 +89,36 @@ class DisentangledConditionalVAE(BaseVAE):
         return (idx[:, None] == torch.arange(self.num_modalities, device=idx.device)[None, :]).any(0)
 
     # -- routing ------------------------------------------------------------------------------
+    def _route_in_params(self):
+        ps = []
+        for m in range(len(self.modality_channels)):
+            proj = self.modality_input_projectors[str(m)] if str(m) in self.modality_input_projectors else None
+            ps += [proj.weight, proj.bias] if proj is not None else [None, None]
+        return ps
+
+    def _head_params(self):
+        ps = []
+        for m, head in enumerate(self.modality_decoders):
+            proj = self.modality_output_projectors[str(m)] if str(m) in self.modality_output_projectors else None
+            ps += [head[0].weight, head[0].bias, head[2].weight, head[2].bias]
+            ps += [proj.weight, proj.bias] if proj is not None else [None, None]
+        return ps
+
+    def _routing_kernel_ok(self, t: torch.Tensor) -> bool:
+        mx = max(self.modality_channels.values())
+        return (t.is_cuda and ROUTING_KERNELS and len(self.modality_channels) == len(self.modality_decoders) and
+                all(c in (1, mx) for c in self.modality_channels.values()) and
+                ops.routing_fits(t.shape[2], t.shape[3], mx, len(self.modality_decoders)))
+
     def encode(self, x: torch.Tensor, modality_indices: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        mx = max(self.modality_channels.values())
+        if self._routing_kernel_ok(x):  # one launch: each sample through its own input projector (csrc/routing.hip)
+            routed = ops.modality_route_in(x, modality_indices, mx, len(self.modality_channels), self._route_in_params())
+            mu, logvar = BaseVAE.encode(self, routed)
+            return _nan_to_zero(mu), _nan_to_zero(logvar)
         x = _nan_to_zero(x)
         idx = self._clamp(modality_indices.to(x.device).long(), len(self.modality_channels))
         sel = idx.view(-1, 1, 1, 1)
-        mx = max(self.modality_channels.values())
         if x.shape[1] >= mx:
             routed = x[:, :mx]
         else:
@@ -101,13 +133,16 @@ class DisentangledConditionalVAE(BaseVAE):
     def _decode_routed(self, z, modality_indices, out_channels: Optional[int]):
         rec = BaseVAE.decode(self, z)
         idx = self._clamp(modality_indices.to(rec.device).long(), len(self.modality_decoders))
+        if out_channels is None:
+            colour = [m for m, c in self.modality_channels.items() if c == max(self.modality_channels.values())]
+            out_channels = 3 if bool(torch.isin(idx, torch.tensor(colour, device=idx.device)).any()) else 1
+        if self._routing_kernel_ok(rec):  # one launch: each sample through its own head + projector
+            return ops.modality_heads(rec, modality_indices, out_channels, len(self.modality_decoders),
+                                      self._head_params())
         sel = idx.view(-1, 1, 1, 1)
         heads = torch.zeros_like(rec)
         for m, head in enumerate(self.modality_decoders):
             heads = torch.where(sel == m, head(rec), heads)
-        if out_channels is None:
-            colour = [m for m, c in self.modality_channels.items() if c == max(self.modality_channels.values())]
-            out_channels = 3 if bool(torch.isin(idx, torch.tensor(colour, device=idx.device)).any()) else 1
         out = heads[:, :out_channels] if out_channels <= heads.shape[1] else heads
         for key, proj in self.modality_output_projectors.items():
             o = proj(heads)  # [B, c_m, H, W]

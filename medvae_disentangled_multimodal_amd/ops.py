@@ -9,6 +9,7 @@ Every op requires CUDA(HIP) tensors: there is no CPU fallback.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 from dataclasses import dataclass
@@ -1078,3 +1079,127 @@ def hinge_fake(logits):  # mean(relu(1 + logits))
 
 def neg_mean(logits):  # -mean(logits)
     return AdvTermFn.apply(logits, 6, -1.0 / logits.numel())
+
+
+# ------------------------------------------------------------------------------------------
+# disentangled modality routing (disentangled_conditional_vae.py:124-193, 241-303): one launch per batch,
+# each sample runs only its own modality's projector / head (csrc/routing.hip)
+# ------------------------------------------------------------------------------------------
+ROUTING_MAX_MODALITIES = 8
+
+
+def _ptr_table(ts):
+    arr = (ctypes.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
+    return arr
+
+
+def routing_fits(h: int, w: int, c: int, nm: int) -> bool:
+    """The routing kernels keep a whole image (zero-bordered, 5 planes in the backward) in LDS."""
+    return c == 3 and 1 <= nm <= ROUTING_MAX_MODALITIES and (4 * (h + 2) * (w + 2) * c + h * w * c) * 4 <= 160 * 1024
+
+
+def _grad_targets(params):
+    """Flat gradient slots of the parameters, or fresh zero tensors (returned to autograd)."""
+    tg, ret = [], []
+    for p in params:
+        if p is None:
+            tg.append(None)
+            ret.append(None)
+            continue
+        g = _main_grad(p)
+        if g is None:
+            if p.dim() == 4:
+                o, i, kh, kw = p.shape
+                g = torch.zeros((o, kh, kw, i), device=p.device, dtype=torch.float32).permute(0, 3, 1, 2)
+            else:
+                g = torch.zeros_like(p, dtype=torch.float32)
+            ret.append(g)
+        else:
+            ret.append(None)
+        tg.append(g)
+    return tg, ret
+
+
+class ModalityHeadsFn(torch.autograd.Function):
+    """Per-sample modality head conv3x3 -> ReLU -> conv3x3 (+ 1x1 output projector, zero-padded to out_c) for
+    the whole batch in one launch. params: per modality (w1, b1, w2, b2, pw, pb), pw/pb None for colour
+    modalities (no projector)."""
+
+    @staticmethod
+    def forward(ctx, rec, idx, out_c: int, nm: int, *params):
+        _check(rec, "decoder output")
+        rec = nhwc(rec)
+        n, c, h, w = rec.shape
+        idx = idx.to(device=rec.device, dtype=torch.long).contiguous()
+        ws = [None if p is None else (_krsc(p) if p.dim() == 4 else p.contiguous()) for p in params]
+        tab = _ptr_table(ws)
+        out = torch.empty((n, out_c, h, w), device=rec.device, dtype=torch.float32, memory_format=CL)
+        _lib.call("mvae_modality_heads_fwd", rec.data_ptr(), idx.data_ptr(), n, h, w, c, nm, tab, out_c,
+                  out.data_ptr(), _stream(rec))
+        ctx.save_for_backward(rec, idx, *[t for t in ws if t is not None])
+        ctx.present = [t is not None for t in ws]
+        ctx.out_c, ctx.nm = out_c, nm
+        ctx.param_refs = params
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        saved = ctx.saved_tensors
+        rec, idx, rest = saved[0], saved[1], list(saved[2:])
+        ws = [rest.pop(0) if pr else None for pr in ctx.present]
+        n, c, h, w = rec.shape
+        dout = nhwc(dout.float())
+        drec = torch.empty_like(rec, memory_format=CL)
+        tg, ret = _grad_targets(ctx.param_refs)
+        gtab = _ptr_table(tg)
+        tab = _ptr_table(ws)
+        nbytes = _lib.query("mvae_modality_heads_workspace_bytes", n, c)
+        wsp = ARENA.get("heads", nbytes, rec.device)
+        _lib.call("mvae_modality_heads_bwd", rec.data_ptr(), idx.data_ptr(), n, h, w, c, ctx.nm, tab, ctx.out_c,
+                  dout.data_ptr(), drec.data_ptr(), gtab, wsp.data_ptr(), wsp.numel(), _stream(rec))
+        _grad_done(*[p for p, r in zip(ctx.param_refs, ret) if p is not None and r is None])
+        return (drec, None, None, None, *ret)
+
+
+def modality_heads(rec, idx, out_c: int, nm: int, params):
+    return ModalityHeadsFn.apply(rec, idx, out_c, nm, *params)
+
+
+class RouteInFn(torch.autograd.Function):
+    """routed[b] = nan_to_zero(projector_m(nan_to_zero(x[b, :1]))) for modalities with an input projector,
+    else nan_to_zero(x[b, :C]) (zero channels beyond x's). params: per modality (w, b) or (None, None)."""
+
+    @staticmethod
+    def forward(ctx, x, idx, c: int, nm: int, *params):
+        _check(x, "input")
+        x = nhwc(x)
+        n, cx, h, w = x.shape
+        idx = idx.to(device=x.device, dtype=torch.long).contiguous()
+        ws = [None if p is None else p.contiguous() for p in params]
+        routed = torch.empty((n, c, h, w), device=x.device, dtype=torch.float32, memory_format=CL)
+        _lib.call("mvae_modality_route_in_fwd", x.data_ptr(), cx, idx.data_ptr(), n, h * w, c, nm, _ptr_table(ws),
+                  routed.data_ptr(), _stream(x))
+        ctx.save_for_backward(x, idx, *[t for t in ws if t is not None])
+        ctx.present = [t is not None for t in ws]
+        ctx.c, ctx.nm = c, nm
+        ctx.param_refs = params
+        return routed
+
+    @staticmethod
+    def backward(ctx, drouted):
+        saved = ctx.saved_tensors
+        x, idx, rest = saved[0], saved[1], list(saved[2:])
+        ws = [rest.pop(0) if pr else None for pr in ctx.present]
+        n, cx, h, w = x.shape
+        drouted = nhwc(drouted.float())
+        tg, ret = _grad_targets(ctx.param_refs)
+        nbytes = _lib.query("mvae_modality_route_in_workspace_bytes", n, ctx.c)
+        wsp = ARENA.get("route_in", nbytes, x.device)
+        _lib.call("mvae_modality_route_in_bwd", x.data_ptr(), cx, idx.data_ptr(), n, h * w, ctx.c, ctx.nm,
+                  _ptr_table(ws), drouted.data_ptr(), _ptr_table(tg), wsp.data_ptr(), wsp.numel(), _stream(x))
+        _grad_done(*[p for p, r in zip(ctx.param_refs, ret) if p is not None and r is None])
+        return (None, None, None, None, *ret)
+
+
+def modality_route_in(x, idx, c: int, nm: int, params):
+    return RouteInFn.apply(x, idx, c, nm, *params)

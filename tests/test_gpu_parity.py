@@ -109,7 +109,12 @@ def test_training_step_matches_reference(name):
         ref_grads.append(g_before[off:off + n].clone())
     for rp, rg in zip(ref_params, ref_grads):
         rp.grad = rg if torch.isfinite(rg).all() else torch.zeros_like(rg)
-    torch.nn.utils.clip_grad_norm_(ref_params, case["clip"])
+    # clip_grad_norm_'s arithmetic with the norm summed in float64 (torch's CPU fp32 norm drifts by 1e-3 at the
+    # 927 M-parameter c4 architecture -- see the total-norm check above)
+    tn64 = math.sqrt(sum(float((rp.grad.double() ** 2).sum()) for rp in ref_params))
+    coef = min(1.0, case["clip"] / (tn64 + 1e-6))
+    for rp in ref_params:
+        rp.grad.mul_(coef)
     oc = case["optimizer"]
     O = torch.optim.AdamW if oc["type"] == "adamw" else torch.optim.Adam
     O(ref_params, lr=oc["lr"], betas=tuple(oc["betas"]), weight_decay=oc["weight_decay"]).step()

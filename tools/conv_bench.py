@@ -45,6 +45,13 @@ def main():
         r = dict(shape=f"{ci}->{co} k{k} s{s} {h}x{h}{' ups' if ups else ''}", gflop=round(fl / 1e9, 1),
                  fwd_tf=round(fl / tf / 1e12, 1), dgrad_tf=round(fl / td / 1e12, 1), wgrad_tf=round(fl / tw / 1e12, 1),
                  ms=[round(tf * 1e3, 2), round(td * 1e3, 2), round(tw * 1e3, 2)])
+        if k == 3 and s == 1 and not ups:  # the training path: GroupNorm output handed over pre-split (3xBF16 hi/lo)
+            xs = torch.empty_like(x)
+            ops._lib.call("mvae_split_bf16", x.data_ptr(), xs.data_ptr(), x.numel(), ops._stream(x))
+            tfs = bench(lambda: ops.conv2d_forward_raw(xs, w, b, None, g, True))
+            tws = bench(lambda: ops.conv2d_wgrad_raw(dy, xs, dw, 0.0, g, x_split=True))
+            r.update(fwd_split_tf=round(fl / tfs / 1e12, 1), wgrad_split_tf=round(fl / tws / 1e12, 1))
+            del xs
         print(json.dumps(r), flush=True)
         res.append(r)
         del x, w, dy, dw
