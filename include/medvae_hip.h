@@ -50,6 +50,10 @@ int mvae_get_math_mode(void);
 /* mode | MVAE_CONV_XSPLIT (mode 0, and mvae_conv2d_wgrad_nhwc mode 0): x is pre-split the same way -- the
  * GroupNorm output written by mvae_group_norm_fwd_nhwc(y_split=1), whose only consumers are convolutions. */
 #define MVAE_CONV_XSPLIT 32
+/* mode | MVAE_CONV_XSPLIT with mode 2 (input gradient): dy (the gathered operand) is pre-split the same way
+ * (mvae_split_bf16 of the conv's output gradient, done once for both backward GEMMs). */
+/* wgrad mode | MVAE_CONV_DYSPLIT: dy (the dY^T operand) is pre-split; the fused bias gradient sums hi + lo. */
+#define MVAE_CONV_DYSPLIT 64
 int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y,
                      int nb, int h, int w_, int cin, int cout, int kh, int kw, int stride, int pad_t,
                      int pad_l, int ho, int wo, int mode, void* stream);
@@ -67,7 +71,8 @@ int mvae_conv2d_gnstats_nhwc(const float* x, const float* w, const float* bias, 
  * encoder_decoder.py:141-163, :318-328): the GEMM epilogue also emits the GroupNorm backward partials
  * part = [nb*h*w/32][cin][2] fp64 {sum dyn, sum dyn*xhat}, dyn = dx*silu'(.), consumed by
  * mvae_group_norm_bwd_part_nhwc. Replaces the reduction half of GroupNorm's backward
- * (aten::native_group_norm_backward). No dropout in between; h*w % 32 == 0, (cin/groups) % 4 == 0. */
+ * (aten::native_group_norm_backward). No dropout in between; h*w % 32 == 0, (cin/groups) % 4 == 0.
+ * w_split flags: bit 0 = wt pre-split (mvae_split_bf16 layout), bit 1 = dy pre-split. */
 int mvae_conv2d_dgrad_gnbwd_nhwc(const float* dy, const float* wt, float* dx, int nb, int ho, int wo, int cout,
                                  int cin, int kh, int kw, int pad_t, int pad_l, int h, int w_, int w_split,
                                  const float* gn_x, const float* mean, const float* rstd, const float* gamma,
@@ -95,7 +100,8 @@ size_t mvae_conv2d_wgrad_small_cout_workspace_bytes(int nb, int cin);
  * class is a dense stride-1 conv of dy [nb][ho][wo][cout] with its own <= 2x2 taps of wt [cin][kh][kw][cout]
  * (mvae_conv_weight_transpose), written interleaved into dx [nb][h][w_][cin] (h, w_ even): the useful
  * MACs only, vs mode 2's transposed gather where 3/4 of the taps hit stride holes.
- * workspace >= 4*kh*kw*cin*cout bytes (per-class weights). */
+ * workspace >= 4*kh*kw*cin*cout bytes (per-class weights). w_split flags: bit 0 = wt pre-split, bit 1 = dy
+ * pre-split (mvae_split_bf16 layout; cout % 4 == 0). */
 int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, int nb, int h, int w_, int cin,
                                    int cout, int kh, int kw, int pad_t, int pad_l, int ho, int wo, int w_split,
                                    float* workspace, size_t workspace_bytes, void* stream);

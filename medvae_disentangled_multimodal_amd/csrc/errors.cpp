@@ -22,8 +22,8 @@ extern "C" int mvae_abi_version(void) { return 1; }
 // GEMM arithmetic of every subsequent convolution / GEMM launch: 0 = 3xBF16 fp32 emulation
 // (default, fp32 training), 1 = bf16 operands with fp32 accumulation (bf16-mixed training).
 extern "C" int mvae_set_math_mode(int mode) {
-  if (mode != 0 && mode != 1) {
-    mvae::set_error("set_math_mode: mode must be 0 (3xbf16) or 1 (bf16)");
+  if (mode != 0 && mode != 1 && mode != 2) {
+    mvae::set_error("set_math_mode: mode must be 0 (3xbf16), 1 (bf16) or 2 (exact fp32)");
     return -1;
   }
   mvae::g_math.store(mode, std::memory_order_relaxed);

@@ -85,7 +85,8 @@ int mvae_conv2d_dgrad_gnbwd_nhwc(const float* dy, const float* wt, float* dx, in
   }
   const GnBwdLink link{gn_x, mean, rstd, gamma, beta, groups, silu, part};
   return conv2d_impl(dy, wt, nullptr, nullptr, dx, nb, ho, wo, cout, cin, kh, kw, 1, pad_t, pad_l, h, wd,
-                     2 | (w_split ? MVAE_CONV_WSPLIT : 0), nullptr, stream, &link);
+                     2 | ((w_split & 1) ? MVAE_CONV_WSPLIT : 0) | ((w_split & 2) ? MVAE_CONV_XSPLIT : 0), nullptr,
+                     stream, &link);
 }
 
 }  // extern "C"
@@ -96,7 +97,11 @@ static int conv2d_impl(const float* x, const float* w, const float* bias, const 
   const bool presplit = (mode & MVAE_CONV_WSPLIT) != 0;
   const bool xsplit = (mode & MVAE_CONV_XSPLIT) != 0;
   mode &= ~(MVAE_CONV_WSPLIT | MVAE_CONV_XSPLIT);
-  if (xsplit && mode != 0) { set_error("conv2d: a pre-split input needs mode 0"); return MVAE_EINVAL; }
+  if (xsplit && mode == 1) { set_error("conv2d: a pre-split input needs mode 0 or 2"); return MVAE_EINVAL; }
+  if ((xsplit || presplit) && split_forbidden()) {
+    set_error("conv2d: pre-split operands are not allowed in the exact-fp32 math mode");
+    return MVAE_EINVAL;
+  }
   if (nb <= 0 || h <= 0 || wd <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || ho <= 0 || wo <= 0 ||
       stride <= 0 || mode < 0 || mode > 2 || (mode == 2 && (stride & (stride - 1)))) {
     set_error("conv2d: bad geometry");
@@ -148,7 +153,10 @@ static int conv2d_impl(const float* x, const float* w, const float* bias, const 
       set_error("conv2d_gnstats: needs the vector (16-B) operand path");
       return MVAE_EINVAL;
     }
-    if (xsplit) {  // x (and w) hold split4_bf16 groups: no staging split at all
+    if (xsplit && mode == 2) {  // dy (the gathered operand of the input gradient) holds split4_bf16 groups
+      if (presplit) launch_big<A_CONV_DGRAD_SPLIT, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
+      else launch_big<A_CONV_DGRAD_SPLIT, 4, B_ROWK, 4>(a, st, cfg);
+    } else if (xsplit) {  // x (and w) hold split4_bf16 groups: no staging split at all
       if (presplit) launch_big<A_CONV_FWD_SPLIT, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
       else launch_big<A_CONV_FWD_SPLIT, 4, B_ROWK, 4>(a, st, cfg);
     } else if (presplit) {  // w holds split4_bf16 groups (MVAE_CONV_WSPLIT): no staging split for B
@@ -227,7 +235,8 @@ int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, 
     // dY row of class row m for tap a: m - pt + a with pt = (r_max - p - pad_t) / 2
     const int pt = (rl[0] - p - pad_t) / 2, pl = (sl[0] - q - pad_l) / 2;
     const bool v = (cout % 4 == 0) && al16(dy) && al16(wcls);
-    if (w_split && !v) { set_error("dgrad_stride2: pre-split weights need cout %% 4 == 0"); return MVAE_EINVAL; }
+    if (w_split && !v) { set_error("dgrad_stride2: pre-split operands need cout %% 4 == 0"); return MVAE_EINVAL; }
+    if (w_split && split_forbidden()) { set_error("dgrad_stride2: pre-split operands in exact-fp32 mode"); return MVAE_EINVAL; }
     for (int b0 = 0; b0 < nb; b0 += chunk) {
       const int n = std::min(chunk, nb - b0);
       GemmArgs a{};
@@ -244,7 +253,9 @@ int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, 
       a.stride = 1; a.stride_shift = 0; a.pad_t = pt; a.pad_l = pl;
       a.sub_w2 = wd; a.sub_par = cls; a.out_remap = 1;
       const int cfg = choose_tile(a, v, false);
-      if (w_split) launch_big<A_CONV_FWD, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
+      if ((w_split & 3) == 3) launch_big<A_CONV_FWD_SPLIT, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
+      else if (w_split & 2) launch_big<A_CONV_FWD_SPLIT, 4, B_ROWK, 4>(a, st, cfg);
+      else if (w_split) launch_big<A_CONV_FWD, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
       else if (v) launch_big<A_CONV_FWD, 4, B_ROWK, 4>(a, st, cfg);
       else launch_small<A_CONV_FWD, 1, B_ROWK, 1>(a, st, cfg);
       const int rc = gemm_finish(a, st);
@@ -277,6 +288,7 @@ int mvae_conv2d_upsample_nhwc(const float* x, const float* w4, const float* bias
   hipStream_t st = (hipStream_t)stream;
   const bool v = (cin % 4 == 0) && al16(x) && al16(w4);
   if (w_split && !v) { set_error("conv2d_upsample: pre-split weights need cin %% 4 == 0"); return MVAE_EINVAL; }
+  if (w_split && split_forbidden()) { set_error("conv2d_upsample: pre-split weights in exact-fp32 mode"); return MVAE_EINVAL; }
   for (int b0 = 0; b0 < nb; b0 += chunk) {
     const int n = std::min(chunk, nb - b0);
     GemmArgs a{};

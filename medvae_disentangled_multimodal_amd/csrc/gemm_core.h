@@ -39,7 +39,7 @@ namespace mvae {
 // operand kinds
 // *_SPLIT kinds read operands already split into 3xBF16 hi/lo groups in HBM (split4_bf16 layout)
 enum { A_ROWK = 0, A_COLM = 1, A_CONV_FWD = 2, A_CONV_UPS = 3, A_CONV_DGRAD = 4, A_CONV_SUBPIX = 5, A_COLM_PIX = 6,
-       A_CONV_FWD_SPLIT = 7 };
+       A_CONV_FWD_SPLIT = 7, A_CONV_DGRAD_SPLIT = 8, A_COLM_SPLIT = 9 };
 enum { B_ROWK = 0, B_COLN = 1, B_WGRAD_FWD = 2, B_WGRAD_UPS = 3, B_WGRAD_SUBPIX = 4, B_ROWK_SPLIT = 5,
        B_WGRAD_FWD_SPLIT = 6 };
 // MODE_SUBPIX: one parity class (ph, pw) of "nearest-x2 upsample then 3x3 conv" as a stride-1 2x2 conv
@@ -67,6 +67,7 @@ __device__ __forceinline__ int col_swz(int kr) { return ((kr >> 3) & 1) << 4; }
 __device__ __forceinline__ int row_off(int r, int kc) { return r * 40 + (((kc >> 1) ^ row_swz(r)) << 3) + ((kc & 1) << 2); }
 constexpr int MVAE_CONV_WSPLIT = 16;  // conv mode flag: weights hold split4_bf16 groups
 constexpr int MVAE_CONV_XSPLIT = 32;  // conv mode flag: the input activation x holds split4_bf16 groups
+constexpr int MVAE_CONV_DYSPLIT = 64;  // wgrad mode flag: the output gradient dy holds split4_bf16 groups
 
 // Exact division by a runtime constant d for 0 <= n < 2^31 (Granlund-Montgomery, N = 31):
 // q = (n * m) >> (31 + l), l = ceil(log2 d), m = floor(2^(31+l) / d) + 1 (< 2^32).
@@ -183,9 +184,19 @@ struct Img {
 
 // PREC 3: hi and lo planes (3xBF16); PREC 1: hi plane only (bf16 operands, fp32 accumulate).
 // hi = bf16(x), lo = bf16(x - hi); per element pair: 2 cvt_pk, 1 shift + 1 and (hi back to fp32), 2 sub
+// PREC 0 (exact fp32, f32-input MFMA): the planes hold the upper / lower 16 BITS of the fp32 word (a bit split,
+// not a value split), so the fragment reads and swizzles of the bf16 images serve unchanged and mma<0>
+// reassembles the exact fp32 operand
 template <int PREC>
 __device__ __forceinline__ void st_split(__bf16* img, int plane, int off, const float4& v) {
   typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
+  if constexpr (PREC == 0) {
+    const unsigned bx = __float_as_uint(v.x), by = __float_as_uint(v.y);
+    const unsigned bz = __float_as_uint(v.z), bw = __float_as_uint(v.w);
+    *(u32x2_t*)(img + off) = u32x2_t{(bx >> 16) | (by & 0xFFFF0000u), (bz >> 16) | (bw & 0xFFFF0000u)};
+    *(u32x2_t*)(img + plane + off) = u32x2_t{(bx & 0xFFFFu) | (by << 16), (bz & 0xFFFFu) | (bw << 16)};
+    return;
+  }
   const unsigned h01 = pk_bf16x2(v.x, v.y), h23 = pk_bf16x2(v.z, v.w);
   *(u32x2_t*)(img + off) = u32x2_t{h01, h23};
   if constexpr (PREC == 3) {
@@ -414,8 +425,9 @@ struct LoadConvA {
   }
 };
 
-// COL image, source element (row, k) at P[k*ld + row] (rows contiguous)
-template <int ROWS, int VEC, int NT, bool IS_A, int PREC>
+// COL image, source element (row, k) at P[k*ld + row] (rows contiguous); PRESPLIT: the source holds
+// split4_bf16 groups of 4 consecutive rows (the wgrad dY^T operand split once per conv, not per workgroup)
+template <int ROWS, int VEC, int NT, bool IS_A, int PREC, bool PRESPLIT = false>
 struct LoadColK {
   static constexpr bool COL = true;
   static constexpr int C4 = ROWS / 4;                 // float4 per k-row
@@ -446,13 +458,26 @@ struct LoadColK {
       v[i].w = bload1(rs, (kv && col + 3 < rows) ? base + 12 : OOB);
     }
   }
+  bool want_bs = true;  // A side: accumulate the row sums (conv bias gradient) -- wave-uniform
   __device__ void store_slot(__bf16* img, int i) {
     constexpr int P_ = Img<ROWS, true>::PITCH;
     const int krow = kr + i * (NT / C4);
     if (krow < BK) {
-      st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
-      if constexpr (IS_A) {
-        bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
+      if constexpr (PRESPLIT) {
+        st_presplit<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
+        if (IS_A && want_bs) {  // element value = hi + lo
+          const unsigned h01 = __float_as_uint(v[i].x), h23 = __float_as_uint(v[i].y);
+          const unsigned l01 = __float_as_uint(v[i].z), l23 = __float_as_uint(v[i].w);
+          bs[0] += __uint_as_float(h01 << 16) + __uint_as_float(l01 << 16);
+          bs[1] += __uint_as_float(h01 & 0xFFFF0000u) + __uint_as_float(l01 & 0xFFFF0000u);
+          bs[2] += __uint_as_float(h23 << 16) + __uint_as_float(l23 << 16);
+          bs[3] += __uint_as_float(h23 & 0xFFFF0000u) + __uint_as_float(l23 & 0xFFFF0000u);
+        }
+      } else {
+        st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
+        if constexpr (IS_A) {
+          bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
+        }
       }
     }
   }
@@ -619,9 +644,27 @@ __device__ __forceinline__ f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, co
 __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f32x16 mfma_f32(float a, float b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma_f32(float a, float b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
 template <int PREC, typename ACC>
 __device__ __forceinline__ void mma(ACC& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
                                     const bf16x8& bl) {
+  if constexpr (PREC == 0) {
+    // exact fp32: element j of every lane's 8-element fragment is one f32-input MFMA (k-group g of the bf16
+    // fragment layout supplies k = 8g + j: the 8 MFMAs cover the fragment's k range once, in the same lanes)
+    typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+    const u16x8 a1 = __builtin_bit_cast(u16x8, ah), a0 = __builtin_bit_cast(u16x8, al);
+    const u16x8 b1 = __builtin_bit_cast(u16x8, bh), b0 = __builtin_bit_cast(u16x8, bl);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      acc = mfma_f32(__uint_as_float(((unsigned)a1[j] << 16) | a0[j]), __uint_as_float(((unsigned)b1[j] << 16) | b0[j]),
+                     acc);
+    return;
+  }
   if constexpr (PREC == 3) {
     acc = mfma_bf16(al, bh, acc);
     acc = mfma_bf16(ah, bl, acc);
@@ -635,7 +678,7 @@ __device__ __forceinline__ int acc_row(int r, int lane) {
   else return 4 * (lane >> 4) + r;
 }
 // MFMA shape of a kernel: 32x32x16 when A is a transposed (COL) image (wgrad, attention backward)
-constexpr int mf_of(int ak) { return (ak == A_COLM || ak == A_COLM_PIX) ? 32 : 16; }
+constexpr int mf_of(int ak) { return (ak == A_COLM || ak == A_COLM_PIX || ak == A_COLM_SPLIT) ? 32 : 16; }
 
 template <int KIND, int ROWS, int VEC, int NT, bool IS_A, int PREC>
 struct Loader;
@@ -665,6 +708,10 @@ template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<7, ROWS, VEC, NT, true, PREC> : LoadConvA<ROWS, VEC, NT, MODE_FWD, PREC, true> {};
 template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<6, ROWS, VEC, NT, false, PREC> : LoadWgradX<ROWS, VEC, NT, MODE_FWD, PREC, true> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<8, ROWS, VEC, NT, true, PREC> : LoadConvA<ROWS, VEC, NT, MODE_DGRAD, PREC, true> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<9, ROWS, VEC, NT, true, PREC> : LoadColK<ROWS, VEC, NT, true, PREC, true> {};
 
 template <int BM, int BN, int WGM, int WGN, int AK, int VA, int BKIND, int VB, int PREC>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
@@ -703,6 +750,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 
   LA la;
   LB lb;
+  if constexpr (AK == A_COLM_SPLIT) la.want_bs = a.bias_ws != nullptr && tn == 0;
   la.init(a, a.A + bidx * a.sA, m0, kb, tid, bidx);
   lb.init(a, a.B + bidx * a.sB, n0, kb, tid, bidx);
 
@@ -743,13 +791,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         bh[j] = read_frag<BN, LB::COL, MF>(Bi, brow + j * MF, ks, lane);
-        if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL, MF>(Bi + IB::PLANE, brow + j * MF, ks, lane);
+        if constexpr (PREC != 1) bl[j] = read_frag<BN, LB::COL, MF>(Bi + IB::PLANE, brow + j * MF, ks, lane);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const bf16x8 ah = read_frag<BM, LA::COL, MF>(Ai, arow + i * MF, ks, lane);
         bf16x8 al{};
-        if constexpr (PREC == 3) al = read_frag<BM, LA::COL, MF>(Ai + IA::PLANE, arow + i * MF, ks, lane);
+        if constexpr (PREC != 1) al = read_frag<BM, LA::COL, MF>(Ai + IA::PLANE, arow + i * MF, ks, lane);
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           mma<PREC>(acc[i][j], ah, al, bh[j], bl[j]);
@@ -783,10 +831,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         bh[j] = read_frag<BN, LB::COL, MF>(Bi, brow + j * MF, 0, lane);
-        if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL, MF>(Bi + IB::PLANE, brow + j * MF, 0, lane);
+        if constexpr (PREC != 1) bl[j] = read_frag<BN, LB::COL, MF>(Bi + IB::PLANE, brow + j * MF, 0, lane);
       }
       ah[0] = read_frag<BM, LA::COL, MF>(Ai, arow, 0, lane);
-      if constexpr (PREC == 3) al[0] = read_frag<BM, LA::COL, MF>(Ai + IA::PLANE, arow, 0, lane);
+      if constexpr (PREC != 1) al[0] = read_frag<BM, LA::COL, MF>(Ai + IA::PLANE, arow, 0, lane);
       auto stage = [&](int st) {
 #pragma unroll
         for (int q = st * NSL / STEPS; q < (st + 1) * NSL / STEPS; ++q) {
@@ -809,7 +857,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
         if (st + 1 < STEPS) {
           const int ks1 = (st + 1) / TM, i1 = (st + 1) % TM;
           ah[cur ^ 1] = read_frag<BM, LA::COL, MF>(Ai, arow + i1 * MF, ks1, lane);
-          if constexpr (PREC == 3) al[cur ^ 1] = read_frag<BM, LA::COL, MF>(Ai + IA::PLANE, arow + i1 * MF, ks1, lane);
+          if constexpr (PREC != 1) al[cur ^ 1] = read_frag<BM, LA::COL, MF>(Ai + IA::PLANE, arow + i1 * MF, ks1, lane);
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -819,7 +867,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             bh[j] = read_frag<BN, LB::COL, MF>(Bi, brow + j * MF, 1, lane);
-            if constexpr (PREC == 3) bl[j] = read_frag<BN, LB::COL, MF>(Bi + IB::PLANE, brow + j * MF, 1, lane);
+            if constexpr (PREC != 1) bl[j] = read_frag<BN, LB::COL, MF>(Bi + IB::PLANE, brow + j * MF, 1, lane);
           }
         }
         if constexpr (!STAG) stage(st);
@@ -869,7 +917,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 
   // wgrad: the conv bias gradient (row sums of A = dY^T over this split's pixels) falls out of the
   // A staging for free; one column of tiles (tn == 0) publishes it, fixed-order reduction in LDS.
-  if constexpr (AK == A_COLM || AK == A_COLM_PIX) {
+  if constexpr (AK == A_COLM || AK == A_COLM_PIX || AK == A_COLM_SPLIT) {
     if (a.bias_ws != nullptr && tn == 0) {
       constexpr int KRN = NT / (BM / 4);
       float* red = (float*)lds;
@@ -1086,8 +1134,9 @@ __global__ void splitk_reduce_kernel(GemmArgs a);
 // ------------------------------------------------------------------------------------------
 enum { T256x256 = 0, T256x128 = 1, T128x256 = 2, T128x128 = 3, T64x64 = 4, T128x16 = 5 };
 
-// process-wide GEMM arithmetic (mvae_set_math_mode): 3xBF16 fp32 emulation (default) or bf16
-enum { MATH_3XBF16 = 0, MATH_BF16 = 1 };
+// process-wide GEMM arithmetic (mvae_set_math_mode): 3xBF16 fp32 emulation (default), bf16, or exact fp32
+// on the f32-input MFMA (v_mfma_f32_{16x16x4,32x32x2}_f32: 1/16 of the bf16 rate)
+enum { MATH_3XBF16 = 0, MATH_BF16 = 1, MATH_FP32 = 2 };
 int math_mode();
 
 inline long long tiles_of(int cfg, const GemmArgs& a) {
@@ -1131,6 +1180,8 @@ inline int choose_tile(const GemmArgs& a, bool allow_big, bool can_split) {
 }
 
 inline bool al16(const void* p);
+// pre-split (3xBF16 value-split) operands cannot feed the exact-fp32 GEMM
+inline bool split_forbidden() { return math_mode() == MATH_FP32; }
 inline bool vec_epi_disabled() {
   static int v = getenv("MVAE_NO_VEC_EPI") != nullptr;  // experiment knob: scalar epilogue everywhere
   return v != 0;
@@ -1152,8 +1203,13 @@ void launch_cfg(GemmArgs& a, hipStream_t st) {
               (!a.res || ((a.ldr & 3) == 0 && (a.sR & 3) == 0 && al16(a.res))) && (!a.bias || al16(a.bias)) &&
               !vec_epi_disabled();
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splits);
-  if (math_mode() == MATH_BF16)
+  constexpr bool presplit = AK == A_CONV_FWD_SPLIT || AK == A_CONV_DGRAD_SPLIT || AK == A_COLM_SPLIT ||
+                            BKIND == B_ROWK_SPLIT || BKIND == B_WGRAD_FWD_SPLIT;
+  const int mm = math_mode();
+  if (mm == MATH_BF16)
     hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, 1>), grid, dim3(64 * WGM * WGN), 0, st, a);
+  else if (mm == MATH_FP32 && !presplit)  // (pre-split operands are value splits: never launched in this mode)
+    hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, 0>), grid, dim3(64 * WGM * WGN), 0, st, a);
   else
     hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, 3>), grid, dim3(64 * WGM * WGN), 0, st, a);
 }

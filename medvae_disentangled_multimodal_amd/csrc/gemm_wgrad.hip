@@ -65,9 +65,18 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
                            int wd, int cin, int cout, int kh, int kw, int stride, int pad_t,
                            int pad_l, int ho, int wo, int mode, float* workspace,
                            size_t workspace_bytes, void* stream) {
-  const bool xsplit = (mode & MVAE_CONV_XSPLIT) != 0;  // x holds split4_bf16 groups
-  mode &= ~MVAE_CONV_XSPLIT;
+  const bool xsplit = (mode & MVAE_CONV_XSPLIT) != 0;   // x holds split4_bf16 groups
+  const bool dysplit = (mode & MVAE_CONV_DYSPLIT) != 0;  // dy holds split4_bf16 groups
+  mode &= ~(MVAE_CONV_XSPLIT | MVAE_CONV_DYSPLIT);
+  if (dysplit && (cout % 4 != 0 || !al16(dy))) {
+    set_error("wgrad: a pre-split dy needs cout %% 4 == 0, 16-B alignment");
+    return MVAE_EINVAL;
+  }
   if (mode != 0 && mode != 1) { set_error("wgrad: mode must be 0 or 1"); return MVAE_EINVAL; }
+  if ((xsplit || dysplit) && split_forbidden()) {
+    set_error("wgrad: pre-split operands are not allowed in the exact-fp32 math mode");
+    return MVAE_EINVAL;
+  }
   if (xsplit && (mode != 0 || cin % 4 != 0 || !al16(x))) {
     set_error("wgrad: a pre-split x needs mode 0, cin %% 4 == 0, 16-B alignment");
     return MVAE_EINVAL;
@@ -100,7 +109,13 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
     plan_splits(a, cfg, workspace, workspace_bytes - bias_bytes);
     // bias partials live after the split-K partials
     a.bias_ws = dbias ? (float*)((char*)workspace + ((splitk_ws_bytes(a) + 255) & ~(size_t)255)) : nullptr;
-    if (xsplit) {
+    if (dysplit) {
+      if (xsplit) launch_big<A_COLM_SPLIT, 4, B_WGRAD_FWD_SPLIT, 4>(a, st, cfg);
+      else if (mode == 0 && vb) launch_big<A_COLM_SPLIT, 4, B_WGRAD_FWD, 4>(a, st, cfg);
+      else if (mode == 0) launch_small<A_COLM_SPLIT, 4, B_WGRAD_FWD, 1>(a, st, cfg);
+      else if (vb) launch_big<A_COLM_SPLIT, 4, B_WGRAD_UPS, 4>(a, st, cfg);
+      else launch_small<A_COLM_SPLIT, 4, B_WGRAD_UPS, 1>(a, st, cfg);
+    } else if (xsplit) {
       if (va) launch_big<A_COLM, 4, B_WGRAD_FWD_SPLIT, 4>(a, st, cfg);
       else launch_small<A_COLM, 1, B_WGRAD_FWD_SPLIT, 4>(a, st, cfg);
     } else if (mode == 0) {

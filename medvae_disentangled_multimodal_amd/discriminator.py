@@ -4,7 +4,8 @@ Mirrors src/models/discriminator.py:11-82 -- same constructor kwargs (input_nc, 
 use_actnorm), the same `main` Sequential and therefore the same state-dict names
 (`main.0.weight`, `main.3.running_mean`, ...): 4x4 convs (stride 2 ... 2, 1, 1; padding 1) on the
 implicit-GEMM kernel, BatchNorm2d fused with the in-place LeakyReLU(0.2) that follows it
-(csrc/disc.hip), the first LeakyReLU as its own kernel.
+(csrc/disc.hip), the first LeakyReLU as its own kernel. The convolutions run in exact fp32 (f32-input MFMA)
+by default: see NLayerDiscriminator.__init__.
 """
 from __future__ import annotations
 
@@ -56,9 +57,15 @@ class _Fused(nn.Module):
 
 
 class NLayerDiscriminator(nn.Module):
-    def __init__(self, input_nc: int = 3, ndf: int = 64, n_layers: int = 3, use_actnorm: bool = False):
+    def __init__(self, input_nc: int = 3, ndf: int = 64, n_layers: int = 3, use_actnorm: bool = False,
+                 exact_fp32: bool = True):
+        """exact_fp32: the discriminator's convolutions run on the exact f32-input MFMA whatever the trainer's
+        precision (its BatchNorm backward removes the per-channel mean of near-constant hinge gradients, which
+        amplifies the 3xBF16 operand rounding of the layer above by ~300x: 3.6e-3 relative on main.0's
+        gradient vs 1e-5 in exact fp32; tests/test_gpu_adversarial.py)."""
         super().__init__()
         self.n_layers = n_layers
+        self.exact_fp32 = exact_fp32
         kw, padw = 4, 1
         use_bias = not use_actnorm
 
@@ -83,4 +90,5 @@ class NLayerDiscriminator(nn.Module):
         self.main = nn.Sequential(*seq)
 
     def forward(self, input: torch.Tensor) -> torch.Tensor:
-        return self.main(input)
+        with ops.math_scope(2 if self.exact_fp32 else None):
+            return self.main(input)

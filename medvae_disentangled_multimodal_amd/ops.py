@@ -178,10 +178,48 @@ WEIGHT_SPLIT = os.environ.get("MVAE_NO_WEIGHT_SPLIT") is None
 SMALL_COUT_WGRAD = os.environ.get("MVAE_NO_SMALL_COUT_WGRAD") is None
 MVAE_CONV_WSPLIT = 16
 MVAE_CONV_XSPLIT = 32
+MVAE_CONV_DYSPLIT = 64
+# the output gradient of a conv split once into 3xBF16 hi/lo groups (mvae_split_bf16) and handed pre-split to
+# both of its GEMMs (input gradient: gathered A operand; weight gradient: dY^T A operand). Off by default: measured
+# on c4 (same box, interleaved) the dgrad GEMMs gain 2.5 % but the wgrad GEMMs lose 2.5 % and the split pass
+# (8 B/elem over every conv's dy, ~13 ms/step) outweighs the rest (441 -> 433 img/s). MVAE_DY_SPLIT=1 enables it.
+DY_SPLIT = os.environ.get("MVAE_DY_SPLIT") is not None
+DY_SPLIT_MIN = 1 << 18  # elements: below this the extra launch outweighs the staging work saved
 
 
 def _al16(*ts) -> bool:
     return all(t.data_ptr() % 16 == 0 for t in ts)
+
+
+# current GEMM arithmetic (mirror of mvae_get_math_mode, kept by set_precision / math_scope): 0 = 3xBF16,
+# 1 = bf16, 2 = exact fp32 (f32-input MFMA). The 3xBF16 pre-split operand layouts are value splits and are
+# not used in the exact mode.
+_MATH = [0]
+
+
+def _splits_ok() -> bool:
+    return _MATH[0] != 2
+
+
+class math_scope:
+    """Run the enclosed launches in GEMM math mode `mode` (a module whose convolutions must run in a fixed
+    arithmetic whatever the trainer precision, e.g. the discriminator in exact fp32)."""
+
+    def __init__(self, mode: Optional[int]):
+        self.mode = mode
+
+    def __enter__(self):
+        self.prev = _MATH[0]
+        if self.mode is not None and self.mode != self.prev:
+            _lib.call("mvae_set_math_mode", int(self.mode))
+            _MATH[0] = int(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        if _MATH[0] != self.prev:
+            _lib.call("mvae_set_math_mode", int(self.prev))
+            _MATH[0] = self.prev
+        return False
 
 
 def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part=None):
@@ -195,7 +233,7 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
     sub = _subpixel_upsample(g)
     alg = ref * 4 / 9 if sub else ref
     st = _stream(x)
-    split = WEIGHT_SPLIT and c % 4 == 0 and _al16(x) and not g.pointwise
+    split = WEIGHT_SPLIT and _splits_ok() and c % 4 == 0 and _al16(x) and not g.pointwise
     if x_split and (g.pointwise or g.upsample or c % 4 or not _al16(x)):
         raise RuntimeError("conv2d: a pre-split input needs a non-pointwise, non-upsample conv with cin % 4 == 0")
     wg = w
@@ -224,9 +262,20 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
     return y
 
 
-def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None):
+def split_dy(dy: torch.Tensor) -> Optional[torch.Tensor]:
+    """dy in the 3xBF16 operand layout (split4_bf16 groups), or None when the conv cannot use it."""
+    if not DY_SPLIT or not _splits_ok() or dy.dim() != 4 or dy.shape[1] % 4 or dy.numel() < DY_SPLIT_MIN or not _al16(dy) or \
+            not dy.is_contiguous(memory_format=CL):
+        return None
+    ds = torch.empty_like(dy, memory_format=CL)
+    _lib.call("mvae_split_bf16", dy.data_ptr(), ds.data_ptr(), dy.numel(), _stream(dy))
+    return ds
+
+
+def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None):
     """gn_link (GnBwdLink): the conv's input was silu?(GroupNorm(x)) -- also emit that GroupNorm's backward
-    partials from the GEMM epilogue (mvae_conv2d_dgrad_gnbwd_nhwc) into gn_link.part when the launch allows it."""
+    partials from the GEMM epilogue (mvae_conv2d_dgrad_gnbwd_nhwc) into gn_link.part when the launch allows it.
+    dys: dy pre-split by split_dy (same values; used as the gathered GEMM operand when given)."""
     n, c, h, wd = x_shape
     co = w.shape[0]
     _, _, ho, wo = dy.shape
@@ -234,16 +283,20 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None):
     st = _stream(dy)
     flops = 2.0 * n * ho * wo * co * c * g.kh * g.kw  # reference count
     shp = (n, c, h, wd, co, g.kh, g.stride, g.upsample)
+    if dys is not None and (g.pointwise or co % 4):
+        dys = None
+    dya = dy if dys is None else dys
     if gn_link is not None and gn_link.usable(dx) and not g.pointwise and not g.upsample and g.stride == 1 and \
             co % 4 == 0 and _al16(dy, dx):
-        split = WEIGHT_SPLIT
+        split = WEIGHT_SPLIT and _splits_ok()
         wt = ARENA.get("wt", c * g.kh * g.kw * co * 4, dy.device)
         _lib.call("mvae_conv_weight_transpose", w.data_ptr(), wt.data_ptr(), co, g.kh, g.kw, c, int(split), st)
         part = torch.empty(n * h * wd // 32 * c * 2, device=dy.device, dtype=torch.float64)
         L = gn_link
+        flags = int(split) | (2 if dys is not None else 0)
         with _timed("conv_dgrad", flops, shp):
-            _lib.call("mvae_conv2d_dgrad_gnbwd_nhwc", dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, ho, wo, co, c,
-                      g.kh, g.kw, g.pad_t, g.pad_l, h, wd, int(split), L.x.data_ptr(), L.mean.data_ptr(),
+            _lib.call("mvae_conv2d_dgrad_gnbwd_nhwc", dya.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, ho, wo, co, c,
+                      g.kh, g.kw, g.pad_t, g.pad_l, h, wd, flags, L.x.data_ptr(), L.mean.data_ptr(),
                       L.rstd.data_ptr(), L.gamma.data_ptr(), L.beta.data_ptr(), L.groups, L.silu, part.data_ptr(), st)
         L.part, L.dx = part, dx
         return dx
@@ -254,44 +307,46 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None):
                       0, 0.0, dx.data_ptr(), c, 0, 1, None, None, 0, 0, None, 0, st)
         return dx
     # the dgrad GEMM's K runs over cout: transposed weights [cin][taps][cout], pre-split when cout % 4 == 0
-    split = WEIGHT_SPLIT and co % 4 == 0 and _al16(dy)
+    split = WEIGHT_SPLIT and _splits_ok() and co % 4 == 0 and _al16(dy)
     wflag = MVAE_CONV_WSPLIT if split else 0
+    xflag = MVAE_CONV_XSPLIT if dys is not None else 0
     if g.upsample:
         wt = ARENA.get("wt", c * 16 * co * 4, dy.device)
         _lib.call("mvae_conv_weight_upsample_dgrad", w.data_ptr(), wt.data_ptr(), co, c, int(split), st)
         # dX = stride-2, pad-1 4x4 conv of dY with the tap-summed kernel (16 taps per low-res pixel)
         with _timed("conv_dgrad", flops * 4 / 9, shp, flops):
-            _lib.call("mvae_conv2d_nhwc", dy.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
-                      4, 4, 2, 1, 1, h, wd, wflag, st)
+            _lib.call("mvae_conv2d_nhwc", dya.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
+                      4, 4, 2, 1, 1, h, wd, wflag | xflag, st)
         return dx
     wt = ARENA.get("wt", c * g.kh * g.kw * co * 4, dy.device)
     _lib.call("mvae_conv_weight_transpose", w.data_ptr(), wt.data_ptr(), co, g.kh, g.kw, c, int(split), st)
     if g.stride == 2 and h % 2 == 0 and wd % 2 == 0 and g.kh <= 4 and g.kw <= 4 and STRIDE2_CLASSES:
         # Downsample's input gradient by dx parity class: only the useful taps (no stride holes)
         wc = ARENA.get("wcls", c * g.kh * g.kw * co * 4, dy.device)
+        flags = int(split) | (2 if dys is not None else 0)
         with _timed("conv_dgrad", flops, shp):
-            _lib.call("mvae_conv2d_dgrad_stride2_nhwc", dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, h, wd, c, co,
-                      g.kh, g.kw, g.pad_t, g.pad_l, ho, wo, int(split), wc.data_ptr(), wc.numel(), st)
+            _lib.call("mvae_conv2d_dgrad_stride2_nhwc", dya.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, h, wd, c, co,
+                      g.kh, g.kw, g.pad_t, g.pad_l, ho, wo, flags, wc.data_ptr(), wc.numel(), st)
         return dx
     with _timed("conv_dgrad", flops, shp):
-        _lib.call("mvae_conv2d_nhwc", dy.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
-                  g.kh, g.kw, g.stride, g.pad_t, g.pad_l, h, wd, 2 | wflag, st)
+        _lib.call("mvae_conv2d_nhwc", dya.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
+                  g.kh, g.kw, g.stride, g.pad_t, g.pad_l, h, wd, 2 | wflag | xflag, st)
     return dx
 
 
-def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool = False):
+def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool = False, dys=None):
     """dw (+ db when given and the conv is not pointwise) accumulate with `beta`. Returns True when
-    the bias gradient was produced by the fused wgrad kernel."""
+    the bias gradient was produced by the fused wgrad kernel. dys: dy pre-split by split_dy."""
     n, c, h, wd = x.shape
     co = dy.shape[1]
     _, _, ho, wo = dy.shape
     ref = 2.0 * n * ho * wo * co * c * g.kh * g.kw
     alg = ref * 4 / 9 if _subpixel_upsample(g) else ref
     with _timed("conv_wgrad", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
-        return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db, x_split)
+        return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db, x_split, dys)
 
 
-def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_split=False):
+def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_split=False, dys=None):
     st = _stream(dy)
     if x_split and (g.pointwise or g.upsample):
         raise RuntimeError("conv2d wgrad: a pre-split input needs a non-pointwise, non-upsample conv")
@@ -320,7 +375,11 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
     nbytes = _lib.query("mvae_conv2d_wgrad_workspace_bytes", n, c, co, g.kh, g.kw, ho, wo)
     ws = ARENA.get("ws", nbytes, dy.device)
     mode = (1 if g.upsample else 0) | (MVAE_CONV_XSPLIT if x_split else 0)
-    _lib.call("mvae_conv2d_wgrad_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db), float(beta), n, h, wd,
+    dya = dy
+    if dys is not None and co % 4 == 0:
+        mode |= MVAE_CONV_DYSPLIT
+        dya = dys
+    _lib.call("mvae_conv2d_wgrad_nhwc", dya.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db), float(beta), n, h, wd,
               c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, mode, ws.data_ptr(), ws.numel(), st)
     return db is not None
 
@@ -371,6 +430,7 @@ class Conv2dFn(torch.autograd.Function):
         w = _krsc(weight)
         res = nhwc(residual) if residual is not None else None
         y = conv2d_forward_raw(x, w, bias, res, geom, xs, gn_part)
+        ctx.math = _MATH[0]  # the backward GEMMs run in the forward's arithmetic
         ctx.geom = geom
         ctx.x_split = xs
         ctx.has_bias = bias is not None
@@ -384,6 +444,11 @@ class Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        with math_scope(ctx.math):
+            return Conv2dFn._backward(ctx, dy)
+
+    @staticmethod
+    def _backward(ctx, dy):
         x, w = ctx.saved_tensors
         g = ctx.geom
         dy = nhwc(dy)
@@ -391,8 +456,9 @@ class Conv2dFn(torch.autograd.Function):
         link = ctx.gn_link
         if link is not None:
             link.part = link.dx = None  # partials of an earlier pass are never reused
+        dys = split_dy(dy) if not g.pointwise and not _subpixel_upsample(g) else None
         if ctx.needs_input_grad[0]:
-            dx = conv2d_dgrad_raw(dy, w, x.shape, g, link if ctx.x_sink is None else None)
+            dx = conv2d_dgrad_raw(dy, w, x.shape, g, link if ctx.x_sink is None else None, dys=dys)
             if ctx.x_sink is not None and ctx.x_sink.park(dx):
                 dx = None
         bias_done = False
@@ -402,12 +468,12 @@ class Conv2dFn(torch.autograd.Function):
             btgt = _main_grad(ctx.bias_ref) if want_b else None
             xs = ctx.x_split
             if tgt is not None and (not want_b or btgt is not None):
-                bias_done = conv2d_wgrad_raw(dy, x, tgt, 1.0, g, btgt, x_split=xs)
+                bias_done = conv2d_wgrad_raw(dy, x, tgt, 1.0, g, btgt, x_split=xs, dys=dys)
             elif tgt is not None:
-                conv2d_wgrad_raw(dy, x, tgt, 1.0, g, x_split=xs)
+                conv2d_wgrad_raw(dy, x, tgt, 1.0, g, x_split=xs, dys=dys)
             else:
                 dw_ret = torch.empty_like(w, memory_format=CL)
-                conv2d_wgrad_raw(dy, x, dw_ret, 0.0, g, x_split=xs)
+                conv2d_wgrad_raw(dy, x, dw_ret, 0.0, g, x_split=xs, dys=dys)
         if ctx.has_bias and ctx.needs_input_grad[2] and not bias_done:
             tgt = _main_grad(ctx.bias_ref)
             n, co, ho, wo = dy.shape
@@ -572,7 +638,7 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
     """for_conv=True: the caller feeds the result straight into ops.conv2d (3x3/stride-1, C % 4 == 0) -- the
     output is then written pre-split for the GEMM (GroupNorm -> conv is the ResnetBlock / norm_out pattern,
     encoder_decoder.py:141-163, :318-328)."""
-    split = bool(for_conv and ACT_SPLIT and x.shape[1] % 4 == 0)
+    split = bool(for_conv and ACT_SPLIT and _splits_ok() and x.shape[1] % 4 == 0)
     part = getattr(x, GN_PART_ATTR, None)
     if part is not None:
         delattr(x, GN_PART_ATTR)  # consumed once; frees the statistics with the next allocation cycle
@@ -614,10 +680,16 @@ class AttnCoreFn(torch.autograd.Function):
         _gemm(0, 0, n, c, n, 1.0, s, n, n * n, v, c, n * c, 0.0, o, c, n * c, b, st)
         ctx.save_for_backward(q, k, v, s)
         ctx.scale = scale
+        ctx.math = _MATH[0]
         return o
 
     @staticmethod
     def backward(ctx, do):
+        with math_scope(ctx.math):
+            return AttnCoreFn._backward(ctx, do)
+
+    @staticmethod
+    def _backward(ctx, do):
         q, k, v, p = ctx.saved_tensors
         do = nhwc(do)
         b, c, h, w = q.shape
@@ -820,23 +892,27 @@ def l1_mean(a, b):
 # ------------------------------------------------------------------------------------------
 # GEMM arithmetic (trainer precision)
 # ------------------------------------------------------------------------------------------
-_PRECISION = {"32": 0, "32-true": 0, "fp32": 0, 32: 0, "bf16": 1, "bf16-mixed": 1, "bf16-true": 1}
+_PRECISION = {"32": 0, "32-true": 0, "fp32": 0, 32: 0, "bf16": 1, "bf16-mixed": 1, "bf16-true": 1,
+              "32-exact": 2, "fp32-exact": 2}
 
 
 def set_precision(precision) -> int:
     """Map the reference trainer's `precision` flag onto the GEMM arithmetic of every following
     conv/bmm launch: "32" -> 3xBF16 fp32 emulation, "bf16-mixed" -> bf16 operands with fp32
-    accumulation (what autocast runs these ops in). Returns the previous mode."""
+    accumulation (what autocast runs these ops in), "32-exact" -> exact fp32 on the f32-input MFMA
+    (parity mode, 1/5 of the 3xBF16 rate). Returns the previous mode."""
     if precision not in _PRECISION:
         raise ValueError(f"precision {precision!r} is not supported on the MI355X path "
                          f"(supported: {sorted(map(str, _PRECISION))})")
     prev = _lib.query("mvae_get_math_mode")
     _lib.call("mvae_set_math_mode", _PRECISION[precision])
+    _MATH[0] = _PRECISION[precision]
     return prev
 
 
 def restore_math_mode(mode: int):
     _lib.call("mvae_set_math_mode", int(mode))
+    _MATH[0] = int(mode)
 
 
 # ------------------------------------------------------------------------------------------

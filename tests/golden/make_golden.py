@@ -40,7 +40,7 @@ from torch.distributions import kl_divergence  # noqa: E402
 
 import src.models as ref_models  # noqa: E402  (the reference)
 from cases import CASES, FULL_GRADS  # noqa: E402
-from weights import synth_state, state_checksum  # noqa: E402
+from weights import synth_param, synth_state, state_checksum  # noqa: E402
 
 
 @contextlib.contextmanager
@@ -192,6 +192,66 @@ def run_case(name, case):
           f"kl={float(ld['kl_loss']):.8f} |g|={float(total_norm):.6f}")
 
 
+DISC_FULL = ["main.0.weight", "main.0.bias", "main.3.weight", "main.3.bias", "main.11.weight", "main.11.bias"]
+
+
+def disc_case():
+    """Adversarial branch pinned on the reference's own NLayerDiscriminator (src/models/discriminator.py:11-82,
+    default config: input_nc 3, ndf 64, n_layers 3, BatchNorm) in train mode, with the generator / discriminator
+    objective arithmetic of LPIPSWithDiscriminator (src/losses/vae_losses.py:297-382; src.losses itself needs
+    lpips, so its few torch calls are restated): g_loss = -mean(D(rec)), the adaptive weight
+    |dNLL/dW| / (|dG/dW| + 1e-4) clamped to [0, 1e4] w.r.t. the last decoder layer W (here a conv3x3 8 -> 3
+    producing rec; NLL = mse(rec, x) stands in for the perceptual term), and the hinge loss
+    0.5 * (mean(relu(1 - D(x))) + mean(relu(1 + D(rec.detach())))). Three train-mode forwards in the training
+    step's order (generator D(rec), then D(x), D(rec)) update the BatchNorm running statistics three times."""
+    torch.manual_seed(0)
+    D = ref_models.NLayerDiscriminator(input_nc=3, ndf=64, n_layers=3)
+    D.train()
+    named = [(k, tuple(v.shape)) for k, v in D.named_parameters()]
+    state = synth_state(named)
+    with torch.no_grad():
+        for k, p in D.named_parameters():
+            p.copy_(torch.from_numpy(state[k]))
+    rng = np.random.Generator(np.random.PCG64(77))
+    x = torch.from_numpy((rng.random((2, 3, 64, 64)) * 2 - 1).astype(np.float32))
+    feat = torch.from_numpy(rng.standard_normal((2, 8, 64, 64)).astype(np.float32))
+    w_last = torch.from_numpy(synth_param("last.weight", (3, 8, 3, 3))).requires_grad_()
+    b_last = torch.from_numpy(synth_param("last.bias", (3,))).requires_grad_()
+    rec = F.conv2d(feat, w_last, b_last, padding=1)
+    nll = F.mse_loss(rec, x)
+    logits_g = D(rec)
+    g_loss = -torch.mean(logits_g)
+    nll_grads = torch.autograd.grad(nll, w_last, retain_graph=True)[0]
+    g_grads = torch.autograd.grad(g_loss, w_last, retain_graph=True)[0]
+    d_weight = torch.clamp(torch.norm(nll_grads) / (torch.norm(g_grads) + 1e-4), 0.0, 1e4).detach()
+    D.zero_grad()
+    logits_real = D(x.detach())
+    logits_fake = D(rec.detach())
+    d_loss = 0.5 * (torch.mean(F.relu(1.0 - logits_real)) + torch.mean(F.relu(1.0 + logits_fake)))
+    d_loss.backward()
+    rec_arr = {"in.x": x.numpy(), "in.feat": feat.numpy(), "out.rec": rec.detach().numpy(),
+               "out.logits_g": logits_g.detach().numpy(),
+               "out.logits_real": logits_real.detach().numpy(), "out.logits_fake": logits_fake.detach().numpy(),
+               "loss.g_loss": np.array(float(g_loss)), "loss.nll": np.array(float(nll)),
+               "loss.d_weight": np.array(float(d_weight)), "loss.d_loss": np.array(float(d_loss)),
+               "grad.nll_last": nll_grads.numpy(), "grad.g_last": g_grads.numpy()}
+    for k, p in D.named_parameters():
+        g = p.grad.double()
+        rec_arr[f"gradsum.{k}"] = np.array([float(g.sum()), float((g * g).sum())])
+        if k in DISC_FULL:
+            rec_arr[f"grad.{k}"] = p.grad.numpy().copy()
+    for k, b in D.named_buffers():
+        if b.is_floating_point():
+            rec_arr[f"buf.{k}"] = b.numpy().copy()
+    np.savez(os.path.join(HERE, "disc.npz"), **rec_arr)
+    meta = dict(params=[[k, list(s)] for k, s in named], weight_checksum=state_checksum(state),
+                config=dict(input_nc=3, ndf=64, n_layers=3), full_grads=DISC_FULL,
+                reference="parsakzr/medvae-disentangled-multimodal @ 2025-08-24", torch=torch.__version__)
+    with open(os.path.join(HERE, "disc.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print(f"disc: g_loss={float(g_loss):.8f} d_weight={float(d_weight):.6f} d_loss={float(d_loss):.8f}")
+
+
 def known_answer_anchor():
     """SURVEY.md section 8(c) known-answer anchor, run on the reference itself."""
     torch.manual_seed(0)
@@ -212,7 +272,10 @@ def known_answer_anchor():
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    sel = sys.argv[1:] or list(CASES)
+    sel = sys.argv[1:] or list(CASES) + ["disc"]
     for n in sel:
-        run_case(n, CASES[n])
+        if n == "disc":
+            disc_case()
+        else:
+            run_case(n, CASES[n])
     known_answer_anchor()

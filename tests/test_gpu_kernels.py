@@ -115,6 +115,74 @@ def test_conv_fwd_dgrad_wgrad(dev, case):
     assert float((bm._mvae_main_grad.cpu().double() - 0.25 - db_ref).abs().max()) < 1e-5 * scale
 
 
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[2] % 4 == 0 and not (c[5] == 1 and c[6] == 1) and not c[8]])
+def test_conv_backward_with_presplit_dy(dev, case, monkeypatch):
+    """The conv's output gradient handed to both backward GEMMs pre-split (ops.split_dy -> dgrad A operand with
+    MVAE_CONV_XSPLIT / stride-2 classes / upsample 4x4 form, wgrad dY^T operand with MVAE_CONV_DYSPLIT and the
+    fused bias sums from hi + lo): the same tolerances as the fp32-operand path, on every geometry."""
+    from medvae_disentangled_multimodal_amd import ops
+    monkeypatch.setattr(ops, "DY_SPLIT_MIN", 0)
+    monkeypatch.setattr(ops, "DY_SPLIT", True)
+    seen = []
+    orig = ops._lib.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return orig(name, *args)
+    monkeypatch.setattr(ops._lib, "call", spy)
+    test_conv_fwd_dgrad_wgrad(dev, case)
+    assert "mvae_split_bf16" in seen
+
+
+@pytest.mark.parametrize("case", CONV_CASES[:14] + CONV_CASES[18:22])
+def test_conv_exact_fp32_mode(dev, case):
+    """Math mode 2 (the trainer's precision "32-exact"; the discriminator's default): every conv GEMM on the
+    f32-input MFMA -- fwd / dgrad / wgrad agree with float64 to fp32 accumulation error (5e-6 norm-wise; the
+    3xBF16 path sits at 1e-5..3e-5), and no pre-split operand is formed."""
+    from medvae_disentangled_multimodal_amd import ops
+    n, ci, co, h, w, k, s, pads, ups = case
+    g = torch.Generator().manual_seed(5 + hash(case) % 1000)
+    x = torch.randn(n, ci, h, w, generator=g)
+    wt = torch.randn(co, ci, k, k, generator=g) / math.sqrt(ci * k * k)
+    b = torch.randn(co, generator=g) * 0.1
+    xr, wr, br = x.double().requires_grad_(), wt.double().requires_grad_(), b.double().requires_grad_()
+    yr = torch_conv(xr, wr, br, s, pads, ups)
+    gy = torch.randn(yr.shape, generator=g)
+    yr.backward(gy.double())
+    geom = ops.ConvGeom(k, k, s, pads[0], pads[1], pads[2], pads[3], ups)
+    with ops.math_scope(2):
+        xd = cl(x, dev).requires_grad_()
+        wd = cl(wt, dev).requires_grad_()
+        bd = b.to(dev).requires_grad_()
+        yd = ops.conv2d(xd, wd, bd, geom)
+        yd.backward(cl(gy, dev))
+    assert ops._MATH[0] == 0
+    assert rel(yd, yr) < 5e-6
+    assert rel(xd.grad, xr.grad) < 5e-6
+    assert rel(wd.grad, wr.grad) < 5e-6
+    assert rel(bd.grad, br.grad) < 5e-6
+
+
+def test_attention_gemm_exact_fp32_mode(dev):
+    from medvae_disentangled_multimodal_amd import ops
+    g = torch.Generator().manual_seed(2)
+    q, k_, v = (torch.randn(4, 64, 8, 8, generator=g) for _ in range(3))
+    qr, kr, vr = (t.double().requires_grad_() for t in (q, k_, v))
+    b, c, hh, ww = q.shape
+    qq, kk, vv = (t.reshape(b, c, hh * ww).permute(0, 2, 1) for t in (qr, kr, vr))
+    p = torch.softmax(qq @ kk.transpose(1, 2) * c ** -0.5, dim=2)
+    o_r = (p @ vv).permute(0, 2, 1).reshape(b, c, hh, ww)
+    go = torch.randn(o_r.shape, generator=g)
+    o_r.backward(go.double())
+    with ops.math_scope(2):
+        qd, kd, vd = (cl(t, dev).requires_grad_() for t in (q, k_, v))
+        o = ops.attention_core(qd, kd, vd)
+        o.backward(cl(go, dev))
+    assert rel(o, o_r) < 5e-6
+    for a, r in ((qd, qr), (kd, kr), (vd, vr)):
+        assert rel(a.grad, r.grad) < 5e-6
+
+
 def test_split_bf16_layout(dev):
     """mvae_split_bf16: per 4 fp32 values hi0..hi3 lo0..lo3 (bf16), hi = RNE(x), lo = RNE(x - hi)."""
     from medvae_disentangled_multimodal_amd import _lib
