@@ -82,9 +82,12 @@ HBM_PEAK_GBS = 8000.0
 def _pmc_traffic(config):
     """HBM bytes per gemm3x_kernel launch from the committed PMC passes (tools/pmc_traffic.sh:
     FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc, separate passes) -- counters cannot be read inside
-    this timed run, so the profile of the same command is attached."""
-    path = os.path.join(ROOT, "profiles", f"r01_{config}_gemm_traffic.json")
-    if not os.path.exists(path):
+    this timed run, so the profile of the same command is attached (newest round first)."""
+    for tag in ("r02", "r01"):
+        path = os.path.join(ROOT, "profiles", f"{tag}_{config}_gemm_traffic.json")
+        if os.path.exists(path):
+            break
+    else:
         return None
     with open(path) as f:
         t = json.load(f)
@@ -92,6 +95,18 @@ def _pmc_traffic(config):
             "fetch_bytes_per_launch": round(t["fetch_bytes_per_launch"]),
             "write_bytes_per_launch": round(t["write_bytes_per_launch"]), "launches": t["launches"],
             "source": os.path.relpath(path, ROOT)}
+
+
+def gemm_algorithmic_bytes(tag, shape):
+    """Operand + output bytes of one GEMM-family launch if every operand were read once and the output written
+    once (fp32): conv passes from the layer shape (n, cin, h, w, cout, k, stride, upsample), attention products
+    from (m, n, k, batch)."""
+    if tag == "attn_gemm":
+        m, n, k, b = shape
+        return 4.0 * b * (m * k + k * n + m * n)
+    n, c, h, w, co, k, stride, ups = shape
+    ho, wo = (2 * h, 2 * w) if ups else (h // stride, w // stride) if stride > 1 else (h, w)
+    return 4.0 * (n * h * w * c + co * k * k * c + n * ho * wo * co)
 
 
 def make_batch(cfg, device, gen):
@@ -272,11 +287,13 @@ def main():
             d[1] += f
             d[2] += s.elapsed_time(e)
         ach = tot_fl / (tot_ms * 1e-3) / 1e12
+        alg_bytes = sum(gemm_algorithmic_bytes(r[0], r[4]) for r in rec) / max(len(rec), 1)
         peak = BF16_DENSE_PEAK_TF if bf16 else PEAK_3XBF16_TF
         roofline = {"bound": "mfma", "kernel": "gemm3x_kernel (implicit-GEMM conv + attention bmm, all launches)",
                     "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                     "frac": round(ach / peak, 4), "traffic": (_pmc_traffic(args.config) or {}).get("bytes_per_launch"),
                     "traffic_unit": "HBM bytes per launch (PMC)", "traffic_detail": _pmc_traffic(args.config),
+                    "algorithmic_bytes_per_launch": round(alg_bytes),
                     "peak_note": ("bf16 dense MFMA peak 2.5 PF/s (bf16 operands, fp32 accumulate)" if bf16 else
                                   "3xBF16 fp32-emulation ceiling = bf16 dense MFMA 2.5 PF/s / 3; "
                                   "native fp32 MFMA peak is 157.3 TF/s"),

@@ -5,6 +5,7 @@ wide streaming reads -> x2; WRITE_SIZE is exact for 16-B/lane stores. Both are r
 import csv, glob, json, os, sys
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c4"
+tag = sys.argv[2] if len(sys.argv) > 2 else "r02"
 root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 
 
@@ -26,6 +27,6 @@ out = {"config": cfg, "kernel": "gemm3x_kernel", "launches": n, "fetch_bytes_per
        "write_bytes_per_launch": wb, "traffic_bytes_per_launch": fb + wb,
        "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, kernel-trace only) over one "
                  "training step; FETCH_SIZE x2 (gfx950 wide-read correction), KB -> bytes"}
-dst = os.path.join(root, "profiles", f"r01_{cfg}_gemm_traffic.json")
+dst = os.path.join(root, "profiles", f"{tag}_{cfg}_gemm_traffic.json")
 json.dump(out, open(dst, "w"), indent=1)
 print(json.dumps(out))

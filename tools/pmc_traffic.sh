@@ -10,4 +10,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
     --output-format csv -- python bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline --no-kernel-timing \
     > gpurun_out/traffic_${CFG}_$C.log 2>&1
 done
-python3 tools/pmc_traffic.py $CFG
+python3 tools/pmc_traffic.py $CFG ${2:-r02}
