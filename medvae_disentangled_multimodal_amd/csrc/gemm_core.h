@@ -1163,6 +1163,11 @@ inline int tile_override() {
   return v;
 }
 
+inline bool tile_rule_legacy() {  // experiment knob: MVAE_TILE_LEGACY=1 restores the >= 240-tiles rule
+  static int v = getenv("MVAE_TILE_LEGACY") != nullptr;
+  return v != 0;
+}
+
 inline int choose_tile(const GemmArgs& a, bool allow_big, bool can_split) {
   const int ov = tile_override();
   if (ov >= 0 && ov <= 4 && (allow_big || ov >= T128x128)) return ov;
@@ -1170,6 +1175,27 @@ inline int choose_tile(const GemmArgs& a, bool allow_big, bool can_split) {
   // skinny N (Decoder.conv_out forward, cout 3; Encoder.conv_in input gradient, cin 6): 128x16 tiles on
   // 2 waves instead of 64-wide tiles that are 95 % padding
   if (allow_big && a.N <= 16 && tiles_of(T128x16, a) >= 512) return T128x16;
+  if (allow_big && !can_split && !tile_rule_legacy()) {
+    // Cost model over the tile configs (fwd / dgrad / batched GEMMs; split-K GEMMs keep the rule below):
+    // time ~ rounds x (tiles resident per CU) x tile area / per-tile efficiency, with rounds =
+    // ceil(tiles / (256 CUs x tiles resident per CU)). Efficiencies are the measured full-chip rates of each
+    // tile relative to 256x256 (tools/tile_sweep.py, c4 shapes: 256x256 1.0, 256x128 / 128x256 0.82,
+    // 128x128 0.70, 64x64 0.50); residency from LDS (160, 120, 120, 80, 40 KB per workgroup). The rule it
+    // replaces (largest tile with >= 240 tiles) lost 18-65 % on the c2 / c3 layers (7x7 and 14x14 at 256-512
+    // channels; 32-64 channels at 14x14-28x28).
+    static const double eff[5] = {1.0, 0.82, 0.82, 0.70, 0.50};
+    static const int res[5] = {1, 1, 1, 2, 4};
+    static const int area[5] = {65536, 32768, 32768, 16384, 4096};
+    int best = T64x64;
+    double best_t = 1e300;
+    for (int c = T256x256; c <= T64x64; ++c) {
+      const long long t = tiles_of(c, a);
+      const double rounds = (double)((t + 256LL * res[c] - 1) / (256LL * res[c]));
+      const double cost = rounds * res[c] * area[c] / eff[c];
+      if (cost < best_t * 0.999) { best_t = cost; best = c; }
+    }
+    return best;
+  }
   if (allow_big) {
     if (tiles_of(T256x256, a) * ms >= 240 && a.M > 128 && a.N > 128) return T256x256;
     if (a.N <= 128 && tiles_of(T256x128, a) * ms >= 240 && a.M > 128) return T256x128;
