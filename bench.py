@@ -318,7 +318,9 @@ def main():
                 "bound": "hbm", "kernel": "GroupNorm(+SiLU) fwd / bwd (gn_* kernel chains, all launches)",
                 "achieved": round(hby / (hms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(hby / (hms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms_per_step": round(hms, 2),
-                "bytes_note": "algorithmic bytes: fwd 8 B/elem (read x, write y), bwd 12 B/elem (read x, dy; write dx)",
+                "bytes_note": "algorithmic bytes: fwd 8 B/elem (read x, write y), bwd 12 B/elem (read x, dy; write dx) "
+                              "+ 4 B/elem where the residual branch's gradient is summed in (ResnetBlock / AttnBlock "
+                              "norm1); chains include the statistics finalize and parameter-gradient kernels",
                 "by_pass": {k: {"launches": v[0], "ms": round(v[2], 2),
                                 "GB/s": round(v[1] / (v[2] * 1e-3) / 1e9, 1)} for k, v in hb.items()}}
 

@@ -16,6 +16,18 @@ namespace mvae {
 #define GN_UNROLL 4  // rows in flight per thread in the streaming GroupNorm kernels
 #endif
 
+// streaming 16-B load of an activation / gradient read once per pass, non-temporal policy (the stream does not
+// displace the consumer GEMM's working set): GroupNorm bwd chain -5 %, fwd -3 % on c4 (same-box A/B);
+// GN_TEMPORAL=1 builds the plain loads
+__device__ __forceinline__ float4 gn_ld4(const float* p) {
+#ifndef GN_TEMPORAL
+  const f32x4 v = __builtin_nontemporal_load((const f32x4*)p);
+  return float4{v[0], v[1], v[2], v[3]};
+#else
+  return *(const float4*)p;
+#endif
+}
+
 // counter-based hash -> uniform [0,1) for the dropout mask (recomputed in backward, never stored)
 __device__ __forceinline__ float hash_uniform(unsigned long long seed, unsigned long long idx) {
   unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
@@ -93,8 +105,8 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(GnArgs a) {
         for (int u = 0; u < GN_UNROLL; ++u) {
           const int r = row + u * mp.rpar;
           const bool ok = r < mp.row_hi;
-          xv[u] = ok ? *(const float4*)(xp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
-          if (KIND == 1) dv[u] = ok ? *(const float4*)(dp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+          xv[u] = ok ? gn_ld4(xp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+          if (KIND == 1) dv[u] = ok ? gn_ld4(dp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int u = 0; u < GN_UNROLL; ++u) {
@@ -246,7 +258,7 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(GnArgs a, const float* __
 #pragma unroll
         for (int u = 0; u < GN_UNROLL; ++u) {
           const int r = row + u * mp.rpar;
-          xv[u] = r < mp.row_hi ? *(const float4*)(xp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+          xv[u] = r < mp.row_hi ? gn_ld4(xp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int u = 0; u < GN_UNROLL; ++u) {
@@ -364,14 +376,17 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
       const float* xp = a.x + sbase + mp.c4 * 4;
       const float* dp = a.dy + sbase + mp.c4 * 4;
       float* op = dx + sbase + mp.c4 * 4;
+      const float* ap = a.dx_add ? a.dx_add + sbase + mp.c4 * 4 : nullptr;
       for (int row = mp.row_lo + mp.rph; row < mp.row_hi; row += GN_UNROLL * mp.rpar) {
-        float4 xv[GN_UNROLL], dv[GN_UNROLL];
+        float4 xv[GN_UNROLL], dv[GN_UNROLL], av[GN_UNROLL];
 #pragma unroll
         for (int u = 0; u < GN_UNROLL; ++u) {
           const int r = row + u * mp.rpar;
           const bool ok = r < mp.row_hi;
-          xv[u] = ok ? *(const float4*)(xp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
-          dv[u] = ok ? *(const float4*)(dp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+          xv[u] = ok ? gn_ld4(xp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+          dv[u] = ok ? gn_ld4(dp + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+          // the residual branch's gradient is loaded with the other streams (not behind the arithmetic)
+          av[u] = (ap != nullptr && ok) ? gn_ld4(ap + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int u = 0; u < GN_UNROLL; ++u) {
@@ -395,9 +410,8 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
             }
             o[e] = d * q1[e] + xs[e] * q2[e] + q3[e];
           }
-          if (a.dx_add) {  // the other branch's gradient of x (ResnetBlock / AttnBlock residual): summed here
-            const float4 ad = *(const float4*)(a.dx_add + off);
-            o[0] += ad.x; o[1] += ad.y; o[2] += ad.z; o[3] += ad.w;
+          if (ap != nullptr) {  // the other branch's gradient of x (ResnetBlock / AttnBlock residual): summed here
+            o[0] += av[u].x; o[1] += av[u].y; o[2] += av[u].z; o[3] += av[u].w;
           }
           *(float4*)(op + (long long)r * a.C) = float4{o[0], o[1], o[2], o[3]};
         }

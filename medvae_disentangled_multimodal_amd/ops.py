@@ -611,7 +611,8 @@ class GroupNormFn(torch.autograd.Function):
             if add.shape != x.shape or add.dtype != torch.float32:
                 raise RuntimeError("group_norm backward: parked branch gradient has the wrong shape")
         gpart = ctx.link.take(dy) if ctx.link is not None and drop_p == 0.0 else None
-        with _timed("gn_bwd", 12.0 * x.numel(), (n, c, h * w)):  # algorithmic HBM bytes: read x, dy; write dx
+        # algorithmic HBM bytes: read x, dy (and the residual branch's gradient when it is summed here); write dx
+        with _timed("gn_bwd", (12.0 + (4.0 if add is not None else 0.0)) * x.numel(), (n, c, h * w)):
             if gpart is not None:  # reduction half emitted by the consuming conv's input-gradient GEMM
                 _lib.call("mvae_group_norm_bwd_part_nhwc", x.data_ptr(), dy.data_ptr(), gpart.data_ptr(),
                           gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
