@@ -55,6 +55,13 @@ CONFIGS = {
                opt=dict(type="adamw", lr=1e-4, weight_decay=1e-5, betas=[0.5, 0.999]), clip=1.0,
                loss=dict(type="lpips_discriminator", perceptual_factor=1.0, kl_factor=1e-5,
                          discriminator_iter_start=10000, allow_synthetic_lpips=True, lpips_net="vgg")),
+    # BASELINE config 1: chest_base_vae at 28x28x1 with the 3-level ch_mult (SURVEY top note 3), bs 32, AdamW 2e-4
+    # wd 1e-4, clip 1.0 (the reference runs it on the CPU; here it is the same step on the GPU path)
+    "c1": dict(cls="BaseVAE", res=28, batch=32, cpu_batch=32,
+               kwargs=dict(input_channels=1, latent_dim=256, hidden_channels=128, ch_mult=(1, 2, 4),
+                           num_res_blocks=2, attn_resolutions=[16], dropout=0.0, resolution=28),
+               opt=dict(type="adamw", lr=2e-4, weight_decay=1e-4, betas=[0.9, 0.999]), clip=1.0,
+               loss=dict(type="vae", recon_loss_type="mse", kl_weight=1.0, recon_weight=1.0)),
     # BASELINE config 2: path_beta_vae at 28x28x3 with the 3-level ch_mult, bs 256
     "c2": dict(cls="BetaVAE", res=28, batch=256, cpu_batch=16,
                kwargs=dict(input_channels=3, latent_dim=128, hidden_channels=128, ch_mult=(1, 2, 4),
@@ -216,7 +223,11 @@ def main():
     import medvae_disentangled_multimodal_amd as M
     from medvae_disentangled_multimodal_amd import ddp, ops
 
-    rank, world, local = ddp.init_from_env()
+    # MVAE_BENCH_BACKEND / MVAE_BENCH_ONE_DEVICE: rehearse the multi-rank bench on a 1-GPU box (gloo transport,
+    # every rank on cuda:0); the production path is RCCL with one rank per GPU
+    rank, world, local = ddp.init_from_env(os.environ.get("MVAE_BENCH_BACKEND"))
+    if os.environ.get("MVAE_BENCH_ONE_DEVICE"):
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cfg = dict(CONFIGS[args.config])
