@@ -170,6 +170,10 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
                              unsigned long long seed, void* workspace, size_t workspace_bytes,
                              void* stream);
 size_t mvae_group_norm_workspace_bytes(int nb, int hw, int c);
+/* Path of mvae_group_norm_fwd_nhwc / _bwd_nhwc (process-wide): 0 = auto (small per-sample tensors -- the
+ * 28x28 / 14x14 / 7x7 levels -- run the register-resident one-pass kernels: x read once per pass),
+ * 1 = streaming only (statistics pass + apply pass). Both are deterministic; they agree to fp32 rounding. */
+int mvae_set_group_norm_path(int mode);
 /* mvae_group_norm_bwd_nhwc (drop_p = 0) from the partials of mvae_conv2d_dgrad_gnbwd_nhwc: no reduction
  * pass over x and dy. hw % 32 == 0. */
 int mvae_group_norm_bwd_part_nhwc(const float* x, const float* dy, const double* part, const float* gamma,

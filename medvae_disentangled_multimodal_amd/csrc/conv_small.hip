@@ -136,24 +136,28 @@ __global__ void __launch_bounds__(256) wgrad_small_cout_kernel(const float* __re
   }
 }
 
-// dw[co][r][s][c] = beta*dw + sum_n part[n][c/64][tap][co][c%64]; dbias[co] = beta*dbias + sum_n bpart[n][co]
+// dw[co][r][s][c] = beta*dw + sum_n part[n][c/64][tap][co][c%64]; dbias[co] = beta*dbias + sum_n bpart[n][co].
+// One wave per output element (the last cout waves: the bias), lanes over the images, then the fixed wave
+// tree: deterministic, and the nb loads of an element are in flight together.
 __global__ void __launch_bounds__(256) wgrad_small_cout_final_kernel(const float* __restrict__ part,
                                                                      const float* __restrict__ bpart, float* dw,
                                                                      float* dbias, float beta, int nb, int cin,
                                                                      int cout, int chunks) {
-  const int i = blockIdx.x * 256 + threadIdx.x;  // over cout * 9 * cin
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;  // over cout * 9 * cin (+ cout)
   const int total = cout * 9 * cin;
   if (i < total) {
     const int c = i % cin, t = (i / cin) % 9, o = i / (9 * cin);
     const int ch = c >> 6, cl = c & 63;
     float s = 0.f;
-    for (int n = 0; n < nb; ++n) s += part[((((long long)n * chunks + ch) * 9 + t) * SC_MAXC + o) * 64 + cl];
-    dw[i] = beta == 0.f ? s : beta * dw[i] + s;
-  }
-  if (dbias != nullptr && blockIdx.x == 0 && threadIdx.x < cout) {
+    for (int n = lane; n < nb; n += 64) s += part[((((long long)n * chunks + ch) * 9 + t) * SC_MAXC + o) * 64 + cl];
+    s = wave_sum_f(s);
+    if (lane == 0) dw[i] = beta == 0.f ? s : beta * dw[i] + s;
+  } else if (dbias != nullptr && i < total + cout) {
+    const int o = i - total;
     float s = 0.f;
-    for (int n = 0; n < nb; ++n) s += bpart[(long long)n * SC_MAXC + threadIdx.x];
-    dbias[threadIdx.x] = beta == 0.f ? s : beta * dbias[threadIdx.x] + s;
+    for (int n = lane; n < nb; n += 64) s += bpart[(long long)n * SC_MAXC + o];
+    s = wave_sum_f(s);
+    if (lane == 0) dbias[o] = beta == 0.f ? s : beta * dbias[o] + s;
   }
 }
 
@@ -208,7 +212,7 @@ int mvae_conv2d_wgrad_small_cout_nhwc(const float* dy, const float* x, float* dw
     hipLaunchKernelGGL((wgrad_small_cout_kernel<false, true>), grid, dim3(256), lds, st, dy, x, part, bpart, h, w, cin, cout);
   else
     hipLaunchKernelGGL((wgrad_small_cout_kernel<false, false>), grid, dim3(256), lds, st, dy, x, part, bpart, h, w, cin, cout);
-  hipLaunchKernelGGL(wgrad_small_cout_final_kernel, dim3(cdiv((long long)cout * 9 * cin, 256)), dim3(256), 0, st,
+  hipLaunchKernelGGL(wgrad_small_cout_final_kernel, dim3(cdiv((long long)cout * 9 * cin + cout, 4)), dim3(256), 0, st,
                      (const float*)part, (const float*)bpart, dw, dbias, beta, nb, cin, cout, chunks);
   return launch_status();
 }

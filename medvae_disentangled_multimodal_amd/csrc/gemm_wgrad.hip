@@ -2,21 +2,24 @@
 #include "gemm_core.h"
 
 namespace mvae {
-// dbias[m] = beta*dbias[m] + sum over splits (fixed order) of the per-split row sums
-__global__ void bias_reduce_kernel(const float* __restrict__ part, int splits, int m, float* dbias, float beta) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// dbias[m] = beta*dbias[m] + sum over splits of the per-split row sums: one wave per row, lanes over the
+// splits, then the fixed wave tree (deterministic; the splits' loads are all in flight at once)
+__global__ void __launch_bounds__(256) bias_reduce_kernel(const float* __restrict__ part, int splits, int m,
+                                                          float* dbias, float beta) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= m) return;
   float s = 0.f;
-  for (int z = 0; z < splits; ++z) s += part[(long long)z * m + i];
-  dbias[i] = (beta != 0.f ? beta * dbias[i] : 0.f) + s;
+  for (int z = lane; z < splits; z += 64) s += part[(long long)z * m + i];
+  s = wave_sum_f(s);
+  if (lane == 0) dbias[i] = (beta != 0.f ? beta * dbias[i] : 0.f) + s;
 }
 
-// Upsample-conv weight gradient from the per-class partials of the sub-pixel form:
-// part[cls][z][co][(2a+b)*cin + ci] (cls = 2*ph+pw, z = split) ->
-// dw[co][r][s][ci] = beta*dw + sum_{(ph,a) in P(r), (pw,b) in P(s)} sum_z part[2ph+pw][z][co][(2a+b)*cin+ci]
+// Upsample-conv weight gradient from the per-class partials of the sub-pixel form, already summed over the
+// split-K slices (class c at part + c*cls_stride, [co][(2a+b)*cin + ci]) ->
+// dw[co][r][s][ci] = beta*dw + sum_{(ph,a) in P(r), (pw,b) in P(s)} part[2ph+pw][co][(2a+b)*cin+ci]
 // with P(0) = {(0,0),(1,0)}, P(1) = {(0,1),(1,0)}, P(2) = {(0,1),(1,1)} (fixed summation order)
-__global__ void __launch_bounds__(256) ups_wgrad_combine_kernel(const float* __restrict__ part, int splits, int cout,
-                                                                int cin, float* __restrict__ dw, float beta) {
+__global__ void __launch_bounds__(256) ups_wgrad_combine_kernel(const float* __restrict__ part, long long cls_stride,
+                                                                int cout, int cin, float* __restrict__ dw, float beta) {
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long long)cout * cin) return;
   const int co = (int)(idx / cin), ci = (int)(idx - (long long)co * cin);
@@ -25,11 +28,7 @@ __global__ void __launch_bounds__(256) ups_wgrad_combine_kernel(const float* __r
 #pragma unroll
   for (int cls = 0; cls < 4; ++cls)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      float s = 0.f;
-      for (int z = 0; z < splits; ++z) s += part[((long long)(cls * splits + z) * cout + co) * n4 + t * cin + ci];
-      g[cls][t] = s;
-    }
+    for (int t = 0; t < 4; ++t) g[cls][t] = part[cls * cls_stride + (long long)co * n4 + t * cin + ci];
   const int pp[3][2][2] = {{{0, 0}, {1, 0}}, {{0, 1}, {1, 0}}, {{0, 1}, {1, 1}}};  // P(r): (parity, tap)
 #pragma unroll
   for (int r = 0; r < 3; ++r)
@@ -130,7 +129,7 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
       else launch_small<A_COLM, 1, B_WGRAD_UPS, 1>(a, st, cfg);
     }
     if (dbias)
-      hipLaunchKernelGGL(bias_reduce_kernel, dim3(cdiv(a.M, 256)), dim3(256), 0, st, (const float*)a.bias_ws,
+      hipLaunchKernelGGL(bias_reduce_kernel, dim3(cdiv(a.M, 4)), dim3(256), 0, st, (const float*)a.bias_ws,
                          a.splits, a.M, dbias, b0 == 0 ? beta : 1.f);
     const int rc = gemm_finish(a, st);
     if (rc) return rc;
@@ -185,11 +184,18 @@ int mvae_conv2d_wgrad_upsample_nhwc(const float* dy, const float* x, float* dw, 
     else launch_small<A_COLM_PIX, 1, B_WGRAD_SUBPIX, 1>(a, st, cfg);
     const float bt = b0 == 0 ? beta : 1.f;
     if (dbias)
-      hipLaunchKernelGGL(bias_reduce_kernel, dim3(cdiv(a.M, 256)), dim3(256), 0, st, (const float*)a.bias_ws,
+      hipLaunchKernelGGL(bias_reduce_kernel, dim3(cdiv(a.M, 4)), dim3(256), 0, st, (const float*)a.bias_ws,
                          a.splits * a.batch, a.M, dbias, bt);
+    // the split-K slices of every class summed in place into slice 0 (the GEMM's vectorized fixed-order reducer),
+    // then the 16 class partials of each 3x3 tap combined
+    GemmArgs r = a;
+    r.C = workspace; r.ldc = a.N; r.sC = (long long)a.splits * a.M * a.N;
+    r.alpha = 1.f; r.beta = 0.f; r.bias = nullptr; r.res = nullptr;
+    const int rrc = gemm_finish(r, st);
+    if (rrc) return rrc;
     const long long tot = (long long)cout * cin;
     hipLaunchKernelGGL(ups_wgrad_combine_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st,
-                       (const float*)workspace, a.splits, cout, cin, dw, bt);
+                       (const float*)workspace, (long long)a.splits * a.M * a.N, cout, cin, dw, bt);
     const int rc = launch_status();
     if (rc) return rc;
   }

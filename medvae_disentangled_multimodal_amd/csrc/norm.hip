@@ -421,6 +421,275 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Resident GroupNorm for small per-sample tensors (the 28x28 / 14x14 / 7x7 levels of c2 / c3, where the
+// producing conv cannot emit the statistics: h*w % 32 != 0). A workgroup owns (sample b, slab of SC
+// channels = whole groups) and holds the slab in registers (IT float4 per thread), so x is read from HBM
+// ONCE per pass: forward = statistics (two-pass: mean, then centred variance, on the resident values) +
+// apply in one launch (8 B/elem); backward = partial sums + finalize + dx in one launch (12 B/elem, +4 with
+// the residual-branch add) and a per-channel parameter-gradient reduction. Cross-thread sums: a fixed wave
+// butterfly, then a fixed-order LDS combine -- bitwise reproducible.
+// Thread map: C4 = SC/4 (a power of two <= 256) channel quads, rpar = 256 / C4 row phases, thread (rph, c4)
+// walks rows rph, rph + rpar, ... (at most IT of them).
+// ------------------------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ void gn_slab_reduce(float (&s)[K], int C4, float* red /*[K][256]*/, float* out /*[C4][K]*/) {
+  const int tid = threadIdx.x;
+  if (C4 < 64) {
+    for (int m = C4; m < 64; m <<= 1) {  // lanes with the same c4 differ by multiples of C4
+#pragma unroll
+      for (int k = 0; k < K; ++k) s[k] += __shfl_xor(s[k], m, 64);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) red[k * 256 + tid] = s[k];
+  __syncthreads();
+  if (tid < C4) {
+    const int stride = C4 < 64 ? 64 : C4;  // one representative per (wave, c4)
+    float t[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) t[k] = 0.f;
+    for (int j = tid; j < 256; j += stride)
+#pragma unroll
+      for (int k = 0; k < K; ++k) t[k] += red[k * 256 + j];
+#pragma unroll
+    for (int k = 0; k < K; ++k) out[tid * K + k] = t[k];
+  }
+  __syncthreads();
+}
+
+constexpr int GN_RES_MAXC = 1024;  // slab channels (C4 <= 256)
+
+template <int IT>
+__global__ void __launch_bounds__(256) gn_fwd_resident_kernel(GnArgs a, int SC, float* __restrict__ y,
+                                                              float* __restrict__ mean, float* __restrict__ rstd,
+                                                              float eps) {
+  __shared__ float red[4 * 256];
+  __shared__ float chs[GN_RES_MAXC];
+  __shared__ float gmu[GN_RES_MAXC], grs[GN_RES_MAXC];  // per slab channel: its group's mean / rstd
+  const int tid = threadIdx.x, b = blockIdx.y, c0 = blockIdx.x * SC;
+  const int C4 = SC >> 2, rpar = 256 / C4, c4 = tid & (C4 - 1), rph = tid / C4;
+  const int cpg = a.C / a.G, ngl = SC / cpg;
+  const double n = (double)a.hw * cpg;
+  const long long sbase = (long long)b * a.hw * a.C + c0 + c4 * 4;
+  float4 v[IT];
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = rph + i * rpar;
+    v[i] = r < a.hw ? gn_ld4(a.x + sbase + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+    s[0] += v[i].x; s[1] += v[i].y; s[2] += v[i].z; s[3] += v[i].w;
+  }
+  gn_slab_reduce<4>(s, C4, red, chs);
+  for (int gl = tid; gl < ngl; gl += 256) {
+    float t = 0.f;
+    for (int j = 0; j < cpg; ++j) t += chs[gl * cpg + j];
+    const float mu = (float)((double)t / n);
+    for (int j = 0; j < cpg; ++j) gmu[gl * cpg + j] = mu;
+  }
+  __syncthreads();
+  float mu[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    mu[e] = gmu[c4 * 4 + e];
+    s[e] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    if (rph + i * rpar < a.hw) {
+      const float d0 = v[i].x - mu[0], d1 = v[i].y - mu[1], d2 = v[i].z - mu[2], d3 = v[i].w - mu[3];
+      s[0] = fmaf(d0, d0, s[0]); s[1] = fmaf(d1, d1, s[1]); s[2] = fmaf(d2, d2, s[2]); s[3] = fmaf(d3, d3, s[3]);
+    }
+  }
+  gn_slab_reduce<4>(s, C4, red, chs);
+  for (int gl = tid; gl < ngl; gl += 256) {
+    float t = 0.f;
+    for (int j = 0; j < cpg; ++j) t += chs[gl * cpg + j];
+    const float rs = (float)(1.0 / sqrt((double)t / n + (double)eps));
+    for (int j = 0; j < cpg; ++j) grs[gl * cpg + j] = rs;
+    const int gi = b * a.G + c0 / cpg + gl;
+    mean[gi] = gmu[gl * cpg];
+    rstd[gi] = rs;
+  }
+  __syncthreads();
+  float sc[4], sh[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = c0 + c4 * 4 + e;
+    sc[e] = grs[c4 * 4 + e] * a.gamma[c];
+    sh[e] = a.beta[c] - mu[e] * sc[e];
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = rph + i * rpar;
+    if (r >= a.hw) continue;
+    float o[4] = {v[i].x * sc[0] + sh[0], v[i].y * sc[1] + sh[1], v[i].z * sc[2] + sh[2], v[i].w * sc[3] + sh[3]};
+    const long long off = sbase + (long long)r * a.C;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (a.silu) o[k] = o[k] * sigmoid_f(o[k]);
+      if (a.drop_p > 0.f) {
+        const float uu = hash_uniform(a.seed, (unsigned long long)(off + k));
+        o[k] = (uu >= a.drop_p) ? o[k] / (1.f - a.drop_p) : 0.f;
+      }
+    }
+    const float4 ov{o[0], o[1], o[2], o[3]};
+    if (a.y_split)
+      *(uint4*)(y + off) = split4_bf16(ov);
+    else
+      *(float4*)(y + off) = ov;
+  }
+}
+
+// backward; pws = [2][C][nb] fp64 per-sample channel sums {sum dyn, sum dyn*xhat} for the parameter gradients
+template <int IT>
+__global__ void __launch_bounds__(256) gn_bwd_resident_kernel(GnArgs a, int SC, double* __restrict__ pws,
+                                                              float* __restrict__ dx) {
+  __shared__ float red[8 * 256];
+  __shared__ float chs[GN_RES_MAXC * 2];
+  __shared__ float gk2[GN_RES_MAXC], gk3[GN_RES_MAXC];
+  const int tid = threadIdx.x, b = blockIdx.y, c0 = blockIdx.x * SC;
+  const int C4 = SC >> 2, rpar = 256 / C4, c4 = tid & (C4 - 1), rph = tid / C4;
+  const int cpg = a.C / a.G, ngl = SC / cpg;
+  const long long sbase = (long long)b * a.hw * a.C + c0 + c4 * 4;
+  float m[4], rs[4], gm[4], bt[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = c0 + c4 * 4 + e, bg = b * a.G + c / cpg;
+    m[e] = a.mean[bg];
+    rs[e] = a.rstd[bg];
+    gm[e] = a.gamma[c];
+    bt[e] = a.beta[c];
+  }
+  float4 xv[IT], dv[IT], av[IT];
+  const bool add = a.dx_add != nullptr;
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = rph + i * rpar;
+    const bool ok = r < a.hw;
+    const long long off = sbase + (long long)r * a.C;
+    xv[i] = ok ? gn_ld4(a.x + off) : float4{0.f, 0.f, 0.f, 0.f};
+    dv[i] = ok ? gn_ld4(a.dy + off) : float4{0.f, 0.f, 0.f, 0.f};
+    av[i] = (add && ok) ? gn_ld4(a.dx_add + off) : float4{0.f, 0.f, 0.f, 0.f};
+  }
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const long long off = sbase + (long long)(rph + i * rpar) * a.C;
+    float xs[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+    float ds[4] = {dv[i].x, dv[i].y, dv[i].z, dv[i].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float d = ds[e];  // rows past hw hold d = 0: they add nothing
+      if (a.drop_p > 0.f) {
+        const float uu = hash_uniform(a.seed, (unsigned long long)(off + e));
+        d = (uu >= a.drop_p) ? d / (1.f - a.drop_p) : 0.f;
+      }
+      const float xh = (xs[e] - m[e]) * rs[e];
+      if (a.silu) {
+        const float yn = xh * gm[e] + bt[e];
+        const float sg = sigmoid_f(yn);
+        d = d * sg * (1.f + yn * (1.f - sg));
+      }
+      ds[e] = d;
+      s[e] += d;
+      s[4 + e] = fmaf(d, xh, s[4 + e]);
+    }
+    dv[i] = float4{ds[0], ds[1], ds[2], ds[3]};
+  }
+  // chs[(c4*8) + k]: k 0-3 = sum dyn of channels c4*4+k, k 4-7 = sum dyn*xhat
+  gn_slab_reduce<8>(s, C4, red, chs);
+  for (int t = tid; t < SC; t += 256) {
+    const int q = t >> 2, e = t & 3, c = c0 + t;
+    pws[(long long)c * a.nb + b] = chs[q * 8 + e];
+    pws[((long long)a.C + c) * a.nb + b] = chs[q * 8 + 4 + e];
+  }
+  for (int gl = tid; gl < ngl; gl += 256) {
+    double A1 = 0.0, A2 = 0.0;
+    for (int j = 0; j < cpg; ++j) {
+      const int cl = gl * cpg + j;
+      const double g = a.gamma[c0 + cl];
+      A1 += g * chs[(cl >> 2) * 8 + (cl & 3)];
+      A2 += g * chs[(cl >> 2) * 8 + 4 + (cl & 3)];
+    }
+    const int gi = b * a.G + c0 / cpg + gl;
+    const double n = (double)a.hw * cpg, r = a.rstd[gi], mu = a.mean[gi];
+    const float k2 = (float)(-r * r * A2 / n), k3 = (float)(-r * A1 / n + mu * r * r * A2 / n);
+    for (int j = 0; j < cpg; ++j) {
+      gk2[gl * cpg + j] = k2;
+      gk3[gl * cpg + j] = k3;
+    }
+  }
+  __syncthreads();
+  float q1[4], q2[4], q3[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    q1[e] = rs[e] * gm[e];
+    q2[e] = gk2[c4 * 4 + e];
+    q3[e] = gk3[c4 * 4 + e];
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = rph + i * rpar;
+    if (r >= a.hw) continue;
+    float4 o{dv[i].x * q1[0] + xv[i].x * q2[0] + q3[0], dv[i].y * q1[1] + xv[i].y * q2[1] + q3[1],
+             dv[i].z * q1[2] + xv[i].z * q2[2] + q3[2], dv[i].w * q1[3] + xv[i].w * q2[3] + q3[3]};
+    if (add) {
+      o.x += av[i].x; o.y += av[i].y; o.z += av[i].z; o.w += av[i].w;
+    }
+    *(float4*)(dx + sbase + (long long)r * a.C) = o;
+  }
+}
+
+// dgamma[c] += sum_b pws[1][c][b], dbeta[c] += sum_b pws[0][c][b]: one block per channel, fixed order
+__global__ void __launch_bounds__(256) gn_param_reduce_kernel(const double* __restrict__ pws, int nb, int C,
+                                                              float* dgamma, float* dbeta) {
+  __shared__ double sh[2][4];
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double s0 = 0.0, s1 = 0.0;
+  for (int i = tid; i < nb; i += 256) {
+    s0 += pws[(long long)c * nb + i];
+    s1 += pws[((long long)C + c) * nb + i];
+  }
+  s0 = wave_sum_d(s0);
+  s1 = wave_sum_d(s1);
+  if (lane == 0) {
+    sh[0][wv] = s0;
+    sh[1][wv] = s1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (dbeta) dbeta[c] += (float)(((sh[0][0] + sh[0][1]) + sh[0][2]) + sh[0][3]);
+    if (dgamma) dgamma[c] += (float)(((sh[1][0] + sh[1][1]) + sh[1][2]) + sh[1][3]);
+  }
+}
+
+// Largest slab (of >= 16 channels: 64-B row segments) with <= 16 rows per thread that still gives >= 512
+// workgroups; else the feasible slab with the most workgroups.
+// slab width for the resident path (0: not eligible). Path selection: mvae_set_group_norm_path (0 auto,
+// 1 streaming only); before any call, MVAE_GN_RESIDENT=0 selects streaming only.
+static int g_gn_path = -1;
+static int gn_resident_slab(int nb, int hw, int C, int G, int* items) {
+  if (g_gn_path < 0) {
+    const char* e = getenv("MVAE_GN_RESIDENT");
+    g_gn_path = (e != nullptr && e[0] == '0') ? 1 : 0;
+  }
+  if (g_gn_path == 1 || C % G) return 0;
+  const int cpg = C / G;
+  int best = 0, best_it = 0;
+  for (int sc = std::min(C, GN_RES_MAXC); sc >= 16; sc >>= 1) {
+    const int c4 = sc >> 2;
+    if ((c4 & (c4 - 1)) || C % sc || sc % cpg) continue;
+    const int it = (hw + 256 / c4 - 1) / (256 / c4);
+    if (it > 16) continue;
+    best = sc;
+    best_it = it;
+    if ((long long)nb * (C / sc) >= 512) break;
+  }
+  *items = best_it <= 4 ? 4 : best_it <= 8 ? 8 : 16;
+  return best;
+}
+
 static int gn_target_blocks() {
   static int v = [] {
     const char* e = getenv("MVAE_GN_BLOCKS");  // experiment knob: target grid size of the streaming kernels
@@ -439,6 +708,15 @@ static int gn_chunks(int nb, int hw) {
 using namespace mvae;
 
 extern "C" {
+
+int mvae_set_group_norm_path(int mode) {
+  if (mode != 0 && mode != 1) {
+    set_error("group_norm path: 0 (auto: resident for small per-sample tensors) or 1 (streaming only)");
+    return MVAE_EINVAL;
+  }
+  g_gn_path = mode;
+  return MVAE_OK;
+}
 
 size_t mvae_group_norm_workspace_bytes(int nb, int hw, int c) {
   const int ch = gn_chunks(nb, hw);
@@ -467,6 +745,15 @@ int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* be
   a.chunks = gn_chunks(nb, hw);
   a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
   a.ws = (double*)workspace;
+  int it = 0;
+  if (const int sc = gn_resident_slab(nb, hw, c, groups, &it)) {
+    a.silu = silu; a.drop_p = drop_p; a.seed = seed; a.y_split = y_split;
+    const dim3 grid(c / sc, nb);
+    if (it == 4) hipLaunchKernelGGL(gn_fwd_resident_kernel<4>, grid, dim3(256), 0, st, a, sc, y, mean, rstd, eps);
+    else if (it == 8) hipLaunchKernelGGL(gn_fwd_resident_kernel<8>, grid, dim3(256), 0, st, a, sc, y, mean, rstd, eps);
+    else hipLaunchKernelGGL(gn_fwd_resident_kernel<16>, grid, dim3(256), 0, st, a, sc, y, mean, rstd, eps);
+    return launch_status();
+  }
   float* scale = (float*)((char*)workspace + (size_t)nb * a.chunks * c * 2 * sizeof(double));
   float* shift = scale + (size_t)nb * c;
   hipLaunchKernelGGL(gn_partial_kernel<0>, dim3(a.chunks, nb), dim3(256), 0, st, a);
@@ -527,6 +814,17 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
   a.chunks = gn_chunks(nb, hw);
   a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
   a.ws = (double*)workspace;
+  int it = 0;
+  if (const int sc = gn_resident_slab(nb, hw, c, groups, &it)) {
+    double* pws = (double*)workspace;  // [2][C][nb] fp64 (within the [nb][chunks][C][2] partial area)
+    const dim3 grid(c / sc, nb);
+    if (it == 4) hipLaunchKernelGGL(gn_bwd_resident_kernel<4>, grid, dim3(256), 0, st, a, sc, pws, dx);
+    else if (it == 8) hipLaunchKernelGGL(gn_bwd_resident_kernel<8>, grid, dim3(256), 0, st, a, sc, pws, dx);
+    else hipLaunchKernelGGL(gn_bwd_resident_kernel<16>, grid, dim3(256), 0, st, a, sc, pws, dx);
+    if (dgamma || dbeta)
+      hipLaunchKernelGGL(gn_param_reduce_kernel, dim3(c), dim3(256), 0, st, (const double*)pws, nb, c, dgamma, dbeta);
+    return launch_status();
+  }
   float* k1 = (float*)((char*)workspace + (size_t)nb * a.chunks * c * 2 * sizeof(double));
   float* k2 = k1 + (size_t)nb * c;
   float* k3 = k2 + (size_t)nb * c;

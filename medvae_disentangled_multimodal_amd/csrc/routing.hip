@@ -244,52 +244,78 @@ __global__ void __launch_bounds__(RT_NT) heads_bwd_kernel(const float* __restric
 #pragma unroll
     for (int c = 0; c < C; ++c) dst[p * C + c] = g[c];
   }
-  // parameter-gradient partials of this sample: one parameter per thread, pixels in order
+  // parameter-gradient partials of this sample: one parameter per thread, a fixed walk over the rows with
+  // pointer increments (no per-pixel index division) and two interleaved accumulators
   float* pp = part + (long long)b * LY::P;
+  const int rs = (w + 2) * C;  // padded row stride of the LDS planes
   for (int q = threadIdx.x; q < LY::P; q += RT_NT) {
-    float s = 0.f;
+    float s0 = 0.f, s1 = 0.f;
     if (q < LY::B1 || (q >= LY::W2 && q < LY::B2)) {  // conv weights [co][kh][kw][ci]
       const bool second = q >= LY::W2;
       const int e = second ? q - LY::W2 : q;
       const int ci = e % C, kw = (e / C) % 3, kh = (e / (3 * C)) % 3, co = e / (9 * C);
-      const float* d = second ? dh2 : dh1;
-      const float* a = second ? r : in;
-      for (int p = 0; p < hw; ++p) {
-        const int y = p / w, x = p - y * w;
-        s = fmaf(d[pd.at(y, x) * C + co], a[pd.at(y + kh - 1, x + kw - 1) * C + ci], s);
+      const float* d = (second ? dh2 : dh1) + pd.at(0, 0) * C + co;
+      const float* a = (second ? r : in) + pd.at(kh - 1, kw - 1) * C + ci;
+      for (int y = 0; y < h; ++y, d += rs, a += rs) {
+        int x = 0;
+        for (; x + 1 < w; x += 2) {
+          s0 = fmaf(d[x * C], a[x * C], s0);
+          s1 = fmaf(d[(x + 1) * C], a[(x + 1) * C], s1);
+        }
+        if (x < w) s0 = fmaf(d[x * C], a[x * C], s0);
       }
     } else if (q < LY::W2 || q < LY::PW) {  // conv biases
       const bool second = q >= LY::B2;
       const int co = second ? q - LY::B2 : q - LY::B1;
-      const float* d = second ? dh2 : dh1;
-      for (int p = 0; p < hw; ++p) {
-        const int y = p / w, x = p - y * w;
-        s += d[pd.at(y, x) * C + co];
+      const float* d = (second ? dh2 : dh1) + pd.at(0, 0) * C + co;
+      for (int y = 0; y < h; ++y, d += rs) {
+        int x = 0;
+        for (; x + 1 < w; x += 2) {
+          s0 += d[x * C];
+          s1 += d[(x + 1) * C];
+        }
+        if (x < w) s0 += d[x * C];
       }
     } else if (q < LY::PB) {  // projector weight [j][c]
       const int e = q - LY::PW, j = e / C, c = e - j * C;
-      if (j < cm && j < out_c)
-        for (int p = 0; p < hw; ++p) s = fmaf(go[p * out_c + j], h2[p * C + c], s);
+      if (j < cm && j < out_c) {
+        int p = 0;
+        for (; p + 1 < hw; p += 2) {
+          s0 = fmaf(go[p * out_c + j], h2[p * C + c], s0);
+          s1 = fmaf(go[(p + 1) * out_c + j], h2[(p + 1) * C + c], s1);
+        }
+        if (p < hw) s0 = fmaf(go[p * out_c + j], h2[p * C + c], s0);
+      }
     } else {  // projector bias
       const int j = q - LY::PB;
-      if (j < cm && j < out_c)
-        for (int p = 0; p < hw; ++p) s += go[p * out_c + j];
+      if (j < cm && j < out_c) {
+        int p = 0;
+        for (; p + 1 < hw; p += 2) {
+          s0 += go[p * out_c + j];
+          s1 += go[(p + 1) * out_c + j];
+        }
+        if (p < hw) s0 += go[p * out_c + j];
+      }
     }
-    pp[q] = s;
+    pp[q] = s0 + s1;
   }
 }
 
-// fixed-order per-modality reduction of the per-sample partials into the flat gradient slots
+// per-modality reduction of the per-sample partials into the flat gradient slots: one wave per (modality,
+// parameter), lanes over the samples, then the fixed wave tree (deterministic)
 template <int C, int CM>
-__global__ void heads_grad_reduce_kernel(const float* __restrict__ part, const long long* __restrict__ idx, int nb, int nm,
-                                         HeadGrad g) {
+__global__ void __launch_bounds__(256) heads_grad_reduce_kernel(const float* __restrict__ part,
+                                                                const long long* __restrict__ idx, int nb, int nm,
+                                                                HeadGrad g) {
   using LY = HeadLayout<C, CM>;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (t >= nm * LY::P) return;
   const int m = t / LY::P, q = t - m * LY::P;
   float s = 0.f;
-  for (int b = 0; b < nb; ++b)
+  for (int b = lane; b < nb; b += 64)
     if (clamp_mod(idx[b], nm) == m) s += part[(long long)b * LY::P + q];
+  s = wave_sum_f(s);
+  if (lane != 0) return;
   float* dst;
   int off;
   if (q < LY::B1) { dst = g.w1[m]; off = q; }
@@ -369,16 +395,18 @@ __global__ void __launch_bounds__(RT_NT) route_in_bwd_kernel(const float* __rest
 }
 
 template <int C>
-__global__ void route_in_grad_reduce_kernel(const float* __restrict__ part, const long long* __restrict__ idx, int nb, int nm,
-                                            ProjGrad g) {
-  const int t = threadIdx.x;
+__global__ void __launch_bounds__(256) route_in_grad_reduce_kernel(const float* __restrict__ part,
+                                                                   const long long* __restrict__ idx, int nb, int nm,
+                                                                   ProjGrad g) {
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;  // one wave per (modality, param)
   if (t >= nm * 2 * C) return;
   const int m = t / (2 * C), q = t - m * 2 * C;
   float s = 0.f;
-  for (int b = 0; b < nb; ++b)
+  for (int b = lane; b < nb; b += 64)
     if (clamp_mod(idx[b], nm) == m) s += part[(long long)b * 2 * C + q];
+  s = wave_sum_f(s);
   float* dst = q < C ? g.w[m] : g.b[m];
-  if (dst != nullptr) dst[q < C ? q : q - C] += s;
+  if (lane == 0 && dst != nullptr) dst[q < C ? q : q - C] += s;
 }
 
 static size_t heads_lds_bytes(int h, int w, int c, bool bwd) {
@@ -467,7 +495,7 @@ int mvae_modality_heads_bwd(const float* rec, const long long* idx, int nb, int 
   hipLaunchKernelGGL((heads_bwd_kernel<3, 1>), dim3(nb), dim3(RT_NT), lds, st, rec, idx, h, w, nm, t, out_c, dout, drec,
                      part);
   const int tot = nm * HeadLayout<3, 1>::P;
-  hipLaunchKernelGGL((heads_grad_reduce_kernel<3, 1>), dim3((tot + 127) / 128), dim3(128), 0, st, part, idx, nb, nm, g);
+  hipLaunchKernelGGL((heads_grad_reduce_kernel<3, 1>), dim3((tot + 3) / 4), dim3(256), 0, st, part, idx, nb, nm, g);
   return launch_status();
 }
 
@@ -513,7 +541,7 @@ int mvae_modality_route_in_bwd(const float* x, int cx, const long long* idx, int
   float* part = (float*)workspace;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(route_in_bwd_kernel<3>, dim3(nb), dim3(RT_NT), 0, st, x, cx, idx, hw, nm, t, drouted, part);
-  hipLaunchKernelGGL(route_in_grad_reduce_kernel<3>, dim3(1), dim3(64), 0, st, part, idx, nb, nm, g);
+  hipLaunchKernelGGL(route_in_grad_reduce_kernel<3>, dim3(cdiv(nm * 2 * 3, 4)), dim3(256), 0, st, part, idx, nb, nm, g);
   return launch_status();
 }
 

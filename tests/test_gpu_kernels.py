@@ -317,6 +317,73 @@ def test_group_norm_silu(dev, n, c, h, w, silu, drop):
     assert rel(bd.grad, br.grad) < 1e-4
 
 
+def _gn_raw(path, x, gamma, beta, dy, add, groups, silu, drop, seed, y_split=0):
+    """One fwd + bwd through the C ABI on the selected GroupNorm path (0 auto/resident, 1 streaming)."""
+    from medvae_disentangled_multimodal_amd import _lib
+    n, h, w, c = x.shape
+    st = torch.cuda.current_stream().cuda_stream
+    _lib.call("mvae_set_group_norm_path", path)
+    try:
+        ws = torch.empty(_lib.query("mvae_group_norm_workspace_bytes", n, h * w, c), dtype=torch.uint8,
+                         device=x.device)
+        y = torch.empty_like(x)
+        mean = torch.empty(n * groups, device=x.device)
+        rstd = torch.empty_like(mean)
+        _lib.call("mvae_group_norm_fwd_nhwc", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
+                  mean.data_ptr(), rstd.data_ptr(), n, h * w, c, groups, 1e-6, int(silu), float(drop), seed, y_split,
+                  ws.data_ptr(), ws.numel(), st)
+        dx = torch.empty_like(x)
+        dg = torch.full((c,), 0.5, device=x.device)  # accumulated into (+=)
+        db = torch.full((c,), -0.25, device=x.device)
+        _lib.call("mvae_group_norm_bwd_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                  mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), add.data_ptr() if add is not None else None,
+                  dg.data_ptr(), db.data_ptr(), n, h * w, c, groups, int(silu), float(drop), seed, ws.data_ptr(),
+                  ws.numel(), st)
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("mvae_set_group_norm_path", 0)
+    return y, mean, rstd, dx, dg, db
+
+
+# the c3 (28/14/7 at hidden 32) and c2 (hidden 128) levels, whose h*w is not a multiple of 32 (no conv-epilogue
+# statistics): auto selects the register-resident one-pass kernels; checked against float64 torch and against
+# the streaming kernels (dropout masks identical: same counter hash)
+@pytest.mark.parametrize("n,c,h,silu,drop,add", [(3, 32, 28, True, 0.0, True), (3, 64, 14, True, 0.1, False),
+                                                  (2, 128, 7, False, 0.0, True), (2, 256, 14, True, 0.0, False),
+                                                  (2, 512, 7, True, 0.1, True), (2, 128, 28, True, 0.0, False),
+                                                  (2, 2048, 4, True, 0.0, True), (5, 96, 9, True, 0.0, False)])
+def test_group_norm_resident_matches_streaming_and_float64(dev, n, c, h, silu, drop, add):
+    g = torch.Generator().manual_seed(c * 7 + h)
+    G = min(32, c)
+    x = (torch.randn(n, h, h, c, generator=g) * 1.5 + 0.3).to(dev)
+    gamma = (1 + 0.2 * torch.randn(c, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(c, generator=g)).to(dev)
+    dy = torch.randn(n, h, h, c, generator=g).to(dev)
+    ad = torch.randn(n, h, h, c, generator=g).to(dev) if add else None
+    res = _gn_raw(0, x, gamma, beta, dy, ad, G, silu, drop, 77)
+    stream = _gn_raw(1, x, gamma, beta, dy, ad, G, silu, drop, 77)
+    for a, b in zip(res, stream):
+        assert rel(a, b) < 1e-5
+    assert torch.equal(res[0] == 0, stream[0] == 0)  # same dropout mask
+    if drop == 0.0:
+        xr = x.double().permute(0, 3, 1, 2).cpu().requires_grad_()
+        gr, br = gamma.double().cpu().requires_grad_(), beta.double().cpu().requires_grad_()
+        yr = F.group_norm(xr, G, gr, br, eps=1e-6)
+        if silu:
+            yr = yr * torch.sigmoid(yr)
+        (yr * dy.double().permute(0, 3, 1, 2).cpu()).sum().backward()
+        y, _, _, dx, dg, db = res
+        assert rel(y.permute(0, 3, 1, 2).cpu(), yr) < FP32_TOL
+        exp_dx = xr.grad + (ad.double().permute(0, 3, 1, 2).cpu() if add else 0.0)
+        assert rel(dx.permute(0, 3, 1, 2).cpu(), exp_dx) < 1e-5
+        assert rel(dg.cpu() - 0.5, gr.grad) < 1e-5
+        assert rel(db.cpu() + 0.25, br.grad) < 1e-5
+    # bitwise reproducible run to run
+    again = _gn_raw(0, x, gamma, beta, dy, ad, G, silu, drop, 77)
+    for a, b in zip(res, again):
+        assert torch.equal(a, b)
+
+
 def test_dropout_mask_statistics_and_grad_consistency(dev):
     from medvae_disentangled_multimodal_amd import ops
     x = cl(torch.randn(4, 64, 16, 16), dev).requires_grad_()
