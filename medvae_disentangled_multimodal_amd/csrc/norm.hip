@@ -423,17 +423,23 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
 
 // ------------------------------------------------------------------------------------------
 // Resident GroupNorm for small per-sample tensors (the 28x28 / 14x14 / 7x7 levels of c2 / c3, where the
-// producing conv cannot emit the statistics: h*w % 32 != 0). A workgroup owns (sample b, slab of SC
-// channels = whole groups) and holds the slab in registers (IT float4 per thread), so x is read from HBM
-// ONCE per pass: forward = statistics (two-pass: mean, then centred variance, on the resident values) +
-// apply in one launch (8 B/elem); backward = partial sums + finalize + dx in one launch (12 B/elem, +4 with
-// the residual-branch add) and a per-channel parameter-gradient reduction. Cross-thread sums: a fixed wave
-// butterfly, then a fixed-order LDS combine -- bitwise reproducible.
-// Thread map: C4 = SC/4 (a power of two <= 256) channel quads, rpar = 256 / C4 row phases, thread (rph, c4)
+// producing conv cannot emit the statistics: h*w % 32 != 0). The work is cut into UNITS = (sample b, slab of
+// SC channels = whole groups); a unit is held in registers (IT float4 per thread), so x is read from HBM ONCE
+// per pass: forward = statistics (two-pass: mean, then centred variance, on the resident values) + apply in
+// one launch (8 B/elem); backward = partial sums + finalize + dx in one launch (12 B/elem, +4 with the
+// residual-branch add) plus a per-channel parameter-gradient reduction.
+// Persistent workgroups walk units u = blockIdx.x, + gridDim.x, ... with a one-unit-deep register prefetch:
+// the next unit's loads are in flight while this unit reduces and stores, so the read and write phases of
+// consecutive units overlap (a one-shot grid would serialize them chip-wide).
+// Cross-thread sums: a fixed wave butterfly, then a fixed-order LDS combine -- bitwise reproducible.
+// Thread map: C4 = SC/4 (a power of two <= NT) channel quads, rpar = NT / C4 row phases; thread (rph, c4)
 // walks rows rph, rph + rpar, ... (at most IT of them).
 // ------------------------------------------------------------------------------------------
+constexpr int GN_RES_NT = 512;
+constexpr int GN_RES_MAXC = 2048;  // slab channels (C4 <= GN_RES_NT)
+
 template <int K>
-__device__ __forceinline__ void gn_slab_reduce(float (&s)[K], int C4, float* red /*[K][256]*/, float* out /*[C4][K]*/) {
+__device__ __forceinline__ void gn_slab_reduce(float (&s)[K], int C4, float* red /*[K][NT]*/, float* out /*[C4][K]*/) {
   const int tid = threadIdx.x;
   if (C4 < 64) {
     for (int m = C4; m < 64; m <<= 1) {  // lanes with the same c4 differ by multiples of C4
@@ -442,56 +448,100 @@ __device__ __forceinline__ void gn_slab_reduce(float (&s)[K], int C4, float* red
     }
   }
 #pragma unroll
-  for (int k = 0; k < K; ++k) red[k * 256 + tid] = s[k];
+  for (int k = 0; k < K; ++k) red[k * GN_RES_NT + tid] = s[k];
   __syncthreads();
   if (tid < C4) {
     const int stride = C4 < 64 ? 64 : C4;  // one representative per (wave, c4)
     float t[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) t[k] = 0.f;
-    for (int j = tid; j < 256; j += stride)
+    for (int j = tid; j < GN_RES_NT; j += stride)
 #pragma unroll
-      for (int k = 0; k < K; ++k) t[k] += red[k * 256 + j];
+      for (int k = 0; k < K; ++k) t[k] += red[k * GN_RES_NT + j];
 #pragma unroll
     for (int k = 0; k < K; ++k) out[tid * K + k] = t[k];
   }
   __syncthreads();
 }
 
-constexpr int GN_RES_MAXC = 1024;  // slab channels (C4 <= 256)
+// Unit geometry (uniform across the workgroup). Every access of a unit goes through a buffer descriptor based
+// at (b, row 0, channel c0) whose range ends at the sample's end: the thread's lane offset is one VGPR and the
+// row step i*rpar*C*4 an SGPR, and rows past hw fall outside the range (loads read 0, stores are dropped).
+typedef __attribute__((ext_vector_type(4))) unsigned gn_u32x4;
+struct GnUnit {
+  int b, c0;
+  long long ubase;  // element offset of (b, row 0, channel c0)
+  unsigned bytes;   // descriptor range: from ubase to the end of sample b
+  __device__ GnUnit(const GnArgs& a, int SC, int u) {
+    const int nsl = a.C / SC;
+    b = u / nsl;
+    c0 = (u - b * nsl) * SC;
+    ubase = (long long)b * a.hw * a.C + c0;
+    bytes = (unsigned)(((long long)a.hw * a.C - c0) * 4);
+  }
+  __device__ __amdgpu_buffer_rsrc_t rsrc(const float* p) const {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p + ubase), (short)0, (int)bytes, 0x00020000);
+  }
+};
 
 template <int IT>
-__global__ void __launch_bounds__(256) gn_fwd_resident_kernel(GnArgs a, int SC, float* __restrict__ y,
-                                                              float* __restrict__ mean, float* __restrict__ rstd,
-                                                              float eps) {
-  __shared__ float red[4 * 256];
-  __shared__ float chs[GN_RES_MAXC];
-  __shared__ float gmu[GN_RES_MAXC], grs[GN_RES_MAXC];  // per slab channel: its group's mean / rstd
-  const int tid = threadIdx.x, b = blockIdx.y, c0 = blockIdx.x * SC;
-  const int C4 = SC >> 2, rpar = 256 / C4, c4 = tid & (C4 - 1), rph = tid / C4;
+__device__ __forceinline__ void gn_res_load(const float* p, const GnArgs& a, int SC, int u, unsigned vo, int rstep,
+                                            bool on, float4 (&v)[IT]) {
+  if (!on) {  // uniform
+#pragma unroll
+    for (int i = 0; i < IT; ++i) v[i] = float4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t r = GnUnit(a, SC, u).rsrc(p);
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const gn_u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, vo, i * rstep, 0);
+    v[i] = float4{__uint_as_float(t.x), __uint_as_float(t.y), __uint_as_float(t.z), __uint_as_float(t.w)};
+  }
+}
+// Stores take the row step in the VGPR offset with soffset = 0: gfx950 has the "VALU overwrites the data VGPRs
+// of a just-issued >8-byte VMEM store" hazard also for buffer stores with an SGPR soffset, which the compiler
+// does not guard (it inserts the wait state only without an SGPR soffset). Measured: with the row step in
+// soffset, a few % of the dx stores of this kernel landed corrupted (tools/gn_stress.py, 14 of 80 runs).
+__device__ __forceinline__ void gn_res_store(__amdgpu_buffer_rsrc_t r, unsigned off, gn_u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+__device__ __forceinline__ gn_u32x4 gn_bits(float4 v) {
+  return gn_u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+}
+
+struct GnFwdSmem {
+  float red[4 * GN_RES_NT];
+  float chs[GN_RES_MAXC];
+  float gmu[GN_RES_MAXC], grs[GN_RES_MAXC];  // per slab channel: its group's mean / rstd
+};
+
+template <int IT>
+__device__ __forceinline__ void gn_fwd_unit(const GnArgs& a, int SC, int u, const float4 (&v)[IT], GnFwdSmem& sm,
+                                            float* __restrict__ y, float* __restrict__ mean, float* __restrict__ rstd,
+                                            float eps) {
+  const int tid = threadIdx.x;
+  const int C4 = SC >> 2, rpar = GN_RES_NT / C4, c4 = tid & (C4 - 1), rph = tid / C4;
   const int cpg = a.C / a.G, ngl = SC / cpg;
   const double n = (double)a.hw * cpg;
-  const long long sbase = (long long)b * a.hw * a.C + c0 + c4 * 4;
-  float4 v[IT];
+  const GnUnit un(a, SC, u);
   float s[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
-    const int r = rph + i * rpar;
-    v[i] = r < a.hw ? gn_ld4(a.x + sbase + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
     s[0] += v[i].x; s[1] += v[i].y; s[2] += v[i].z; s[3] += v[i].w;
   }
-  gn_slab_reduce<4>(s, C4, red, chs);
-  for (int gl = tid; gl < ngl; gl += 256) {
+  gn_slab_reduce<4>(s, C4, sm.red, sm.chs);
+  for (int gl = tid; gl < ngl; gl += GN_RES_NT) {
     float t = 0.f;
-    for (int j = 0; j < cpg; ++j) t += chs[gl * cpg + j];
+    for (int j = 0; j < cpg; ++j) t += sm.chs[gl * cpg + j];
     const float mu = (float)((double)t / n);
-    for (int j = 0; j < cpg; ++j) gmu[gl * cpg + j] = mu;
+    for (int j = 0; j < cpg; ++j) sm.gmu[gl * cpg + j] = mu;
   }
   __syncthreads();
   float mu[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    mu[e] = gmu[c4 * 4 + e];
+    mu[e] = sm.gmu[c4 * 4 + e];
     s[e] = 0.f;
   }
 #pragma unroll
@@ -501,82 +551,98 @@ __global__ void __launch_bounds__(256) gn_fwd_resident_kernel(GnArgs a, int SC, 
       s[0] = fmaf(d0, d0, s[0]); s[1] = fmaf(d1, d1, s[1]); s[2] = fmaf(d2, d2, s[2]); s[3] = fmaf(d3, d3, s[3]);
     }
   }
-  gn_slab_reduce<4>(s, C4, red, chs);
-  for (int gl = tid; gl < ngl; gl += 256) {
+  gn_slab_reduce<4>(s, C4, sm.red, sm.chs);
+  for (int gl = tid; gl < ngl; gl += GN_RES_NT) {
     float t = 0.f;
-    for (int j = 0; j < cpg; ++j) t += chs[gl * cpg + j];
+    for (int j = 0; j < cpg; ++j) t += sm.chs[gl * cpg + j];
     const float rs = (float)(1.0 / sqrt((double)t / n + (double)eps));
-    for (int j = 0; j < cpg; ++j) grs[gl * cpg + j] = rs;
-    const int gi = b * a.G + c0 / cpg + gl;
-    mean[gi] = gmu[gl * cpg];
+    for (int j = 0; j < cpg; ++j) sm.grs[gl * cpg + j] = rs;
+    const int gi = un.b * a.G + un.c0 / cpg + gl;
+    mean[gi] = sm.gmu[gl * cpg];
     rstd[gi] = rs;
   }
   __syncthreads();
   float sc[4], sh[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const int c = c0 + c4 * 4 + e;
-    sc[e] = grs[c4 * 4 + e] * a.gamma[c];
+    const int c = un.c0 + c4 * 4 + e;
+    sc[e] = sm.grs[c4 * 4 + e] * a.gamma[c];
     sh[e] = a.beta[c] - mu[e] * sc[e];
   }
+  const __amdgpu_buffer_rsrc_t yr = un.rsrc(y);
+  const unsigned vo = (unsigned)(rph * a.C + c4 * 4) * 4u;
+  const int rstep = rpar * a.C * 4;
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
-    const int r = rph + i * rpar;
-    if (r >= a.hw) continue;
     float o[4] = {v[i].x * sc[0] + sh[0], v[i].y * sc[1] + sh[1], v[i].z * sc[2] + sh[2], v[i].w * sc[3] + sh[3]};
-    const long long off = sbase + (long long)r * a.C;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (a.silu) o[k] = o[k] * sigmoid_f(o[k]);
       if (a.drop_p > 0.f) {
+        const long long off = un.ubase + (long long)(rph + i * rpar) * a.C + c4 * 4;
         const float uu = hash_uniform(a.seed, (unsigned long long)(off + k));
         o[k] = (uu >= a.drop_p) ? o[k] / (1.f - a.drop_p) : 0.f;
       }
     }
     const float4 ov{o[0], o[1], o[2], o[3]};
-    if (a.y_split)
-      *(uint4*)(y + off) = split4_bf16(ov);
-    else
-      *(float4*)(y + off) = ov;
+    const uint4 sp = a.y_split ? split4_bf16(ov) : uint4{0u, 0u, 0u, 0u};
+    gn_res_store(yr, vo + (unsigned)(i * rstep), a.y_split ? gn_u32x4{sp.x, sp.y, sp.z, sp.w} : gn_bits(ov));  // rows past hw: dropped
   }
 }
 
-// backward; pws = [2][C][nb] fp64 per-sample channel sums {sum dyn, sum dyn*xhat} for the parameter gradients
 template <int IT>
-__global__ void __launch_bounds__(256) gn_bwd_resident_kernel(GnArgs a, int SC, double* __restrict__ pws,
-                                                              float* __restrict__ dx) {
-  __shared__ float red[8 * 256];
-  __shared__ float chs[GN_RES_MAXC * 2];
-  __shared__ float gk2[GN_RES_MAXC], gk3[GN_RES_MAXC];
-  const int tid = threadIdx.x, b = blockIdx.y, c0 = blockIdx.x * SC;
-  const int C4 = SC >> 2, rpar = 256 / C4, c4 = tid & (C4 - 1), rph = tid / C4;
+__global__ void __launch_bounds__(GN_RES_NT) gn_fwd_resident_kernel(GnArgs a, int SC, int units, float* __restrict__ y,
+                                                                    float* __restrict__ mean, float* __restrict__ rstd,
+                                                                    float eps) {
+  __shared__ GnFwdSmem sm;
+  const int C4 = SC >> 2, rpar = GN_RES_NT / C4, c4 = threadIdx.x & (C4 - 1), rph = threadIdx.x / C4;
+  const int G = gridDim.x;
+  const unsigned vo = (unsigned)(rph * a.C + c4 * 4) * 4u;
+  const int rstep = rpar * a.C * 4;
+  float4 va[IT], vb[IT];
+  int u = blockIdx.x;
+  gn_res_load<IT>(a.x, a, SC, u, vo, rstep, u < units, va);
+  while (u < units) {  // ping-pong: the next unit's loads fly while this one reduces and stores
+    gn_res_load<IT>(a.x, a, SC, u + G, vo, rstep, u + G < units, vb);
+    gn_fwd_unit<IT>(a, SC, u, va, sm, y, mean, rstd, eps);
+    u += G;
+    if (u >= units) break;
+    gn_res_load<IT>(a.x, a, SC, u + G, vo, rstep, u + G < units, va);
+    gn_fwd_unit<IT>(a, SC, u, vb, sm, y, mean, rstd, eps);
+    u += G;
+  }
+}
+
+struct GnBwdSmem {
+  float red[8 * GN_RES_NT];
+  float chs[GN_RES_MAXC * 2];
+  float gk2[GN_RES_MAXC], gk3[GN_RES_MAXC];
+};
+
+// backward of one unit; pws = [2][C][nb] fp64 per-sample channel sums {sum dyn, sum dyn*xhat}
+template <int IT>
+__device__ __forceinline__ void gn_bwd_unit(const GnArgs& a, int SC, int u, const float4 (&xv)[IT], float4 (&dv)[IT],
+                                            GnBwdSmem& sm, double* __restrict__ pws, float* __restrict__ dx) {
+  const int tid = threadIdx.x;
+  const int C4 = SC >> 2, rpar = GN_RES_NT / C4, c4 = tid & (C4 - 1), rph = tid / C4;
   const int cpg = a.C / a.G, ngl = SC / cpg;
-  const long long sbase = (long long)b * a.hw * a.C + c0 + c4 * 4;
+  const GnUnit un(a, SC, u);
+  const unsigned vo = (unsigned)(rph * a.C + c4 * 4) * 4u;
+  const int rstep = rpar * a.C * 4;
   float m[4], rs[4], gm[4], bt[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const int c = c0 + c4 * 4 + e, bg = b * a.G + c / cpg;
+    const int c = un.c0 + c4 * 4 + e, bg = un.b * a.G + c / cpg;
     m[e] = a.mean[bg];
     rs[e] = a.rstd[bg];
     gm[e] = a.gamma[c];
     bt[e] = a.beta[c];
   }
-  float4 xv[IT], dv[IT], av[IT];
-  const bool add = a.dx_add != nullptr;
-#pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    const int r = rph + i * rpar;
-    const bool ok = r < a.hw;
-    const long long off = sbase + (long long)r * a.C;
-    xv[i] = ok ? gn_ld4(a.x + off) : float4{0.f, 0.f, 0.f, 0.f};
-    dv[i] = ok ? gn_ld4(a.dy + off) : float4{0.f, 0.f, 0.f, 0.f};
-    av[i] = (add && ok) ? gn_ld4(a.dx_add + off) : float4{0.f, 0.f, 0.f, 0.f};
-  }
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
-    const long long off = sbase + (long long)(rph + i * rpar) * a.C;
-    float xs[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+    const long long off = un.ubase + (long long)(rph + i * rpar) * a.C + c4 * 4;
+    const float xs[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
     float ds[4] = {dv[i].x, dv[i].y, dv[i].z, dv[i].w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -595,49 +661,74 @@ __global__ void __launch_bounds__(256) gn_bwd_resident_kernel(GnArgs a, int SC, 
       s[e] += d;
       s[4 + e] = fmaf(d, xh, s[4 + e]);
     }
-    dv[i] = float4{ds[0], ds[1], ds[2], ds[3]};
+    dv[i] = float4{ds[0], ds[1], ds[2], ds[3]};  // now the gradient at the normalized output (dropout / SiLU)
   }
   // chs[(c4*8) + k]: k 0-3 = sum dyn of channels c4*4+k, k 4-7 = sum dyn*xhat
-  gn_slab_reduce<8>(s, C4, red, chs);
-  for (int t = tid; t < SC; t += 256) {
-    const int q = t >> 2, e = t & 3, c = c0 + t;
-    pws[(long long)c * a.nb + b] = chs[q * 8 + e];
-    pws[((long long)a.C + c) * a.nb + b] = chs[q * 8 + 4 + e];
+  gn_slab_reduce<8>(s, C4, sm.red, sm.chs);
+  for (int t = tid; t < SC; t += GN_RES_NT) {
+    const int q = t >> 2, e = t & 3, c = un.c0 + t;
+    pws[(long long)c * a.nb + un.b] = sm.chs[q * 8 + e];
+    pws[((long long)a.C + c) * a.nb + un.b] = sm.chs[q * 8 + 4 + e];
   }
-  for (int gl = tid; gl < ngl; gl += 256) {
+  for (int gl = tid; gl < ngl; gl += GN_RES_NT) {
     double A1 = 0.0, A2 = 0.0;
     for (int j = 0; j < cpg; ++j) {
       const int cl = gl * cpg + j;
-      const double g = a.gamma[c0 + cl];
-      A1 += g * chs[(cl >> 2) * 8 + (cl & 3)];
-      A2 += g * chs[(cl >> 2) * 8 + 4 + (cl & 3)];
+      const double g = a.gamma[un.c0 + cl];
+      A1 += g * sm.chs[(cl >> 2) * 8 + (cl & 3)];
+      A2 += g * sm.chs[(cl >> 2) * 8 + 4 + (cl & 3)];
     }
-    const int gi = b * a.G + c0 / cpg + gl;
+    const int gi = un.b * a.G + un.c0 / cpg + gl;
     const double n = (double)a.hw * cpg, r = a.rstd[gi], mu = a.mean[gi];
     const float k2 = (float)(-r * r * A2 / n), k3 = (float)(-r * A1 / n + mu * r * r * A2 / n);
     for (int j = 0; j < cpg; ++j) {
-      gk2[gl * cpg + j] = k2;
-      gk3[gl * cpg + j] = k3;
+      sm.gk2[gl * cpg + j] = k2;
+      sm.gk3[gl * cpg + j] = k3;
     }
   }
+  // the residual branch's gradient: loaded here, its latency behind the finalize barrier
+  float4 av[IT];
+  gn_res_load<IT>(a.dx_add, a, SC, u, vo, rstep, a.dx_add != nullptr, av);
   __syncthreads();
   float q1[4], q2[4], q3[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     q1[e] = rs[e] * gm[e];
-    q2[e] = gk2[c4 * 4 + e];
-    q3[e] = gk3[c4 * 4 + e];
+    q2[e] = sm.gk2[c4 * 4 + e];
+    q3[e] = sm.gk3[c4 * 4 + e];
   }
+  const __amdgpu_buffer_rsrc_t dr = un.rsrc(dx);
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
-    const int r = rph + i * rpar;
-    if (r >= a.hw) continue;
-    float4 o{dv[i].x * q1[0] + xv[i].x * q2[0] + q3[0], dv[i].y * q1[1] + xv[i].y * q2[1] + q3[1],
-             dv[i].z * q1[2] + xv[i].z * q2[2] + q3[2], dv[i].w * q1[3] + xv[i].w * q2[3] + q3[3]};
-    if (add) {
-      o.x += av[i].x; o.y += av[i].y; o.z += av[i].z; o.w += av[i].w;
-    }
-    *(float4*)(dx + sbase + (long long)r * a.C) = o;
+    // av is zero when there is no residual-branch gradient; rows past hw: the store is dropped
+    const float4 o{dv[i].x * q1[0] + xv[i].x * q2[0] + q3[0] + av[i].x, dv[i].y * q1[1] + xv[i].y * q2[1] + q3[1] + av[i].y,
+                   dv[i].z * q1[2] + xv[i].z * q2[2] + q3[2] + av[i].z, dv[i].w * q1[3] + xv[i].w * q2[3] + q3[3] + av[i].w};
+    gn_res_store(dr, vo + (unsigned)(i * rstep), gn_bits(o));
+  }
+}
+
+template <int IT>
+__global__ void __launch_bounds__(GN_RES_NT) gn_bwd_resident_kernel(GnArgs a, int SC, int units, double* __restrict__ pws,
+                                                                    float* __restrict__ dx) {
+  __shared__ GnBwdSmem sm;
+  const int C4 = SC >> 2, rpar = GN_RES_NT / C4, c4 = threadIdx.x & (C4 - 1), rph = threadIdx.x / C4;
+  const int G = gridDim.x;
+  float4 xa[IT], da[IT], xb[IT], db[IT];
+  const unsigned vo = (unsigned)(rph * a.C + c4 * 4) * 4u;
+  const int rstep = rpar * a.C * 4;
+  int u = blockIdx.x;
+  gn_res_load<IT>(a.x, a, SC, u, vo, rstep, u < units, xa);
+  gn_res_load<IT>(a.dy, a, SC, u, vo, rstep, u < units, da);
+  while (u < units) {  // ping-pong prefetch of x and dy, as in the forward
+    gn_res_load<IT>(a.x, a, SC, u + G, vo, rstep, u + G < units, xb);
+    gn_res_load<IT>(a.dy, a, SC, u + G, vo, rstep, u + G < units, db);
+    gn_bwd_unit<IT>(a, SC, u, xa, da, sm, pws, dx);
+    u += G;
+    if (u >= units) break;
+    gn_res_load<IT>(a.x, a, SC, u + G, vo, rstep, u + G < units, xa);
+    gn_res_load<IT>(a.dy, a, SC, u + G, vo, rstep, u + G < units, da);
+    gn_bwd_unit<IT>(a, SC, u, xb, db, sm, pws, dx);
+    u += G;
   }
 }
 
@@ -664,30 +755,52 @@ __global__ void __launch_bounds__(256) gn_param_reduce_kernel(const double* __re
   }
 }
 
-// Largest slab (of >= 16 channels: 64-B row segments) with <= 16 rows per thread that still gives >= 512
-// workgroups; else the feasible slab with the most workgroups.
-// slab width for the resident path (0: not eligible). Path selection: mvae_set_group_norm_path (0 auto,
+// Slab width for the resident path (0: not eligible). Path selection: mvae_set_group_norm_path (0 auto,
 // 1 streaming only); before any call, MVAE_GN_RESIDENT=0 selects streaming only.
+// Largest slab (of >= 16 channels: 64-B row segments) with <= max_it rows per thread (forward 16: one 128-B
+// row segment per 8 lanes at the 28x28x32 level, 41 -> 33 us; backward 8: two units of x and dy in registers).
 static int g_gn_path = -1;
-static int gn_resident_slab(int nb, int hw, int C, int G, int* items) {
+static int gn_resident_slab(int nb, int hw, int C, int G, int* items, int max_it) {
   if (g_gn_path < 0) {
     const char* e = getenv("MVAE_GN_RESIDENT");
     g_gn_path = (e != nullptr && e[0] == '0') ? 1 : 0;
   }
   if (g_gn_path == 1 || C % G) return 0;
   const int cpg = C / G;
-  int best = 0, best_it = 0;
   for (int sc = std::min(C, GN_RES_MAXC); sc >= 16; sc >>= 1) {
     const int c4 = sc >> 2;
-    if ((c4 & (c4 - 1)) || C % sc || sc % cpg) continue;
-    const int it = (hw + 256 / c4 - 1) / (256 / c4);
-    if (it > 16) continue;
-    best = sc;
-    best_it = it;
-    if ((long long)nb * (C / sc) >= 512) break;
+    if ((c4 & (c4 - 1)) || c4 > GN_RES_NT || C % sc || sc % cpg) continue;
+    const int rpar = GN_RES_NT / c4, it = (hw + rpar - 1) / rpar;
+    if (it > max_it) continue;
+    *items = it <= 4 ? 4 : it <= 8 ? 8 : 16;
+    return sc;
   }
-  *items = best_it <= 4 ? 4 : best_it <= 8 ? 8 : 16;
-  return best;
+  return 0;
+}
+
+// persistent grid: as many workgroups as fit on the chip at once (occupancy query, cached per kernel/device)
+static int gn_res_grid(const void* kernel, int units) {
+  struct Entry { const void* k; int dev, slots; };
+  static Entry cache[16];
+  static int n_cache = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int slots = 0;
+  for (int i = 0; i < n_cache; ++i)
+    if (cache[i].k == kernel && cache[i].dev == dev) slots = cache[i].slots;
+  if (slots == 0) {
+    int cus = 0, per_cu = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, GN_RES_NT, 0);
+    slots = std::max(1, cus) * std::max(1, per_cu);
+    if (n_cache < 16) cache[n_cache++] = Entry{kernel, dev, slots};
+  }
+  // experiment knob: MVAE_GN_RES_GRID = k > 0: k x the resident slots; 0: one workgroup per unit (no persistence)
+  if (const char* e = getenv("MVAE_GN_RES_GRID")) {
+    const int k = atoi(e);
+    return k <= 0 ? units : std::max(1, std::min(units, slots * k));
+  }
+  return std::max(1, std::min(units, slots));
 }
 
 static int gn_target_blocks() {
@@ -746,12 +859,19 @@ int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* be
   a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
   a.ws = (double*)workspace;
   int it = 0;
-  if (const int sc = gn_resident_slab(nb, hw, c, groups, &it)) {
+  static const int fwd_max_it = [] {
+    const char* e = getenv("MVAE_GN_RES_FWD_IT");  // experiment knob: rows per thread allowed in the forward
+    return e ? atoi(e) : 16;
+  }();
+  if (const int sc = gn_resident_slab(nb, hw, c, groups, &it, fwd_max_it)) {
     a.silu = silu; a.drop_p = drop_p; a.seed = seed; a.y_split = y_split;
-    const dim3 grid(c / sc, nb);
-    if (it == 4) hipLaunchKernelGGL(gn_fwd_resident_kernel<4>, grid, dim3(256), 0, st, a, sc, y, mean, rstd, eps);
-    else if (it == 8) hipLaunchKernelGGL(gn_fwd_resident_kernel<8>, grid, dim3(256), 0, st, a, sc, y, mean, rstd, eps);
-    else hipLaunchKernelGGL(gn_fwd_resident_kernel<16>, grid, dim3(256), 0, st, a, sc, y, mean, rstd, eps);
+    const int units = nb * (c / sc);
+    const void* k = it == 4 ? (const void*)gn_fwd_resident_kernel<4>
+                  : it == 8 ? (const void*)gn_fwd_resident_kernel<8> : (const void*)gn_fwd_resident_kernel<16>;
+    const dim3 grid(gn_res_grid(k, units));
+    if (it == 4) hipLaunchKernelGGL(gn_fwd_resident_kernel<4>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, y, mean, rstd, eps);
+    else if (it == 8) hipLaunchKernelGGL(gn_fwd_resident_kernel<8>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, y, mean, rstd, eps);
+    else hipLaunchKernelGGL(gn_fwd_resident_kernel<16>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, y, mean, rstd, eps);
     return launch_status();
   }
   float* scale = (float*)((char*)workspace + (size_t)nb * a.chunks * c * 2 * sizeof(double));
@@ -815,12 +935,17 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
   a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
   a.ws = (double*)workspace;
   int it = 0;
-  if (const int sc = gn_resident_slab(nb, hw, c, groups, &it)) {
+  int sc = gn_resident_slab(nb, hw, c, groups, &it, 8);
+  // the backward holds x and dy of two units (2 waves/SIMD): with 64-B row segments (sc < 32) it streams at
+  // ~3.1 TB/s, below the streaming kernels on tensors past ~64 MB (c2's 28x28x128 level: 140 vs 124 us)
+  if (sc > 0 && sc < 32 && (long long)nb * hw * c * 4 > (64LL << 20)) sc = 0;
+  if (sc) {
     double* pws = (double*)workspace;  // [2][C][nb] fp64 (within the [nb][chunks][C][2] partial area)
-    const dim3 grid(c / sc, nb);
-    if (it == 4) hipLaunchKernelGGL(gn_bwd_resident_kernel<4>, grid, dim3(256), 0, st, a, sc, pws, dx);
-    else if (it == 8) hipLaunchKernelGGL(gn_bwd_resident_kernel<8>, grid, dim3(256), 0, st, a, sc, pws, dx);
-    else hipLaunchKernelGGL(gn_bwd_resident_kernel<16>, grid, dim3(256), 0, st, a, sc, pws, dx);
+    const int units = nb * (c / sc);
+    const void* k = it == 4 ? (const void*)gn_bwd_resident_kernel<4> : (const void*)gn_bwd_resident_kernel<8>;
+    const dim3 grid(gn_res_grid(k, units));
+    if (it == 4) hipLaunchKernelGGL(gn_bwd_resident_kernel<4>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, pws, dx);
+    else hipLaunchKernelGGL(gn_bwd_resident_kernel<8>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, pws, dx);
     if (dgamma || dbeta)
       hipLaunchKernelGGL(gn_param_reduce_kernel, dim3(c), dim3(256), 0, st, (const double*)pws, nb, c, dgamma, dbeta);
     return launch_status();
