@@ -1274,18 +1274,32 @@ inline void set_splits(GemmArgs& a, int splits) {
 // Split-K factor: fill the chip AND avoid wave quantisation (a last round of blocks that leaves
 // most CUs idle): the smallest s whose tiles*s blocks make >= 1 round of 256 CUs at >= 95 % round
 // efficiency (fewer splits = less partial-sum traffic); otherwise the most efficient s.
+// A "round" counts the workgroups resident per CU at once (1 for the 256-wide tiles, 2 for 128x128, 4 for
+// 64x64 / 128x16): a small-tile split-K GEMM (c3's wgrad of 32-128 channels: M x N = 32 x 288 .. 128 x 1152,
+// K = 25k-400k pixels) with one workgroup per CU runs its K loop latency-bound (one tile in flight per CU).
+constexpr int MAX_SPLITS = 256;
+inline bool split_res_legacy() {  // experiment knob: MVAE_SPLIT_LEGACY=1 restores one-workgroup-per-CU rounds
+  static int v = getenv("MVAE_SPLIT_LEGACY") != nullptr;
+  return v != 0;
+}
 inline int choose_splits(const GemmArgs& a, int cfg) {
+  static const int res_of[6] = {1, 1, 1, 2, 4, 4};
+  const bool legacy = split_res_legacy();
+  const int res = legacy ? 1 : res_of[cfg];
+  const long long slots = 256LL * res;
   const long long tiles = tiles_of(cfg, a);
-  const int ms = std::max(1, (int)std::min<long long>(64, a.K / 512));
-  if (tiles >= 1024) return 1;
+  const int ms = legacy ? std::max(1, (int)std::min<long long>(64, a.K / 512))
+                        : std::max(1, (int)std::min<long long>(MAX_SPLITS, a.K / 256));
+  if (tiles >= 4 * slots) return 1;
   int best = 1;
   double best_eff = -1.0;
   for (int s = 1; s <= ms; ++s) {
     const long long blocks = tiles * s;
-    const long long rounds = (blocks + 255) / 256;
-    const double eff = (double)blocks / (double)(rounds * 256);
-    if (blocks >= 240 && eff >= 0.95) return s;
-    const double score = eff - (blocks < 240 ? 0.5 : 0.0);
+    const long long rounds = (blocks + slots - 1) / slots;
+    const double eff = (double)blocks / (double)(rounds * slots);
+    const bool full = blocks * 100 >= slots * 94;  // >= 240 of 256 slots
+    if (full && eff >= 0.95) return s;
+    const double score = eff - (full ? 0.0 : 0.5);
     if (score > best_eff + 1e-9) { best_eff = score; best = s; }
   }
   return best;

@@ -103,7 +103,7 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
     set_gather_magic(a);
     a.stride = stride; a.pad_t = pad_t; a.pad_l = pad_l;
     const int cfg = choose_tile(a, va && vb, workspace != nullptr);
-    const size_t bias_bytes = dbias ? ((size_t)64 * a.M * sizeof(float) + 256) : 0;
+    const size_t bias_bytes = dbias ? ((size_t)MAX_SPLITS * a.M * sizeof(float) + 256) : 0;
     if (dbias && workspace_bytes < bias_bytes) { set_error("wgrad: workspace too small"); return MVAE_EWORKSPACE; }
     plan_splits(a, cfg, workspace, workspace_bytes - bias_bytes);
     // bias partials live after the split-K partials
@@ -168,7 +168,7 @@ int mvae_conv2d_wgrad_upsample_nhwc(const float* dy, const float* x, float* dw, 
     a.stride = 1; a.pad_t = 1; a.pad_l = 1;
     a.sub_w2 = 2 * wd; a.sub_par = 0; a.out_remap = 0;
     const int cfg = choose_tile(a, va && vb, true);
-    const size_t bias_bytes = dbias ? ((size_t)4 * 64 * a.M * sizeof(float) + 256) : 0;
+    const size_t bias_bytes = dbias ? ((size_t)4 * MAX_SPLITS * a.M * sizeof(float) + 256) : 0;
     if (workspace_bytes < bias_bytes) { set_error("wgrad_upsample: workspace too small"); return MVAE_EWORKSPACE; }
     const size_t avail = workspace_bytes - bias_bytes;
     set_splits(a, choose_splits(a, cfg));
@@ -210,7 +210,7 @@ size_t mvae_conv2d_wgrad_upsample_workspace_bytes(int nb, int h, int wd, int cin
     set_splits(a, choose_splits(a, choose_tile(a, big != 0, true)));
     b = std::max(b, ups_part_bytes(a));
   }
-  return ((b + 255) & ~(size_t)255) + (size_t)4 * 64 * a.M * sizeof(float) + 256;
+  return ((b + 255) & ~(size_t)255) + (size_t)4 * MAX_SPLITS * a.M * sizeof(float) + 256;
 }
 
 size_t mvae_conv2d_wgrad_workspace_bytes(int nb, int cin, int cout, int kh, int kw, int ho, int wo) {
@@ -219,7 +219,7 @@ size_t mvae_conv2d_wgrad_workspace_bytes(int nb, int cin, int cout, int kh, int 
   set_splits(a, choose_splits(a, choose_tile(a, true, true)));
   size_t b1 = splitk_ws_bytes(a);
   set_splits(a, choose_splits(a, choose_tile(a, false, true)));
-  return ((std::max(b1, splitk_ws_bytes(a)) + 255) & ~(size_t)255) + (size_t)64 * a.M * sizeof(float) + 256;
+  return ((std::max(b1, splitk_ws_bytes(a)) + 255) & ~(size_t)255) + (size_t)MAX_SPLITS * a.M * sizeof(float) + 256;
 }
 
 }  // extern "C"
