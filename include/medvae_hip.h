@@ -95,6 +95,15 @@ int mvae_conv2d_wgrad_small_cout_nhwc(const float* dy, const float* x, float* dw
                                       int h, int w_, int cin, int cout, int x_split, void* workspace,
                                       size_t workspace_bytes, void* stream);
 size_t mvae_conv2d_wgrad_small_cout_workspace_bytes(int nb, int cin);
+/* Weight (+ bias) gradient of a 3x3 / stride-1 / pad-1 conv with cin, cout in {32, 64} (the 28x28 / 14x14 levels
+ * of the c3 disentangled model): replaces the implicit-GEMM form of convolution_backward's weight half there.
+ * Per-tap 32x32x16 MFMA products over LDS-resident row bands, persistent grid, fixed-order partial reduction.
+ * dw, dbias (optional) accumulate with beta. x_split: x holds split4_bf16 groups. Math modes 0 (3xBF16) and 1
+ * (bf16); the exact-fp32 mode is rejected (use mvae_conv2d_wgrad_nhwc). */
+int mvae_conv2d_wgrad_direct_nhwc(const float* dy, const float* x, float* dw, float* dbias, float beta, int nb, int h,
+                                  int w, int cin, int cout, int x_split, void* workspace, size_t workspace_bytes,
+                                  void* stream);
+size_t mvae_conv2d_wgrad_direct_workspace_bytes(int nb, int h, int w, int cin, int cout);
 
 /* Input gradient of a stride-2 conv (Downsample, encoder_decoder.py:184-188) by dx parity class: each
  * class is a dense stride-1 conv of dy [nb][ho][wo][cout] with its own <= 2x2 taps of wt [cin][kh][kw][cout]

@@ -436,6 +436,7 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
 // walks rows rph, rph + rpar, ... (at most IT of them).
 // ------------------------------------------------------------------------------------------
 constexpr int GN_RES_NT = 512;
+static int g_gn_path = -1;  // mvae_set_group_norm_path: 0 auto, 1 streaming only (-1: not yet read from the env)
 constexpr int GN_RES_MAXC = 2048;  // slab channels (C4 <= GN_RES_NT)
 
 template <int K>
@@ -732,6 +733,148 @@ __global__ void __launch_bounds__(GN_RES_NT) gn_bwd_resident_kernel(GnArgs a, in
   }
 }
 
+// Backward of a large per-sample tensor (c4's 64x64 / 32x32 levels) as units too: a workgroup owns
+// (sample, slab of whole groups) and streams it TWICE -- pass 1 (temporal loads) accumulates the partial sums,
+// the finalize runs in the workgroup, pass 2 re-reads x and dy (non-temporal, last use) and writes dx. With one
+// workgroup per CU the units in flight (256 x <= 128 KB) stay cached between the passes, so HBM sees x and dy
+// once (16 B/elem with the residual add) instead of the streaming chain's 24.
+template <int U>
+__global__ void __launch_bounds__(GN_RES_NT) gn_bwd_unit2_kernel(GnArgs a, int SC, int units, double* __restrict__ pws,
+                                                                 float* __restrict__ dx) {
+  __shared__ GnBwdSmem sm;
+  const int tid = threadIdx.x;
+  const int C4 = SC >> 2, rpar = GN_RES_NT / C4, c4 = tid & (C4 - 1), rph = tid / C4;
+  const int cpg = a.C / a.G, ngl = SC / cpg;
+  for (int u = blockIdx.x; u < units; u += gridDim.x) {
+    const GnUnit un(a, SC, u);
+    const long long tb = un.ubase + c4 * 4;  // this thread's channel quad, row 0
+    float m[4], rs[4], gm[4], bt[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = un.c0 + c4 * 4 + e, bg = un.b * a.G + c / cpg;
+      m[e] = a.mean[bg];
+      rs[e] = a.rstd[bg];
+      gm[e] = a.gamma[c];
+      bt[e] = a.beta[c];
+    }
+    auto dyn = [&](float4 xv, float4 dv, long long off, float (&d)[4], float (&xh)[4]) {
+      const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+      const float ds[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float g = ds[e];
+        if (a.drop_p > 0.f) {
+          const float uu = hash_uniform(a.seed, (unsigned long long)(off + e));
+          g = (uu >= a.drop_p) ? g / (1.f - a.drop_p) : 0.f;
+        }
+        xh[e] = (xs[e] - m[e]) * rs[e];
+        if (a.silu) {
+          const float yn = xh[e] * gm[e] + bt[e];
+          const float sg = sigmoid_f(yn);
+          g = g * sg * (1.f + yn * (1.f - sg));
+        }
+        d[e] = g;
+      }
+    };
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r0 = rph; r0 < a.hw; r0 += U * rpar) {  // pass 1: partial sums (loads keep the lines cached)
+      float4 xv[U], dv[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const int r = r0 + q * rpar;
+        const bool ok = r < a.hw;
+        xv[q] = ok ? *(const float4*)(a.x + tb + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+        dv[q] = ok ? *(const float4*)(a.dy + tb + (long long)r * a.C) : float4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        float d[4], xh[4];
+        dyn(xv[q], dv[q], tb + (long long)(r0 + q * rpar) * a.C, d, xh);  // rows past hw: dv = 0 -> d = 0
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s[e] += d[e];
+          s[4 + e] = fmaf(d[e], xh[e], s[4 + e]);
+        }
+      }
+    }
+    gn_slab_reduce<8>(s, C4, sm.red, sm.chs);
+    for (int t = tid; t < SC; t += GN_RES_NT) {
+      const int q = t >> 2, e = t & 3, c = un.c0 + t;
+      pws[(long long)c * a.nb + un.b] = sm.chs[q * 8 + e];
+      pws[((long long)a.C + c) * a.nb + un.b] = sm.chs[q * 8 + 4 + e];
+    }
+    for (int gl = tid; gl < ngl; gl += GN_RES_NT) {
+      double A1 = 0.0, A2 = 0.0;
+      for (int j = 0; j < cpg; ++j) {
+        const int cl = gl * cpg + j;
+        const double g = a.gamma[un.c0 + cl];
+        A1 += g * sm.chs[(cl >> 2) * 8 + (cl & 3)];
+        A2 += g * sm.chs[(cl >> 2) * 8 + 4 + (cl & 3)];
+      }
+      const int gi = un.b * a.G + un.c0 / cpg + gl;
+      const double n = (double)a.hw * cpg, r = a.rstd[gi], mu = a.mean[gi];
+      const float k2 = (float)(-r * r * A2 / n), k3 = (float)(-r * A1 / n + mu * r * r * A2 / n);
+      for (int j = 0; j < cpg; ++j) {
+        sm.gk2[gl * cpg + j] = k2;
+        sm.gk3[gl * cpg + j] = k3;
+      }
+    }
+    __syncthreads();
+    float q1[4], q2[4], q3[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      q1[e] = rs[e] * gm[e];
+      q2[e] = sm.gk2[c4 * 4 + e];
+      q3[e] = sm.gk3[c4 * 4 + e];
+    }
+    __syncthreads();  // gk2 / gk3 are rewritten by the next unit
+    const bool add = a.dx_add != nullptr;
+    for (int r0 = rph; r0 < a.hw; r0 += U * rpar) {  // pass 2: dx (last use of x and dy: non-temporal)
+      float4 xv[U], dv[U], av[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const int r = r0 + q * rpar;
+        const bool ok = r < a.hw;
+        const long long off = tb + (long long)r * a.C;
+        xv[q] = ok ? gn_ld4(a.x + off) : float4{0.f, 0.f, 0.f, 0.f};
+        dv[q] = ok ? gn_ld4(a.dy + off) : float4{0.f, 0.f, 0.f, 0.f};
+        av[q] = (add && ok) ? gn_ld4(a.dx_add + off) : float4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const int r = r0 + q * rpar;
+        if (r >= a.hw) continue;
+        const long long off = tb + (long long)r * a.C;
+        float d[4], xh[4];
+        dyn(xv[q], dv[q], off, d, xh);
+        const float xs[4] = {xv[q].x, xv[q].y, xv[q].z, xv[q].w};
+        *(float4*)(dx + off) = float4{d[0] * q1[0] + xs[0] * q2[0] + q3[0] + av[q].x,
+                                      d[1] * q1[1] + xs[1] * q2[1] + q3[1] + av[q].y,
+                                      d[2] * q1[2] + xs[2] * q2[2] + q3[2] + av[q].z,
+                                      d[3] * q1[3] + xs[3] * q2[3] + q3[3] + av[q].w};
+      }
+    }
+  }
+}
+
+// slab of the two-pass unit backward: >= 16 channels (64-B row segments), whole groups, <= 128 KB of x + dy
+// per unit. Opt-in (MVAE_GN_UNIT=1): whether the second pass hits in cache is not stable -- c4's 32x32x512
+// level measured 533 us in one run and 1068 us in another against the streaming chain's 600 (512-KB units at
+// 64x64: 1.9x slower every time).
+static int gn_unit2_slab(int hw, int C, int G) {
+  static const bool off = [] {  // opt-in: MVAE_GN_UNIT=1
+    const char* e = getenv("MVAE_GN_UNIT");
+    return e == nullptr || e[0] != '1';
+  }();
+  if (off || g_gn_path == 1 || C % G) return 0;
+  const int cpg = C / G;
+  for (int sc = 64; sc >= 16; sc >>= 1) {
+    if (C % sc || sc % cpg) continue;
+    if ((long long)hw * sc * 8 <= (128LL << 10)) return sc;
+  }
+  return 0;
+}
+
 // dgamma[c] += sum_b pws[1][c][b], dbeta[c] += sum_b pws[0][c][b]: one block per channel, fixed order
 __global__ void __launch_bounds__(256) gn_param_reduce_kernel(const double* __restrict__ pws, int nb, int C,
                                                               float* dgamma, float* dbeta) {
@@ -759,7 +902,6 @@ __global__ void __launch_bounds__(256) gn_param_reduce_kernel(const double* __re
 // 1 streaming only); before any call, MVAE_GN_RESIDENT=0 selects streaming only.
 // Largest slab (of >= 16 channels: 64-B row segments) with <= max_it rows per thread (forward 16: one 128-B
 // row segment per 8 lanes at the 28x28x32 level, 41 -> 33 us; backward 8: two units of x and dy in registers).
-static int g_gn_path = -1;
 static int gn_resident_slab(int nb, int hw, int C, int G, int* items, int max_it) {
   if (g_gn_path < 0) {
     const char* e = getenv("MVAE_GN_RESIDENT");
@@ -946,6 +1088,22 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
     const dim3 grid(gn_res_grid(k, units));
     if (it == 4) hipLaunchKernelGGL(gn_bwd_resident_kernel<4>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, pws, dx);
     else hipLaunchKernelGGL(gn_bwd_resident_kernel<8>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, pws, dx);
+    if (dgamma || dbeta)
+      hipLaunchKernelGGL(gn_param_reduce_kernel, dim3(c), dim3(256), 0, st, (const double*)pws, nb, c, dgamma, dbeta);
+    return launch_status();
+  }
+  if (const int sc2 = gn_unit2_slab(hw, c, groups)) {
+    double* pws = (double*)workspace;
+    const int units = nb * (c / sc2);
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    static const int per_cu = [] {
+      const char* e = getenv("MVAE_GN_UNIT_PER_CU");  // experiment knob: workgroups per CU
+      return e ? std::max(1, atoi(e)) : 1;
+    }();
+    const dim3 grid(std::max(1, std::min(units, std::max(1, cus) * per_cu)));
+    hipLaunchKernelGGL(gn_bwd_unit2_kernel<4>, grid, dim3(GN_RES_NT), 0, st, a, sc2, units, pws, dx);
     if (dgamma || dbeta)
       hipLaunchKernelGGL(gn_param_reduce_kernel, dim3(c), dim3(256), 0, st, (const double*)pws, nb, c, dgamma, dbeta);
     return launch_status();

@@ -64,6 +64,12 @@ CONV_CASES = [
     # skinny-N 128x16 tiles (>= 512 tiles): conv_out forward (cout 3), conv_in input gradient (cin 6)
     (64, 64, 3, 32, 32, 3, 1, (1, 1, 1, 1), False),
     (64, 6, 64, 32, 32, 3, 1, (1, 1, 1, 1), False),
+    # direct small-channel weight gradient (cin, cout in {32, 64}): c3 level shapes, odd / non-square images,
+    # more bands than workgroups (persistent loop)
+    (3, 64, 32, 28, 28, 3, 1, (1, 1, 1, 1), False),
+    (2, 64, 32, 14, 14, 3, 1, (1, 1, 1, 1), False),
+    (2, 32, 32, 9, 11, 3, 1, (1, 1, 1, 1), False),
+    (600, 32, 32, 7, 5, 3, 1, (1, 1, 1, 1), False),
 ]
 
 
@@ -113,6 +119,34 @@ def test_conv_fwd_dgrad_wgrad(dev, case):
     assert wm.grad is None and bm.grad is None
     assert rel(wm._mvae_main_grad - 0.5, wr.grad) < CONV_TOL
     assert float((bm._mvae_main_grad.cpu().double() - 0.25 - db_ref).abs().max()) < 1e-5 * scale
+
+
+@pytest.mark.parametrize("ci,co,h,w,beta", [(32, 32, 28, 28, 0.0), (64, 32, 14, 14, 1.0), (32, 64, 14, 14, 0.5),
+                                              (64, 64, 9, 11, 0.0)])
+def test_wgrad_direct_capi_channel_pairs(dev, ci, co, h, w, beta):
+    """mvae_conv2d_wgrad_direct_nhwc for every (cin, cout) pair it accepts (ops routes only cout 32 to it): dw and
+    dbias accumulate with beta, against a float64 reference."""
+    from medvae_disentangled_multimodal_amd import _lib
+    n = 3
+    g = torch.Generator().manual_seed(ci * 3 + co + h)
+    x = torch.randn(n, h, w, ci, generator=g)
+    dy = torch.randn(n, h, w, co, generator=g)
+    dw0 = torch.randn(co, 3, 3, ci, generator=g)
+    db0 = torch.randn(co, generator=g)
+    xr = x.double().permute(0, 3, 1, 2)
+    dyr = dy.double().permute(0, 3, 1, 2)
+    wr = torch.zeros(co, ci, 3, 3, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xr, wr, padding=1).mul(dyr).sum().backward()
+    exp_dw = beta * dw0.double() + wr.grad.permute(0, 2, 3, 1)
+    exp_db = beta * db0.double() + dyr.sum((0, 2, 3))
+    xd, dyd, dwd, dbd = x.to(dev), dy.to(dev), dw0.to(dev), db0.to(dev)
+    ws = torch.empty(_lib.query("mvae_conv2d_wgrad_direct_workspace_bytes", n, h, w, ci, co), dtype=torch.uint8,
+                     device=dev)
+    _lib.call("mvae_conv2d_wgrad_direct_nhwc", dyd.data_ptr(), xd.data_ptr(), dwd.data_ptr(), dbd.data_ptr(),
+              float(beta), n, h, w, ci, co, 0, ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert rel(dwd, exp_dw) < CONV_TOL
+    assert rel(dbd, exp_db) < 1e-5
 
 
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[2] % 4 == 0 and not (c[5] == 1 and c[6] == 1) and not c[8]])
@@ -346,12 +380,15 @@ def _gn_raw(path, x, gamma, beta, dy, add, groups, silu, drop, seed, y_split=0):
 
 
 # the c3 (28/14/7 at hidden 32) and c2 (hidden 128) levels, whose h*w is not a multiple of 32 (no conv-epilogue
-# statistics): auto selects the register-resident one-pass kernels; checked against float64 torch and against
-# the streaming kernels (dropout masks identical: same counter hash)
+# statistics): auto selects the register-resident one-pass kernels (backward of larger tensors: the two-pass
+# unit kernel); checked against float64 torch and against the streaming kernels (dropout masks identical: same
+# counter hash)
 @pytest.mark.parametrize("n,c,h,silu,drop,add", [(3, 32, 28, True, 0.0, True), (3, 64, 14, True, 0.1, False),
                                                   (2, 128, 7, False, 0.0, True), (2, 256, 14, True, 0.0, False),
                                                   (2, 512, 7, True, 0.1, True), (2, 128, 28, True, 0.0, False),
-                                                  (2, 2048, 4, True, 0.0, True), (5, 96, 9, True, 0.0, False)])
+                                                  (2, 2048, 4, True, 0.0, True), (5, 96, 9, True, 0.0, False),
+                                                  # two-pass unit backward (64x64 / 48x48: too many rows to hold)
+                                                  (2, 256, 64, True, 0.1, True), (2, 512, 48, True, 0.0, False)])
 def test_group_norm_resident_matches_streaming_and_float64(dev, n, c, h, silu, drop, add):
     g = torch.Generator().manual_seed(c * 7 + h)
     G = min(32, c)

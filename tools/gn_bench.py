@@ -10,8 +10,8 @@ REPS = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 SHAPES = [(512, 32, 28, True), (512, 64, 14, True), (512, 128, 7, True), (256, 128, 28, True), (256, 256, 14, False),
           (256, 512, 7, True)]
 if os.environ.get("GN_BENCH_C4"):
-    SHAPES = [(256, 2048, 8, True), (256, 2048, 8, False), (256, 1024, 16, True), (256, 512, 32, True),
-              (256, 256, 64, True)]
+    SHAPES = [(256, 2048, 8, True), (256, 1024, 16, True), (256, 512, 32, True), (256, 256, 64, True),
+              (256, 256, 64, False), (256, 512, 64, False)]
 st = torch.cuda.current_stream().cuda_stream
 tot = {0: [0.0, 0.0], 1: [0.0, 0.0]}
 for n, c, h, add in SHAPES:

@@ -9,6 +9,7 @@ dev = torch.device("cuda:0")
 REPS = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 SHAPES = [  # n, cin, cout, h, k
     (512, 32, 32, 28, 3), (512, 64, 64, 14, 3), (512, 128, 128, 7, 3), (512, 128, 128, 7, 1), (512, 64, 32, 28, 3),
+    (512, 32, 64, 14, 3), (512, 64, 32, 14, 3),
     (256, 128, 128, 28, 3), (256, 256, 256, 14, 3), (256, 512, 512, 7, 3),
     (256, 2048, 2048, 8, 3), (256, 256, 256, 64, 3),
 ]
