@@ -34,6 +34,9 @@ for cfg in ("c4", "c2", "c3", "c5", "c1"):
         agg[key][0] += 1
         agg[key][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
     tot = sum(v[1] for v in agg.values())
+    HELPERS = ("splitk_reduce", "bias_reduce", "w_transpose", "w_ups_dgrad", "split_bf16", "ups_wgrad_combine",
+               "tap_select", "wgrad_direct", "wgrad_small_cout")
+    fam = sum(v[1] for k, v in agg.items() if k.startswith("gemm3x") or any(h in k for h in HELPERS))
     g = agg["gemm3x_kernel (all tile / operand instantiations)"]
     out = [f"rocprofv3 --kernel-trace --stats -- python3 bench.py --config {cfg} --steps {STEPS} --warmup 0 "
            f"--no-cpu-baseline --no-kernel-timing   (round {rnd}, run {tag})",
@@ -41,7 +44,11 @@ for cfg in ("c4", "c2", "c3", "c5", "c1"):
            f"(bench line: {bench['ms_per_step']} ms/step wall)",
            f"gemm3x_kernel: {g[1] / STEPS:.2f} ms/step, {g[0] / STEPS:.1f} launches/step, "
            f"average {g[1] / max(g[0], 1) * 1e3:.1f} us/launch (bench live HIP events: "
-           f"{(bench.get('roofline') or {}).get('avg_launch_us')} us/launch)", "",
+           f"{(bench.get('roofline') or {}).get('avg_launch_us')} us/launch)",
+           # the live HIP-event bracket is the whole conv / attention GEMM op: its helper kernels (split-K and bias
+           # reducers, weight re-layouts / pre-splits, the direct small-channel wgrad kernels) run inside it
+           f"conv/attention op family (gemm3x + helpers inside the live bracket): {fam / STEPS:.2f} ms/step "
+           f"(bench live HIP events: {(bench.get('roofline') or {}).get('gemm_ms_per_step')} ms/step)", "",
            f"{'ms/step':>9} {'calls/step':>10} {'avg us':>9}  kernel"]
     for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:40]:
         out.append(f"{t / STEPS:9.2f} {c / STEPS:10.1f} {t / c * 1e3:9.1f}  {k[:110]}")
