@@ -84,6 +84,10 @@ METRIC_C4 = "training images/sec (whole node) + ELBO parity, multimodal CVAE 64\
 BF16_DENSE_PEAK_TF = 2500.0
 PEAK_3XBF16_TF = BF16_DENSE_PEAK_TF / 3.0
 HBM_PEAK_GBS = 8000.0
+# measured on MI355X (profiles/r02_ceilings.txt): the GEMM main-loop structure without global traffic, per MFMA
+# shape (fp32-equivalent TF/s), and plain HBM streams (read-only / copy)
+STRUCT_CEIL_TF = {"conv_fwd": 598.0, "conv_dgrad": 598.0, "conv_wgrad": 559.0, "attn_gemm": 559.0}
+HBM_MEASURED_GBS = {"read_only": 6262.0, "copy": 5314.0}
 
 
 def _pmc_traffic(config):
@@ -316,6 +320,17 @@ def main():
                     "gemm_share_of_step": round(tot_ms / step_ms, 3),
                     "by_pass": {k: {"launches": v[0], "ms": round(v[2], 2),
                                     "TFLOP/s": round(v[1] / (v[2] * 1e-3) / 1e12, 1)} for k, v in by.items()}}
+        if not bf16:  # measured ceiling of the main-loop structure (no global traffic): profiles/r02_ceilings.txt
+            for k, v in roofline["by_pass"].items():
+                c = STRUCT_CEIL_TF.get(k)
+                if c is None:
+                    continue
+                v["structure_ceiling_TFLOP/s"] = c
+                v["frac_of_structure_ceiling"] = round(v["TFLOP/s"] / c, 3)
+            roofline["structure_ceiling_note"] = (
+                "measured on the box: the kernel's per-wave 3xBF16 LDS-fragment + MFMA loop with one barrier per "
+                "K-tile and no global loads, random operands (tools/micro/mfma_shape.hip): 16x16x32 (fwd / dgrad) "
+                "598 TF/s, 32x32x16 (wgrad / attention) 559 TF/s fp32-equivalent")
         if hbm_rec:  # the memory-bound GroupNorm(+SiLU) family against the HBM roofline
             hb = {}
             for tag, nbytes, s, e, _, _ in hbm_rec:
@@ -329,6 +344,7 @@ def main():
                 "bound": "hbm", "kernel": "GroupNorm(+SiLU) fwd / bwd (gn_* kernel chains, all launches)",
                 "achieved": round(hby / (hms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(hby / (hms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms_per_step": round(hms, 2),
+                "measured_stream_GB/s": HBM_MEASURED_GBS,
                 "bytes_note": "algorithmic bytes: fwd 8 B/elem (read x, write y), bwd 12 B/elem (read x, dy; write dx) "
                               "+ 4 B/elem where the residual branch's gradient is summed in (ResnetBlock / AttnBlock "
                               "norm1); chains include the statistics finalize and parameter-gradient kernels",
