@@ -57,6 +57,14 @@ int mvae_get_math_mode(void);
 int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y,
                      int nb, int h, int w_, int cin, int cout, int kh, int kw, int stride, int pad_t,
                      int pad_l, int ho, int wo, int mode, void* stream);
+/* mvae_conv2d_nhwc with a split-K workspace (same nn.Conv2d forward / input-gradient semantics): a launch whose
+ * output tiles leave most of the chip idle for a partial round (small spatial sizes at wide channels, e.g. the 7x7
+ * level at 512 channels of BetaVAE at 28x28) splits K over `workspace` (fp32 partials, summed in a fixed order
+ * with bias / residual: deterministic). Size it with mvae_conv2d_split_workspace_bytes (0 = never splits). */
+int mvae_conv2d_ws_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y,
+                        int nb, int h, int w_, int cin, int cout, int kh, int kw, int stride, int pad_t,
+                        int pad_l, int ho, int wo, int mode, float* workspace, size_t workspace_bytes, void* stream);
+size_t mvae_conv2d_split_workspace_bytes(int nb, int cin, int cout, int kh, int kw, int ho, int wo);
 /* mvae_conv2d_nhwc that also emits, from the GEMM epilogue, the GroupNorm statistics of y for the
  * Normalize that consumes it (ResnetBlock conv1 -> norm2, block output -> next norm1, ...,
  * encoder_decoder.py:141-170): gn_part = [nb*ho*wo/32][cout/4][2] fp64 {sum y, sum y^2} over 32 pixels

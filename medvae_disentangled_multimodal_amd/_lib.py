@@ -26,6 +26,8 @@ SIGNATURES = {
     "mvae_set_math_mode": (I, [I]),
     "mvae_get_math_mode": (I, []),
     "mvae_conv2d_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P]),
+    "mvae_conv2d_ws_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),
+    "mvae_conv2d_split_workspace_bytes": (Z, [I, I, I, I, I, I, I]),
     "mvae_conv2d_gnstats_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P]),
     "mvae_conv2d_dgrad_gnbwd_nhwc": (I, [P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P, P, I, I, P, P]),
     "mvae_conv2d_wgrad_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),

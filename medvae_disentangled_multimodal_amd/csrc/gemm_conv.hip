@@ -39,13 +39,37 @@ struct GnBwdLink {
 };
 static int conv2d_impl(const float* x, const float* w, const float* bias, const float* residual, float* y, int nb,
                        int h, int wd, int cin, int cout, int kh, int kw, int stride, int pad_t, int pad_l, int ho,
-                       int wo, int mode, double* gn_part, void* stream, const GnBwdLink* gnb = nullptr);
+                       int wo, int mode, double* gn_part, void* stream, const GnBwdLink* gnb = nullptr,
+                       float* ws = nullptr, size_t ws_bytes = 0);
 
 int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const float* residual,
                      float* y, int nb, int h, int wd, int cin, int cout, int kh, int kw,
                      int stride, int pad_t, int pad_l, int ho, int wo, int mode, void* stream) {
   return conv2d_impl(x, w, bias, residual, y, nb, h, wd, cin, cout, kh, kw, stride, pad_t, pad_l, ho, wo, mode,
                      nullptr, stream);
+}
+
+// mvae_conv2d_nhwc with a split-K workspace: a launch whose tiles leave most of the 256 CUs idle for a partial
+// round (small spatial sizes at wide channels) may split K over `workspace` (fp32 partials, reduced in a fixed
+// order with bias / residual). Size from mvae_conv2d_split_workspace_bytes; a smaller workspace means fewer splits.
+int mvae_conv2d_ws_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y, int nb,
+                        int h, int wd, int cin, int cout, int kh, int kw, int stride, int pad_t, int pad_l, int ho,
+                        int wo, int mode, float* workspace, size_t workspace_bytes, void* stream) {
+  return conv2d_impl(x, w, bias, residual, y, nb, h, wd, cin, cout, kh, kw, stride, pad_t, pad_l, ho, wo, mode,
+                     nullptr, stream, nullptr, workspace, workspace_bytes);
+}
+
+// Workspace bytes mvae_conv2d_ws_nhwc would use for this geometry (0: the launch stays unsplit).
+size_t mvae_conv2d_split_workspace_bytes(int nb, int cin, int cout, int kh, int kw, int ho, int wo) {
+  if (nb <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || ho <= 0 || wo <= 0 || cin % 4) return 0;
+  GemmArgs a{};
+  a.M = nb * ho * wo; a.N = cout; a.K = kh * kw * cin; a.batch = 1; a.splits = 1; a.k_split = a.K;
+  const int cfg = choose_tile(a, true, false);
+  int s = 1;
+  const int c2 = conv_split_cfg(a, cfg, (size_t)1 << 40, &s);
+  if (c2 < 0) return 0;
+  set_splits(a, s);
+  return splitk_ws_bytes(a);
 }
 
 // mvae_conv2d_nhwc that also emits the GroupNorm statistics of y for the Normalize that follows
@@ -93,7 +117,8 @@ int mvae_conv2d_dgrad_gnbwd_nhwc(const float* dy, const float* wt, float* dx, in
 
 static int conv2d_impl(const float* x, const float* w, const float* bias, const float* residual, float* y, int nb,
                        int h, int wd, int cin, int cout, int kh, int kw, int stride, int pad_t, int pad_l, int ho,
-                       int wo, int mode, double* gn_part, void* stream, const GnBwdLink* gnb) {
+                       int wo, int mode, double* gn_part, void* stream, const GnBwdLink* gnb, float* ws,
+                       size_t ws_bytes) {
   const bool presplit = (mode & MVAE_CONV_WSPLIT) != 0;
   const bool xsplit = (mode & MVAE_CONV_XSPLIT) != 0;
   mode &= ~(MVAE_CONV_WSPLIT | MVAE_CONV_XSPLIT);
@@ -148,7 +173,16 @@ static int conv2d_impl(const float* x, const float* w, const float* bias, const 
       a.gnb_gamma = gnb->gamma; a.gnb_beta = gnb->beta;
       a.gnb_hw = hw; a.gnb_G = gnb->groups; a.gnb_cpg = cout / gnb->groups; a.gnb_silu = gnb->silu;
     }
-    const int cfg = choose_tile(a, v, false);
+    int cfg = choose_tile(a, v, false);
+    if (ws != nullptr && gn_part == nullptr && gnb == nullptr && v) {  // under-filled launch: split K (conv_split_cfg)
+      int s = 1;
+      const int c2 = conv_split_cfg(a, cfg, ws_bytes, &s);
+      if (c2 >= 0) {
+        cfg = c2;
+        set_splits(a, s);
+        a.ws = ws;
+      }
+    }
     if ((gn_part || gnb) && !v) {
       set_error("conv2d_gnstats: needs the vector (16-B) operand path");
       return MVAE_EINVAL;

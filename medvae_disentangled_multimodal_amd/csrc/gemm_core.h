@@ -1382,6 +1382,47 @@ inline int choose_splits(const GemmArgs& a, int cfg) {
   return best;
 }
 
+// Split-K for an under-filled implicit-GEMM conv (fwd / dgrad of the small-spatial layers: c2's 7x7 level at 512
+// channels is 98-196 tiles of any shape for 256 CUs, i.e. one partial round): the unsplit tile the cost model chose
+// (cfg0) against 256-wide tiles over K split s ways plus the fixed-order reducer, by a time model -- GEMM: rounds x
+// tiles resident per CU x tile area x K / s / (per-tile efficiency x MAC rate per CU); reducer: (s + 2) x M x N x 4 B
+// at HBM speed + one launch. Returns the tile config with *splits set, or -1 to stay unsplit. Splits keep >= 16
+// K-tiles each and must fit ws_bytes.
+inline int conv_split_cfg(const GemmArgs& a, int cfg0, size_t ws_bytes, int* splits_out) {
+  static const double eff[5] = {1.0, 0.82, 0.82, 0.70, 0.50};
+  static const int res[5] = {1, 1, 1, 2, 4};
+  static const int area[5] = {65536, 32768, 32768, 16384, 4096};
+  if (cfg0 < T256x256 || cfg0 > T64x64 || ws_bytes == 0 || a.batch != 1) return -1;
+  const double mac_rate = 0.9e12;  // MAC/s per CU at 256x256 (efficiency 1.0): ~470 TF/s chip-wide, 3xBF16
+  auto gemm_s = [&](int c, long long blocks, double k) {
+    const long long slots = 256LL * res[c];
+    const double rounds = (double)((blocks + slots - 1) / slots);
+    return rounds * res[c] * area[c] * k / eff[c] / mac_rate;
+  };
+  const double t0 = gemm_s(cfg0, tiles_of(cfg0, a), (double)a.K);
+  const double mn4 = 4.0 * (double)a.M * (double)a.N;
+  int best = -1, best_s = 1;
+  double best_t = t0 * 0.92;  // demand a clear gain: the model ignores prologue / epilogue per split
+  for (int c = T256x256; c <= T128x256; ++c) {
+    if ((c == T256x256 && (a.M <= 128 || a.N <= 128)) || (c == T256x128 && a.M <= 128) || (c == T128x256 && a.N <= 128))
+      continue;
+    const long long tiles = tiles_of(c, a);
+    for (int s = 2; s <= 32 && (long long)a.K / s >= 16 * BK; ++s) {
+      GemmArgs b = a;
+      set_splits(b, s);
+      if (b.splits < 2 || splitk_ws_bytes(b) > ws_bytes) continue;
+      const double t = gemm_s(c, tiles * b.splits, (double)b.k_split) + (b.splits + 2.0) * mn4 / 5.0e12 + 4.0e-6;
+      if (t < best_t) {
+        best_t = t;
+        best = c;
+        best_s = b.splits;
+      }
+    }
+  }
+  *splits_out = best_s;
+  return best;
+}
+
 inline void plan_splits(GemmArgs& a, int cfg, float* ws, size_t ws_bytes) {
   set_splits(a, ws ? choose_splits(a, cfg) : 1);
   while (a.splits > 1 && splitk_ws_bytes(a) > ws_bytes) set_splits(a, a.splits / 2);

@@ -223,6 +223,29 @@ class math_scope:
         return False
 
 
+# Split-K for under-filled conv launches (mvae_conv2d_ws_nhwc: the small-spatial, wide-channel layers of the 28x28
+# models leave most CUs idle for a partial round); MVAE_NO_CONV_SPLITK=1 keeps every fwd / dgrad launch unsplit.
+CONV_SPLITK = os.environ.get("MVAE_NO_CONV_SPLITK") is None
+_CONV_WS_CACHE = {}
+
+
+def _conv_call(x, w, b, res, y, n, h, wd, c, co, kh, kw, stride, pad_t, pad_l, ho, wo, mode, st):
+    """mvae_conv2d_nhwc, or its split-K form when the library's planner splits this geometry."""
+    nbytes = 0
+    if CONV_SPLITK:
+        key = (n, c, co, kh, kw, ho, wo)
+        nbytes = _CONV_WS_CACHE.get(key)
+        if nbytes is None:
+            nbytes = _CONV_WS_CACHE[key] = int(_lib.query("mvae_conv2d_split_workspace_bytes", n, c, co, kh, kw, ho, wo))
+    if nbytes:
+        ws = ARENA.get("convsplit", nbytes, y.device)
+        _lib.call("mvae_conv2d_ws_nhwc", x, w, b, res, y.data_ptr(), n, h, wd, c, co, kh, kw, stride, pad_t, pad_l, ho,
+                  wo, mode, ws.data_ptr(), ws.numel(), st)
+    else:
+        _lib.call("mvae_conv2d_nhwc", x, w, b, res, y.data_ptr(), n, h, wd, c, co, kh, kw, stride, pad_t, pad_l, ho, wo,
+                  mode, st)
+
+
 def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part=None):
     """gn_part (fp64 [n*ho*wo/32 * cout/4 * 2]): also emit the GroupNorm statistics of y from the GEMM
     epilogue (mvae_conv2d_gnstats_nhwc; only on the plain implicit-GEMM path -- the caller checks)."""
@@ -258,8 +281,8 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
                 _lib.call("mvae_conv2d_gnstats_nhwc", x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(),
                           n, h, wd, c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, mode, gn_part.data_ptr(), st)
             else:
-                _lib.call("mvae_conv2d_nhwc", x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n, h, wd,
-                          c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, mode, st)
+                _conv_call(x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y, n, h, wd, c, co, g.kh, g.kw, g.stride,
+                           g.pad_t, g.pad_l, ho, wo, mode, st)
     return y
 
 
@@ -330,8 +353,8 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None):
                       g.kh, g.kw, g.pad_t, g.pad_l, ho, wo, flags, wc.data_ptr(), wc.numel(), st)
         return dx
     with _timed("conv_dgrad", flops, shp):
-        _lib.call("mvae_conv2d_nhwc", dya.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
-                  g.kh, g.kw, g.stride, g.pad_t, g.pad_l, h, wd, 2 | wflag | xflag, st)
+        _conv_call(dya.data_ptr(), wt.data_ptr(), None, None, dx, n, ho, wo, co, c, g.kh, g.kw, g.stride, g.pad_t,
+                   g.pad_l, h, wd, 2 | wflag | xflag, st)
     return dx
 
 

@@ -70,6 +70,10 @@ CONV_CASES = [
     (2, 64, 32, 14, 14, 3, 1, (1, 1, 1, 1), False),
     (2, 32, 32, 9, 11, 3, 1, (1, 1, 1, 1), False),
     (600, 32, 32, 7, 5, 3, 1, (1, 1, 1, 1), False),
+    # under-filled launches that the planner splits over K (mvae_conv2d_ws_nhwc): c2's 7x7 level at 512 channels,
+    # a 2048 -> 512 narrowing conv; both fwd and dgrad split
+    (64, 512, 512, 7, 7, 3, 1, (1, 1, 1, 1), False),
+    (8, 1024, 256, 8, 8, 3, 1, (1, 1, 1, 1), False),
 ]
 
 
@@ -119,6 +123,33 @@ def test_conv_fwd_dgrad_wgrad(dev, case):
     assert wm.grad is None and bm.grad is None
     assert rel(wm._mvae_main_grad - 0.5, wr.grad) < CONV_TOL
     assert float((bm._mvae_main_grad.cpu().double() - 0.25 - db_ref).abs().max()) < 1e-5 * scale
+
+
+@pytest.mark.parametrize("n,ci,co,h", [(64, 512, 512, 7), (8, 1024, 256, 8), (32, 256, 512, 7)])
+def test_conv_splitk_matches_unsplit(dev, n, ci, co, h, monkeypatch):
+    """The split-K form of an under-filled conv (fwd and input gradient) is taken and agrees with the unsplit launch
+    and with float64 torch."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    assert _lib.query("mvae_conv2d_split_workspace_bytes", n, ci, co, 3, 3, h, h) > 0
+    assert _lib.query("mvae_conv2d_split_workspace_bytes", n, co, ci, 3, 3, h, h) > 0
+    g = torch.Generator().manual_seed(n + ci + co)
+    x = torch.randn(n, ci, h, h, generator=g)
+    wt = torch.randn(co, ci, 3, 3, generator=g) / math.sqrt(ci * 9)
+    b = torch.randn(co, generator=g) * 0.1
+    res = torch.randn(n, co, h, h, generator=g)
+    dy = torch.randn(n, co, h, h, generator=g)
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
+    y64 = F.conv2d(x.double(), wt.double(), b.double(), padding=1) + res.double()
+    dx64 = torch.nn.grad.conv2d_input(x.shape, wt.double(), dy.double(), padding=1)
+    outs = {}
+    for on in (True, False):
+        monkeypatch.setattr(ops, "CONV_SPLITK", on)
+        y = ops.conv2d_forward_raw(cl(x, dev), cl(wt, dev), b.to(dev), cl(res, dev), geom)
+        dx = ops.conv2d_dgrad_raw(cl(dy, dev), cl(wt, dev), x.shape, geom)
+        torch.cuda.synchronize()
+        assert rel(y, y64) < CONV_TOL and rel(dx, dx64) < CONV_TOL
+        outs[on] = (y.cpu(), dx.cpu())
+    assert rel(outs[True][0], outs[False][0]) < 1e-4 and rel(outs[True][1], outs[False][1]) < 1e-4
 
 
 @pytest.mark.parametrize("ci,co,h,w,beta", [(32, 32, 28, 28, 0.0), (64, 32, 14, 14, 1.0), (32, 64, 14, 14, 0.5),
@@ -553,11 +584,13 @@ def test_block_input_gradient_branches_summed_in_groupnorm(dev, cin, cout, attn)
 
 
 @pytest.mark.parametrize("n,c,co,h,res", [(4, 64, 128, 16, False), (8, 128, 256, 8, True), (16, 256, 256, 32, True)])
-def test_conv_epilogue_groupnorm_statistics(dev, n, c, co, h, res):
+def test_conv_epilogue_groupnorm_statistics(dev, n, c, co, h, res, monkeypatch):
     """conv2d(gn_stats=True) emits {sum, sum sq} per 32 pixels x 4 channels from the GEMM epilogue and the
     following GroupNorm(+SiLU) finalizes from them (no statistics pass): same output as the two-pass
-    GroupNorm of the same conv output; an in-place change of the conv output drops the statistics."""
+    GroupNorm of the same conv output; an in-place change of the conv output drops the statistics.
+    (The statistics launch is never split over K; the plain launch is held unsplit too, for bitwise equality.)"""
     from medvae_disentangled_multimodal_amd import ops
+    monkeypatch.setattr(ops, "CONV_SPLITK", False)
     g = torch.Generator().manual_seed(7)
     x = cl(torch.randn(n, c, h, h, generator=g), dev)
     w = cl(torch.randn(co, c, 3, 3, generator=g) / math.sqrt(9 * c), dev)
