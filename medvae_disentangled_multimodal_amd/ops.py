@@ -882,31 +882,32 @@ class ReconFn(torch.autograd.Function):
 
 
 class _FiniteGateFn(torch.autograd.Function):
-    """v = fn(*inputs); backward recomputes fn under autograd and hands back its input gradients only if v
-    was finite (device-side flag, no host sync). This is the reference's `if isnan(v) or isinf(v): v =
-    tensor(0.)` (disentangled_conditional_vae.py:528-550): a non-finite term is cut out of the graph, so
-    its backward can never inject 0*inf = NaN into the shared encoder gradients."""
+    """v = fn(*inputs); the input gradients are handed back only if v was finite (device-side flag, no host
+    sync). This is the reference's `if isnan(v) or isinf(v): v = tensor(0.)` (disentangled_conditional_vae.py:
+    528-550): a non-finite term is cut out of the graph, so its backward can never inject 0*inf = NaN into the
+    shared encoder gradients. fn runs once, under autograd on detached inputs; its small sub-graph (the [B, 8]
+    latent statistics of the separation / contrastive terms) is kept for the backward instead of recomputed."""
 
     @staticmethod
     def forward(ctx, fn, *inputs):
-        v = fn(*inputs)
-        ctx.fn = fn
-        ctx.ok = torch.isfinite(v).all()
-        ctx.save_for_backward(*inputs)
-        return v
+        need = ctx.needs_input_grad[1:]
+        with torch.enable_grad():
+            req = [t.detach().requires_grad_(bool(n)) if torch.is_tensor(t) else t for t, n in zip(inputs, need)]
+            v = fn(*req)
+        ctx.v, ctx.req = v, req
+        ctx.ok = torch.isfinite(v.detach()).all()
+        return v.detach()
 
     @staticmethod
     def backward(ctx, g):
-        ins = ctx.saved_tensors
-        need = ctx.needs_input_grad[1:]
-        with torch.enable_grad():
-            req = [t.detach().requires_grad_(bool(n)) for t, n in zip(ins, need)]
-            v = ctx.fn(*req)
-            want = [r for r in req if r.requires_grad]
-            got = list(torch.autograd.grad(v, want, g, allow_unused=True)) if want else []
+        req, v = ctx.req, ctx.v
+        ctx.v = ctx.req = None
+        want = [r for r in req if torch.is_tensor(r) and r.requires_grad]
+        got = list(torch.autograd.grad(v, want, g, allow_unused=True)) if want and v.requires_grad else \
+            [None] * len(want)
         out = []
         for r in req:
-            gr = got.pop(0) if r.requires_grad else None
+            gr = got.pop(0) if torch.is_tensor(r) and r.requires_grad else None
             if gr is not None:
                 gr = torch.where(ctx.ok, gr, torch.zeros((), device=gr.device, dtype=gr.dtype))
             out.append(gr)
