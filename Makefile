@@ -8,7 +8,14 @@ SRC := $(wildcard $(PKG)/csrc/*.hip) $(PKG)/csrc/errors.cpp
 OBJ := $(patsubst $(PKG)/csrc/%,build/%.o,$(SRC))
 CXXFLAGS := -O3 -std=c++17 -fPIC -fno-slp-vectorize --offload-arch=$(ARCH) -Wall -Wno-unused-function -Wno-unused-variable
 
-all: $(PKG)/libmvae_hip.so
+PYINC := $(shell python3 -c "import sysconfig; print(sysconfig.get_paths()['include'])")
+PYEXT := $(shell python3 -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
+
+all: $(PKG)/libmvae_hip.so $(PKG)/_mvae_fast$(PYEXT)
+
+# host-side call path (Python -> C ABI) without ctypes argument conversion: csrc/pyfast.c
+$(PKG)/_mvae_fast$(PYEXT): $(PKG)/csrc/pyfast.c
+	gcc -O2 -shared -fPIC -Wall -I$(PYINC) $< -o $@
 
 build/%.o: $(PKG)/csrc/% $(PKG)/csrc/common.h $(PKG)/csrc/gemm_core.h
 	@mkdir -p build
@@ -18,6 +25,6 @@ $(PKG)/libmvae_hip.so: $(OBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(OBJ) -o $@
 
 clean:
-	rm -rf build $(PKG)/libmvae_hip.so
+	rm -rf build $(PKG)/libmvae_hip.so $(PKG)/_mvae_fast*.so
 
 .PHONY: all clean

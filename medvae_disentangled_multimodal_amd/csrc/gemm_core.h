@@ -806,81 +806,6 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
     }
   };
   int t = 0;
-#ifdef MVAE_PINGPONG
-  if constexpr (NT == 512) {
-    // Ping-pong (8 waves = 2 per SIMD; waves w and w+4 share a SIMD): the two halves of the workgroup run the
-    // same K-tile one barrier interval apart, so in every interval one wave of each SIMD issues a dense block of
-    // MFMAs from registers while its partner does the memory work -- fragment reads for its own next block, its
-    // share of tile t+1's staging (split + LDS write) and the global loads of tile t+2. A K-tile is NPH phases of
-    // [load section | barrier | MFMA section | barrier]; waves 4-7 enter one barrier late and waves 0-3 leave one
-    // barrier late, so every wave executes the same number of barriers.
-    // LDS order (2 buffers): tile t+1 is written during the load sections of tile t (both halves), all of which
-    // end before the barrier that precedes the first read of tile t+1 (waves 0-3's first load section of t+1);
-    // its buffer held tile t-1, whose last read (waves 4-7's last load section of t-1) ended at the barrier
-    // before waves 0-3's first load section of t. Fragments are read only in load sections, so each MFMA
-    // section runs without an LDS wait.
-    constexpr int STEPS = KS * TM;
-    constexpr int NPH = (PREC == 1 || STEPS < 8) ? 2 : 4;  // phases per K-tile
-    constexpr int SPP = STEPS / NPH;                       // MFMA steps (one A fragment x TN) per phase
-    constexpr int NSL = LA::NS + LB::NS;
-    static_assert(STEPS % NPH == 0, "ping-pong phases must split the K-tile's MFMA steps evenly");
-    const bool late = wid >= (NT / 64) / 2;
-    bf16x8 bh[TN], bl[TN], ah[SPP], al[SPP];
-    if (late) __syncthreads();
-    for (; t + 2 < nt; ++t) {
-      __bf16* nb = lds + ((t & 1) ^ 1) * BUF;
-      const __bf16* Ai = lds + (t & 1) * BUF;
-      const __bf16* Bi = Ai + IA::SIZE;
-#pragma unroll
-      for (int p = 0; p < NPH; ++p) {
-        // ---- load section: fragments of this phase's steps, then this phase's share of the staging
-#pragma unroll
-        for (int s = 0; s < SPP; ++s) {
-          const int st = p * SPP + s, ks = st / TM, i = st % TM;
-          if (i == 0) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              bh[j] = read_frag<BN, LB::COL, MF>(Bi, brow + j * MF, ks, lane);
-              if constexpr (PREC != 1) bl[j] = read_frag<BN, LB::COL, MF>(Bi + IB::PLANE, brow + j * MF, ks, lane);
-            }
-          }
-          ah[s] = read_frag<BM, LA::COL, MF>(Ai, arow + i * MF, ks, lane);
-          if constexpr (PREC != 1) al[s] = read_frag<BM, LA::COL, MF>(Ai + IA::PLANE, arow + i * MF, ks, lane);
-        }
-        if (p == 0) {
-          la.advance();
-          lb.advance();
-          la.prep(a);
-          lb.prep(a);
-        }
-#pragma unroll
-        for (int q = p * NSL / NPH; q < (p + 1) * NSL / NPH; ++q) {
-          if (q < LA::NS) {
-            la.store_slot(nb, q);
-            la.load_slot(a, q);
-          } else {
-            lb.store_slot(nb + IA::SIZE, q - LA::NS);
-            lb.load_slot(a, q - LA::NS);
-          }
-        }
-        __syncthreads();
-        __builtin_amdgcn_sched_barrier(0);
-        // ---- MFMA section
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int s = 0; s < SPP; ++s) {
-          const int i = (p * SPP + s) % TM;
-#pragma unroll
-          for (int j = 0; j < TN; ++j) mma<PREC>(acc[i][j], ah[s], al[s], bh[j], bl[j]);
-        }
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-        __syncthreads();
-      }
-    }
-    if (!late) __syncthreads();
-  } else
-#endif
   {
 #ifndef MVAE_BLOCK_STAGING
   // steady state, software-pipelined by hand: the K-tile's KS*TM MFMA steps (one MF-row A fragment

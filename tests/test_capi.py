@@ -68,3 +68,21 @@ def test_missing_library_fails_loudly(monkeypatch):
     monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libmvae_hip.so")
     with pytest.raises(_lib.HipLibraryError):
         _lib.load()
+
+
+def test_fastcall_path_matches_ctypes_without_gpu():
+    """The low-overhead call path (csrc/pyfast.c) binds every int / size_t entry point of the same library and
+    returns what ctypes returns; argument errors come back through the library's status + message."""
+    lib = _lib.load()
+    if _lib._fast_mod is None:
+        pytest.skip("_mvae_fast not built (make builds it next to libmvae_hip.so)")
+    assert set(_lib.SIGNATURES) - set(_lib._FAST) == {"mvae_last_error"}
+    for args in [(64, 512, 512, 3, 3, 7, 7), (8, 1024, 256, 3, 3, 8, 8), (256, 2048, 2048, 3, 3, 8, 8)]:
+        assert _lib.query("mvae_conv2d_split_workspace_bytes", *args) == lib.mvae_conv2d_split_workspace_bytes(*args)
+    assert _lib.query("mvae_gemm_workspace_bytes", 64, 64, 100000, 1) == lib.mvae_gemm_workspace_bytes(64, 64, 100000, 1)
+    assert _lib.query("mvae_group_norm_workspace_bytes", 2, 64, 32) == lib.mvae_group_norm_workspace_bytes(2, 64, 32)
+    assert _lib.query("mvae_abi_version") == 1
+    with pytest.raises(RuntimeError, match="softmax"):
+        _lib.call("mvae_softmax_rows", None, None, 0, 0, None)
+    with pytest.raises(RuntimeError, match="bad geometry"):  # float + pointer + int mix through the trampoline
+        _lib.call("mvae_conv2d_nhwc", 0, 0, None, None, 0, -1, 8, 8, 4, 4, 3, 3, 1, 1, 1, 8, 8, 0, None)
