@@ -41,6 +41,9 @@ static PyObject* fast_bind(PyObject* self, PyObject* args) {
   unsigned long long addr;
   const char* sig;
   if (!PyArg_ParseTuple(args, "Ks", &addr, &sig)) return NULL;
+#if !(defined(__x86_64__) && defined(__linux__))
+  Py_RETURN_NONE; /* the trampoline assumes the x86-64 SysV argument placement: other hosts stay on ctypes */
+#endif
   const int n = (int)strlen(sig) - 1;
   if (n < 0 || n > MAX_ARGS || g_nfn >= MAX_FN || (sig[0] != 'I' && sig[0] != 'Z')) Py_RETURN_NONE;
   int ni = 0, nf = 0;
