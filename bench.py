@@ -57,13 +57,13 @@ CONFIGS = {
                          discriminator_iter_start=10000, allow_synthetic_lpips=True, lpips_net="vgg")),
     # BASELINE config 1: chest_base_vae at 28x28x1 with the 3-level ch_mult (SURVEY top note 3), bs 32, AdamW 2e-4
     # wd 1e-4, clip 1.0 (the reference runs it on the CPU; here it is the same step on the GPU path)
-    "c1": dict(cls="BaseVAE", res=28, batch=32, cpu_batch=32,
+    "c1": dict(cls="BaseVAE", res=28, batch=32, cpu_batch=32, graph=True,
                kwargs=dict(input_channels=1, latent_dim=256, hidden_channels=128, ch_mult=(1, 2, 4),
                            num_res_blocks=2, attn_resolutions=[16], dropout=0.0, resolution=28),
                opt=dict(type="adamw", lr=2e-4, weight_decay=1e-4, betas=[0.9, 0.999]), clip=1.0,
                loss=dict(type="vae", recon_loss_type="mse", kl_weight=1.0, recon_weight=1.0)),
     # BASELINE config 2: path_beta_vae at 28x28x3 with the 3-level ch_mult, bs 256
-    "c2": dict(cls="BetaVAE", res=28, batch=256, cpu_batch=16,
+    "c2": dict(cls="BetaVAE", res=28, batch=256, cpu_batch=16, graph=True,
                kwargs=dict(input_channels=3, latent_dim=128, hidden_channels=128, ch_mult=(1, 2, 4),
                            num_res_blocks=2, attn_resolutions=[16], dropout=0.0, resolution=28, beta=6.0),
                opt=dict(type="adamw", lr=1e-4, weight_decay=1e-4, betas=[0.9, 0.999]), clip=1.0,
@@ -71,7 +71,7 @@ CONFIGS = {
     # BASELINE config 3: disentangled_multi_modal_cvae_quick (configs/model/disentangled_conditional_vae_quick.yaml,
     # configs/experiment/disentangled_multi_modal_cvae_quick.yaml: Adam lr 5e-4, clip 0.5, dropout 0.1), bs 512,
     # a mixed batch of the 5 modalities (1-channel images zero-padded to 3 by the collate)
-    "c3": dict(cls="DisentangledConditionalVAE", res=28, batch=512, cpu_batch=512,
+    "c3": dict(cls="DisentangledConditionalVAE", res=28, batch=512, cpu_batch=512, graph=True,
                kwargs=dict(num_modalities=5, shared_latent_dim=8, modality_latent_dim=8, hidden_channels=32,
                            ch_mult=(1, 2, 4), num_res_blocks=1, attn_resolutions=[], dropout=0.1, resolution=28,
                            modality_separation_weight=0.1, contrastive_weight=0.05),
@@ -216,6 +216,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--detail", action="store_true", help="per-shape GEMM launch timings on stderr")
+    ap.add_argument("--eager", action="store_true", help="launch every kernel from Python (no HIP-graph replay)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -249,15 +250,21 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     batches = [make_batch(cfg, dev, gen) for _ in range(2)]
 
+    # the small configs (c1-c3: ~800 launches of a few microseconds per step) replay the whole step as one captured
+    # HIP graph -- same kernels and arithmetic, the host issues one launch per step; eager for c4 / c5 and N > 1
+    graphed = cfg.get("graph", False) and world == 1 and not args.eager
+    step = mod.fit_step_graphed if graphed else mod.fit_step
     for i in range(args.warmup):
         mod.fit_step(batches[i % 2], i)
+    if graphed:  # capture (recorded, not executed) + one replay, untimed
+        step(batches[args.warmup % 2], args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss = mod.fit_step(batches[i % 2], i)
+        loss = step(batches[i % 2], i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -368,7 +375,8 @@ def main():
                                       f"train step (fwd+loss+bwd+clip+AdamW)", "model": cfg["cls"],
                           "params": nparams, "global_batch": cfg["batch"] * world, "per_gpu_batch": cfg["batch"],
                           "resolution": cfg["res"], "parallelism": f"dp{world}", "rccl_world_size": world,
-                          "backend": dist.get_backend() if world > 1 else None},
+                          "backend": dist.get_backend() if world > 1 else None,
+                          "step_launch": "hip graph (captured step)" if graphed else "eager"},
                "loss": round(loss_v, 6), "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     if world > 1:

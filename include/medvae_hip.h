@@ -37,6 +37,10 @@ int mvae_abi_version(void);
  *     autocast runs these convolutions/bmm in bf16; main.py trainer precision flag). */
 int mvae_set_math_mode(int mode);
 int mvae_get_math_mode(void);
+/* Dropout salt (device pointer to one uint64, or NULL): mixed into the seed of every following GroupNorm dropout
+ * mask (ResnetBlock nn.Dropout, encoder_decoder.py:163). Lets a captured HIP graph of a training step draw fresh
+ * masks per replay: the graph advances the salt on the device; the frozen per-launch seeds stay valid. */
+int mvae_set_dropout_salt(const void* salt_dev);
 
 /* ---- convolutions (implicit GEMM on MFMA, 3xBF16 split arithmetic, fp32 accumulate) ------------
  * Replaces nn.Conv2d forward in ResnetBlock/AttnBlock/Encoder/Decoder

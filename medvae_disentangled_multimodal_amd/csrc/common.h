@@ -17,6 +17,8 @@ namespace mvae {
 // an argument error and the positive hipError_t value for a launch error.
 enum { MVAE_OK = 0, MVAE_EINVAL = -1, MVAE_EWORKSPACE = -2 };
 void set_error(const char* fmt, ...);
+// device pointer of the process-wide dropout salt (mvae_set_dropout_salt), or nullptr
+const unsigned long long* dropout_salt();
 
 inline int launch_status() {
   hipError_t e = hipGetLastError();

@@ -13,6 +13,8 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 static std::atomic<int> g_math{0};
+static std::atomic<const unsigned long long*> g_salt{nullptr};
+const unsigned long long* dropout_salt() { return g_salt.load(std::memory_order_relaxed); }
 int math_mode() { return g_math.load(std::memory_order_relaxed); }
 }  // namespace mvae
 
@@ -30,3 +32,12 @@ extern "C" int mvae_set_math_mode(int mode) {
   return 0;
 }
 extern "C" int mvae_get_math_mode(void) { return mvae::g_math.load(std::memory_order_relaxed); }
+
+// Dropout salt: a uint64 in device memory mixed into every dropout seed of the following GroupNorm(+Dropout)
+// launches (their masks are hashes of seed and element index). A captured HIP graph freezes the per-launch
+// seeds; advancing the salt on the device once per replay gives each replayed step fresh, reproducible masks.
+// nullptr (the default) = plain seeds, as before.
+extern "C" int mvae_set_dropout_salt(const void* salt_dev) {
+  mvae::g_salt.store((const unsigned long long*)salt_dev, std::memory_order_relaxed);
+  return 0;
+}

@@ -55,7 +55,13 @@ struct GnArgs {
   double* ws;  // [nb][chunks][C][2]
   int y_split;  // forward apply: write y as split4_bf16 groups (the 3xBF16 GEMM operand format)
   const float* dx_add;  // backward: optional gradient of the same tensor from another branch, summed into dx
+  // process-wide dropout salt in device memory (mvae_set_dropout_salt): mixed into the seed, so a replayed HIP
+  // graph -- whose kernel arguments, seeds included, are frozen -- still draws a fresh mask once the salt advances
+  const unsigned long long* salt;
 };
+__device__ __forceinline__ unsigned long long drop_seed(const GnArgs& a) {
+  return a.salt ? a.seed ^ (*a.salt * 0xD1B54A32D192ED03ull) : a.seed;
+}
 
 // Thread mapping shared by the NHWC GroupNorm kernels: a block owns (sample b, chunk of rows); a
 // thread owns one 4-channel column group c4 and walks rows row_lo + rph, + rpar, ... (rpar rows in
@@ -126,7 +132,7 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(GnArgs a) {
             for (int e = 0; e < 4; ++e) {
               float d = ds[e];
               if (a.drop_p > 0.f) {
-                const float uu = hash_uniform(a.seed, (unsigned long long)(off + e));
+                const float uu = hash_uniform(drop_seed(a), (unsigned long long)(off + e));
                 d = (uu >= a.drop_p) ? d / (1.f - a.drop_p) : 0.f;
               }
               const float xh = (xs[e] - m[e]) * rs[e];
@@ -270,7 +276,7 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(GnArgs a, const float* __
           for (int k = 0; k < 4; ++k) {
             if (a.silu) o[k] = o[k] * sigmoid_f(o[k]);
             if (a.drop_p > 0.f) {
-              const float uu = hash_uniform(a.seed, (unsigned long long)(off + k));
+              const float uu = hash_uniform(drop_seed(a), (unsigned long long)(off + k));
               o[k] = (uu >= a.drop_p) ? o[k] / (1.f - a.drop_p) : 0.f;
             }
           }
@@ -400,7 +406,7 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
           for (int e = 0; e < 4; ++e) {
             float d = ds[e];
             if (a.drop_p > 0.f) {
-              const float uu = hash_uniform(a.seed, (unsigned long long)(off + e));
+              const float uu = hash_uniform(drop_seed(a), (unsigned long long)(off + e));
               d = (uu >= a.drop_p) ? d / (1.f - a.drop_p) : 0.f;
             }
             if (a.silu) {
@@ -581,7 +587,7 @@ __device__ __forceinline__ void gn_fwd_unit(const GnArgs& a, int SC, int u, cons
       if (a.silu) o[k] = o[k] * sigmoid_f(o[k]);
       if (a.drop_p > 0.f) {
         const long long off = un.ubase + (long long)(rph + i * rpar) * a.C + c4 * 4;
-        const float uu = hash_uniform(a.seed, (unsigned long long)(off + k));
+        const float uu = hash_uniform(drop_seed(a), (unsigned long long)(off + k));
         o[k] = (uu >= a.drop_p) ? o[k] / (1.f - a.drop_p) : 0.f;
       }
     }
@@ -649,7 +655,7 @@ __device__ __forceinline__ void gn_bwd_unit(const GnArgs& a, int SC, int u, cons
     for (int e = 0; e < 4; ++e) {
       float d = ds[e];  // rows past hw hold d = 0: they add nothing
       if (a.drop_p > 0.f) {
-        const float uu = hash_uniform(a.seed, (unsigned long long)(off + e));
+        const float uu = hash_uniform(drop_seed(a), (unsigned long long)(off + e));
         d = (uu >= a.drop_p) ? d / (1.f - a.drop_p) : 0.f;
       }
       const float xh = (xs[e] - m[e]) * rs[e];
@@ -764,7 +770,7 @@ __global__ void __launch_bounds__(GN_RES_NT) gn_bwd_unit2_kernel(GnArgs a, int S
       for (int e = 0; e < 4; ++e) {
         float g = ds[e];
         if (a.drop_p > 0.f) {
-          const float uu = hash_uniform(a.seed, (unsigned long long)(off + e));
+          const float uu = hash_uniform(drop_seed(a), (unsigned long long)(off + e));
           g = (uu >= a.drop_p) ? g / (1.f - a.drop_p) : 0.f;
         }
         xh[e] = (xs[e] - m[e]) * rs[e];
@@ -1006,7 +1012,7 @@ int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* be
     return e ? atoi(e) : 16;
   }();
   if (const int sc = gn_resident_slab(nb, hw, c, groups, &it, fwd_max_it)) {
-    a.silu = silu; a.drop_p = drop_p; a.seed = seed; a.y_split = y_split;
+    a.silu = silu; a.drop_p = drop_p; a.seed = seed; a.y_split = y_split; a.salt = dropout_salt();
     const int units = nb * (c / sc);
     const void* k = it == 4 ? (const void*)gn_fwd_resident_kernel<4>
                   : it == 8 ? (const void*)gn_fwd_resident_kernel<8> : (const void*)gn_fwd_resident_kernel<16>;
@@ -1021,7 +1027,7 @@ int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* be
   hipLaunchKernelGGL(gn_partial_kernel<0>, dim3(a.chunks, nb), dim3(256), 0, st, a);
   hipLaunchKernelGGL(gn_stats_finalize_kernel, dim3(cdiv((long long)nb * groups, 4)), dim3(256), 0, st, a,
                      mean, rstd, scale, shift, eps);
-  a.silu = silu; a.drop_p = drop_p; a.seed = seed; a.y_split = y_split;
+  a.silu = silu; a.drop_p = drop_p; a.seed = seed; a.y_split = y_split; a.salt = dropout_salt();
   hipLaunchKernelGGL(gn_apply_kernel, dim3(a.chunks, nb), dim3(256), 0, st, a, scale, shift, y);
   return launch_status();
 }
@@ -1050,7 +1056,7 @@ int mvae_group_norm_fwd_part_nhwc(const float* x, const double* part, const floa
   float* shift = scale + (size_t)nb * c;
   hipLaunchKernelGGL(gn_stats_finalize_part_kernel, dim3(cdiv((long long)nb * groups, 4)), dim3(256), 0, st, a, part,
                      mean, rstd, scale, shift, eps);
-  a.silu = silu; a.drop_p = drop_p; a.seed = seed; a.y_split = y_split;
+  a.silu = silu; a.drop_p = drop_p; a.seed = seed; a.y_split = y_split; a.salt = dropout_salt();
   hipLaunchKernelGGL(gn_apply_kernel, dim3(a.chunks, nb), dim3(256), 0, st, a, scale, shift, y);
   return launch_status();
 }
@@ -1072,7 +1078,7 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
   hipStream_t st = (hipStream_t)stream;
   GnArgs a{};
   a.x = x; a.dy = dy; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta; a.dx_add = dx_add;
-  a.nb = nb; a.hw = hw; a.C = c; a.G = groups; a.silu = silu; a.drop_p = drop_p; a.seed = seed;
+  a.nb = nb; a.hw = hw; a.C = c; a.G = groups; a.silu = silu; a.drop_p = drop_p; a.seed = seed; a.salt = dropout_salt();
   a.chunks = gn_chunks(nb, hw);
   a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
   a.ws = (double*)workspace;

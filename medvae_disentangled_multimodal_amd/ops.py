@@ -948,6 +948,21 @@ def set_precision(precision) -> int:
     return prev
 
 
+_SALT = {}
+
+
+def dropout_salt(device) -> torch.Tensor:
+    """The process-wide dropout salt of `device` (one int64 in device memory, allocated once and never freed) and
+    make it the library's salt (mvae_set_dropout_salt): it is mixed into every following GroupNorm dropout seed, so
+    a replayed graph of a training step that advances it draws fresh masks."""
+    device = torch.device(device)
+    t = _SALT.get(device)
+    if t is None:
+        t = _SALT[device] = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64, device=device)
+    _lib.call("mvae_set_dropout_salt", t.data_ptr())
+    return t
+
+
 def restore_math_mode(mode: int):
     _lib.call("mvae_set_math_mode", int(mode))
     _MATH[0] = int(mode)
