@@ -256,7 +256,9 @@ def main():
     step = mod.fit_step_graphed if graphed else mod.fit_step
     for i in range(args.warmup):
         mod.fit_step(batches[i % 2], i)
-    if graphed:  # capture (recorded, not executed) + one replay, untimed
+    if graphed:  # graph set-up, untimed: one eager step (if no warm-up ran), the capture (records, executes
+        if args.warmup == 0:  # nothing), one replay
+            mod.fit_step(batches[0], 0)
         step(batches[args.warmup % 2], args.warmup)
     torch.cuda.synchronize()
     if world > 1:
