@@ -27,6 +27,10 @@ for cfg in ("c4", "c2", "c3", "c5", "c1"):
     if not os.path.exists(tr):
         continue
     rows = list(csv.DictReader(open(tr)))
+    # steps the profiled process executed: the 3 timed ones, plus for a graph-replayed config (c1-c3) the set-up
+    # eager step (--warmup 0) and the first replay after the capture
+    graphed = "graph" in str(bench.get("config", {}).get("step_launch", ""))
+    STEPS = 3 + (2 if graphed else 0)
     agg = collections.defaultdict(lambda: [0, 0.0])
     for r in rows:
         name = r["Kernel_Name"]
@@ -38,8 +42,9 @@ for cfg in ("c4", "c2", "c3", "c5", "c1"):
                "tap_select", "wgrad_direct", "wgrad_small_cout")
     fam = sum(v[1] for k, v in agg.items() if k.startswith("gemm3x") or any(h in k for h in HELPERS))
     g = agg["gemm3x_kernel (all tile / operand instantiations)"]
-    out = [f"rocprofv3 --kernel-trace --stats -- python3 bench.py --config {cfg} --steps {STEPS} --warmup 0 "
-           f"--no-cpu-baseline --no-kernel-timing   (round {rnd}, run {tag})",
+    out = [f"rocprofv3 --kernel-trace --stats -- python3 bench.py --config {cfg} --steps 3 --warmup 0 "
+           f"--no-cpu-baseline --no-kernel-timing   (round {rnd}, run {tag}; normalised by the {STEPS} steps it "
+           f"executes{': 1 eager set-up + 1 replay after the capture + 3 timed replays' if graphed else ''})",
            f"kernel time {tot / STEPS:.2f} ms/step over {len(rows) / STEPS:.0f} launches/step "
            f"(bench line: {bench['ms_per_step']} ms/step wall)",
            f"gemm3x_kernel: {g[1] / STEPS:.2f} ms/step, {g[0] / STEPS:.1f} launches/step, "
