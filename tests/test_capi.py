@@ -86,3 +86,20 @@ def test_fastcall_path_matches_ctypes_without_gpu():
         _lib.call("mvae_softmax_rows", None, None, 0, 0, None)
     with pytest.raises(RuntimeError, match="bad geometry"):  # float + pointer + int mix through the trampoline
         _lib.call("mvae_conv2d_nhwc", 0, 0, None, None, 0, -1, 8, 8, 4, 4, 3, 3, 1, 1, 1, 8, 8, 0, None)
+
+
+def test_conv_split_planner_without_gpu():
+    """Split-K planning for under-filled conv launches (mvae_conv2d_split_workspace_bytes, host only): BetaVAE's
+    7x7 level at 512 channels (98-196 tiles for 256 CUs) and the 2048 -> 512 narrowing conv split; launches that
+    already fill the chip (c4's 64x64 / 16x16 / 8x8x2048 levels) and short-K layers stay unsplit; a split always
+    leaves >= 16 K-tiles per split and the workspace holds whole fp32 partial planes."""
+    q = lambda *a: _lib.query("mvae_conv2d_split_workspace_bytes", *a)
+    n, c, co = 256, 512, 512
+    b = q(n, c, co, 3, 3, 7, 7)
+    m_n = n * 7 * 7 * co * 4
+    assert b > 0 and b % m_n == 0 and 2 <= b // m_n <= (9 * c) // (16 * 32)
+    assert q(256, 2048, 512, 3, 3, 8, 8) > 0
+    for shape in [(256, 256, 256, 3, 3, 64, 64), (256, 1024, 1024, 3, 3, 16, 16), (256, 2048, 2048, 3, 3, 8, 8),
+                  (512, 32, 32, 3, 3, 28, 28), (256, 128, 128, 3, 3, 28, 28)]:
+        assert q(*shape) == 0, shape
+    assert q(256, 6, 256, 3, 3, 64, 64) == 0 and q(0, 512, 512, 3, 3, 7, 7) == 0  # cin % 4, empty batch
