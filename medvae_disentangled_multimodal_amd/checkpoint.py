@@ -70,6 +70,7 @@ def load_checkpoint(module, ckpt, strict: bool = True, load_optimizer: bool = Tr
     optimizer is configured, the Adam/AdamW moments and step counts."""
     if isinstance(ckpt, str):
         ckpt = torch.load(ckpt, map_location="cpu", weights_only=True)
+    module._graph = None  # a captured step froze the old hyper-parameters (betas / eps / lr) as launch values
     sd = {k[len("model."):]: v for k, v in ckpt["state_dict"].items() if k.startswith("model.")}
     module.model.load_state_dict(sd, strict=strict)
     crit = getattr(module, "criterion", None)

@@ -121,8 +121,9 @@ class DisentangledConditionalVAE(BaseVAE):
         sel = idx.view(-1, 1, 1, 1)
         if x.shape[1] >= mx:
             routed = x[:, :mx]
-        else:
-            routed = torch.zeros((x.shape[0], mx) + tuple(x.shape[2:]), device=x.device, dtype=x.dtype)
+        else:  # fewer channels than the colour modalities take (a 1-channel batch): zero-padded, as the collate
+            # pads gray images (medmnist_data.py:16-72) and as the routing kernel reads them (the reference errors)
+            routed = torch.cat([x, x.new_zeros((x.shape[0], mx - x.shape[1]) + tuple(x.shape[2:]))], 1)
         gray = x[:, :1]
         for key, proj in self.modality_input_projectors.items():
             p = _nan_to_zero(proj(gray))

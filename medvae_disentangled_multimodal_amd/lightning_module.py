@@ -224,6 +224,7 @@ class VAELightningModule(_Base):
 
     # ---------------------------------------------------------------------------------------
     def configure_optimizers(self):
+        self._graph = None  # a captured step holds the previous optimizer's buffers and hyper-parameters
         if self.flat is None:
             self.flat = FlatParameters(self.model)
         oc = self.optimizer_config
@@ -277,8 +278,13 @@ class VAELightningModule(_Base):
         if self.optimizer is None or self.global_step_count == 0:
             raise RuntimeError("fit_step_graphed: run at least one eager fit_step first")
         ins = list(batch) + ([eps] if eps is not None else [])
-        key = (tuple((tuple(t.shape), t.dtype, t.device) for t in ins), eps is not None,
-               self.optimizer.param_groups[0]["lr"], self.precision)
+        # everything the captured launches freeze as host values: shapes, the optimizer's hyper-parameters
+        # (lr, betas, eps, weight decay), clip norm and gradient scale, the GEMM arithmetic
+        opt = self.optimizer
+        hyper = tuple(sorted((k, tuple(v) if isinstance(v, (list, tuple)) else v)
+                             for k, v in opt.param_groups[0].items() if k != "params"))
+        key = (tuple((tuple(t.shape), t.dtype, t.device) for t in ins), eps is not None, hyper,
+               opt.max_grad_norm, getattr(opt, "grad_scale", None), id(opt), id(self.flat), self.precision)
         g = getattr(self, "_graph", None)
         if g is None or g["key"] != key:
             g = self._capture_step(ins, len(batch), batch_idx, key)
@@ -295,13 +301,18 @@ class VAELightningModule(_Base):
         salt = ops.dropout_salt(dev)
         self._last_outputs = None  # no autograd graph of an earlier step may outlive into the capture
         torch.cuda.synchronize(dev)
+        self._graph = None  # release an outdated graph (and the arena buffers it pinned) before recording
         graph = torch.cuda.CUDAGraph()
         step0 = self.global_step_count
-        with torch.cuda.graph(graph):  # recorded, not executed: capturing performs no optimisation step
-            salt.add_(1)
-            loss = self.fit_step(static[:nb], batch_idx, eps=static[nb] if len(static) > nb else None)
+        pinned = ops.ARENA.pinning = []  # the graph keeps every scratch buffer it bakes in (ops._Arena)
+        try:
+            with torch.cuda.graph(graph):  # recorded, not executed: capturing performs no optimisation step
+                salt.add_(1)
+                loss = self.fit_step(static[:nb], batch_idx, eps=static[nb] if len(static) > nb else None)
+        finally:
+            ops.ARENA.pinning = None
         self.global_step_count = step0
-        self._graph = dict(graph=graph, inputs=static, loss=loss, salt=salt, key=key)
+        self._graph = dict(graph=graph, inputs=static, loss=loss, salt=salt, key=key, arena=pinned)
         return self._graph
 
     def _adversarial_fit_step(self, batch, eps=None) -> torch.Tensor:

@@ -59,7 +59,13 @@ class LPIPS(nn.Module):
             chans = VGG_CHANNELS
         self.lins = nn.ParameterList([nn.Parameter(torch.empty(c)) for c in chans])
         self.register_buffer("shift", torch.tensor(_SHIFT, dtype=torch.float32))
-        self.register_buffer("inv_scale", 1.0 / torch.tensor(_SCALE, dtype=torch.float32))
+        self.register_buffer("scale", torch.tensor(_SCALE, dtype=torch.float32))
+        self.register_buffer("inv_scale", 1.0 / self.scale, persistent=False)
+        # state dicts use the lpips package's names (LPIPS(net=...).state_dict()), so a reference
+        # checkpoint's `criterion.perceptual_loss.lpips.*` keys load and written checkpoints match them
+        self._register_state_dict_hook(LPIPS._to_package_names)
+        self._register_load_state_dict_pre_hook(LPIPS._from_package_names, with_module=True)
+        self.register_load_state_dict_post_hook(LPIPS._refresh_inv_scale)
         if weights is None:
             path = os.environ.get("MVAE_LPIPS_WEIGHTS")
             if path:
@@ -94,15 +100,71 @@ class LPIPS(nn.Module):
             c = lin.numel()
             lin.copy_(torch.rand(c, generator=g) / c)  # non-negative, like the trained linear layers
 
+    def _conv_names(self):
+        """(internal prefix, lpips-package prefix) of every conv: `conv1` <-> `net.slice1.0`, `vgg.3` <->
+        `net.slice2.7` (lpips.pretrained_networks slices over torchvision's `features` indices)."""
+        names = _ALEX_CONVS if self.net == "alex" else _VGG_CONVS
+        internal = [f"conv{i + 1}" for i in range(5)] if self.net == "alex" else [f"vgg.{i}" for i in range(13)]
+        return [(a, f"net.slice{sl}.{idx}") for a, (sl, idx) in zip(internal, names)]
+
+    @staticmethod
+    def _to_package_names(module, state_dict, prefix, local_metadata):
+        for ours, theirs in module._conv_names():
+            for t in ("weight", "bias"):
+                state_dict[f"{prefix}{theirs}.{t}"] = state_dict.pop(f"{prefix}{ours}.{t}")
+        for k in range(len(module.lins)):
+            w = state_dict.pop(f"{prefix}lins.{k}").reshape(1, -1, 1, 1)
+            state_dict[f"{prefix}lin{k}.model.1.weight"] = w
+            state_dict[f"{prefix}lins.{k}.model.1.weight"] = w  # lpips registers its lin layers twice
+        for b in ("shift", "scale"):
+            state_dict[f"{prefix}scaling_layer.{b}"] = state_dict.pop(f"{prefix}{b}").reshape(1, 3, 1, 1)
+        return state_dict
+
+    @staticmethod
+    def _from_package_names(module, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                            error_msgs):
+        """Translate lpips-package keys to the module's own (both spellings load)."""
+        for ours, theirs in module._conv_names():
+            for t in ("weight", "bias"):
+                if f"{prefix}{theirs}.{t}" in state_dict:
+                    state_dict[f"{prefix}{ours}.{t}"] = state_dict.pop(f"{prefix}{theirs}.{t}")
+        for k in range(len(module.lins)):
+            dup = state_dict.pop(f"{prefix}lins.{k}.model.1.weight", None)
+            w = state_dict.pop(f"{prefix}lin{k}.model.1.weight", dup)
+            if w is not None:
+                state_dict[f"{prefix}lins.{k}"] = w.reshape(-1)
+        for b in ("shift", "scale"):
+            if f"{prefix}scaling_layer.{b}" in state_dict:
+                state_dict[f"{prefix}{b}"] = state_dict.pop(f"{prefix}scaling_layer.{b}").reshape(-1)
+        if f"{prefix}inv_scale" in state_dict and f"{prefix}scale" not in state_dict:  # round-2 checkpoints
+            state_dict[f"{prefix}scale"] = 1.0 / state_dict.pop(f"{prefix}inv_scale")
+        state_dict.pop(f"{prefix}inv_scale", None)
+
+    @staticmethod
+    def _refresh_inv_scale(module, incompatible_keys):
+        with torch.no_grad():
+            module.inv_scale.copy_(1.0 / module.scale)
+
+    def internal_weights(self) -> Dict[str, torch.Tensor]:
+        """Weights under the module's own names (the oracle's lpips_alex / lpips_vgg take these)."""
+        out = {f"{ours}.{t}": getattr(c, t) for (ours, _), c in zip(self._conv_names(), self.convs())
+               for t in ("weight", "bias")}
+        out.update({f"lins.{k}": w for k, w in enumerate(self.lins)})
+        return out
+
     @torch.no_grad()
     def load_lpips_state_dict(self, sd: Dict[str, torch.Tensor]):
-        """Load weights named as in the lpips package (LPIPS(net=...).state_dict())."""
-        names = _ALEX_CONVS if self.net == "alex" else _VGG_CONVS
-        for conv, (sl, idx) in zip(self.convs(), names):
-            conv.weight.copy_(sd[f"net.slice{sl}.{idx}.weight"])
-            conv.bias.copy_(sd[f"net.slice{sl}.{idx}.bias"])
-        for k, lin in enumerate(self.lins):
-            lin.copy_(sd[f"lin{k}.model.1.weight"].reshape(-1))
+        """Load weights named as in the lpips package (LPIPS(net=...).state_dict()); the ScalingLayer
+        buffers are optional (lpips hard-codes them)."""
+        sd = dict(sd)
+        for b in ("shift", "scale"):
+            sd.setdefault(f"scaling_layer.{b}", getattr(self, b).detach().clone().view(1, 3, 1, 1))
+        self.load_state_dict(sd, strict=False)
+        missing = [f"{t}.{x}" for _, t in self._conv_names() for x in ("weight", "bias") if f"{t}.{x}" not in sd]
+        missing += [f"lin{k}.model.1.weight" for k in range(len(self.lins))
+                    if f"lin{k}.model.1.weight" not in sd and f"lins.{k}.model.1.weight" not in sd]
+        if missing:
+            raise KeyError(f"lpips weights missing: {missing[:4]}")
 
     def features(self, x: torch.Tensor) -> List[torch.Tensor]:
         if self.net == "vgg":

@@ -48,10 +48,18 @@ def nhwc(t: torch.Tensor) -> torch.Tensor:
 
 
 class _Arena:
-    """Per-device scratch buffers reused across launches (all work is ordered on one stream)."""
+    """Per-device scratch buffers reused across launches (all work is ordered on one stream).
+
+    A buffer that is outgrown is replaced (and its memory returned to the caching allocator). A captured
+    HIP graph bakes in the raw pointers of the buffers it used, so while a capture records (`pinning`
+    set by VAELightningModule._capture_step) every buffer handed out is also kept in that list: the graph
+    holds them for its lifetime and later eager calls that grow the arena cannot free memory a replay
+    writes into. `generation` counts replacements."""
 
     def __init__(self):
         self.bufs = {}
+        self.generation = 0
+        self.pinning = None
 
     def get(self, key: str, nbytes: int, device) -> torch.Tensor:
         k = (key, str(device))
@@ -59,6 +67,9 @@ class _Arena:
         if t is None or t.numel() < nbytes:
             t = torch.empty(max(int(nbytes * 1.25) + 256, 256), dtype=torch.uint8, device=device)
             self.bufs[k] = t
+            self.generation += 1
+        if self.pinning is not None and not any(p is t for p in self.pinning):
+            self.pinning.append(t)
         return t
 
 

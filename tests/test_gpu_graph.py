@@ -83,3 +83,50 @@ def test_graph_salt_advances_and_lr_change_recaptures(dev):
     l3 = float(mod.fit_step_graphed(batch, 3))
     assert mod._graph["graph"] is not g1
     assert all(v == v and abs(v) < 1e6 for v in (l1, l2, l3))
+
+
+def test_graph_survives_eager_calls_that_grow_the_arena(dev):
+    """a replay writes into the scratch buffers baked into the graph. An eager evaluate at twice
+    the batch grows (replaces) those arena buffers between replays; the graph must keep its own buffers alive, so
+    graphed steps interleaved with the large eager call give the eager-only steps' results."""
+    from medvae_disentangled_multimodal_amd import ops
+    cls, kw, loss = CASES[1]
+    batch, big = _batch(cls, dev), _batch(cls, dev, B=32)
+    a = _module(cls, kw, loss, dev)
+    b = _module(cls, kw, loss, dev)
+    r = 28 // 2 ** (len(kw["ch_mult"]) - 1)
+    g = torch.Generator().manual_seed(9)
+    eps = [torch.randn(16, a.model.latent_dim, r, r, generator=g).to(dev) for _ in range(4)]
+    la = [a.fit_step(batch, i, eps=eps[i]) for i in range(4)]
+    lb = [b.fit_step(batch, 0, eps=eps[0]), b.fit_step_graphed(batch, 1, eps=eps[1]).clone()]
+    gen0 = ops.ARENA.generation
+    ea = b.evaluate(big)  # eager, 2x batch: outgrows the scratch buffers the graph captured
+    assert ops.ARENA.generation > gen0 and b._graph["arena"], "the test needs an arena reallocation"
+    junk = torch.full((64 << 20,), float("nan"), device=dev)  # reuse freed memory, if any was freed
+    lb += [b.fit_step_graphed(batch, i, eps=eps[i]).clone() for i in (2, 3)]
+    torch.cuda.synchronize()
+    del junk
+    for x, y in zip(la, lb):
+        assert abs(float(x) - float(y)) <= 1e-5 * abs(float(x)) + 1e-7, (float(x), float(y))
+    assert float((a.flat.data - b.flat.data).abs().max()) <= 1e-5
+    assert all(torch.isfinite(v).all() for v in ea.values() if torch.is_tensor(v))
+
+
+def test_graph_key_covers_optimizer_hyperparameters(dev):
+    """betas / eps / weight decay / clip norm are frozen into the captured launches; changing
+    any of them (e.g. a checkpoint load) must re-capture."""
+    cls, kw, loss = CASES[1]
+    mod = _module(cls, kw, loss, dev)
+    batch = _batch(cls, dev)
+    mod.fit_step(batch, 0)
+    mod.fit_step_graphed(batch, 1)
+    g1 = mod._graph["graph"]
+    mod.fit_step_graphed(batch, 2)
+    assert mod._graph["graph"] is g1
+    mod.optimizer.param_groups[0]["betas"] = (0.5, 0.999)
+    mod.fit_step_graphed(batch, 3)
+    g2 = mod._graph["graph"]
+    assert g2 is not g1
+    mod.optimizer.max_grad_norm = 2.0
+    mod.fit_step_graphed(batch, 4)
+    assert mod._graph["graph"] is not g2

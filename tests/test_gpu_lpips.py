@@ -70,7 +70,7 @@ def test_lpips_layer_distance(dev):
 
 
 def _lpips_weights(m):
-    return {k: v.detach().cpu().double() for k, v in m.state_dict().items() if not k.endswith(("shift", "inv_scale"))}
+    return {k: v.detach().cpu().double() for k, v in m.internal_weights().items()}
 
 
 def test_lpips_network_vs_oracle(dev):

@@ -111,3 +111,23 @@ def test_route_in_matches_per_sample_loop():
         gw, gb = gw.cpu(), gb.cpu()
         assert float((pj.weight.grad.double().cpu() - gw).norm() / gw.norm()) < 1e-5
         assert float((pj.bias.grad.double().cpu() - gb).norm() / gb.norm()) < 1e-5
+
+
+def test_one_channel_batch_routing_kernel_matches_grouped_form(monkeypatch):
+    """a 1-channel batch (cx = 1) with colour modalities present. The routing kernel reads the
+    missing channels as zeros ([x0, 0, 0]); the grouped form (MVAE_NO_ROUTING / large images) zero-pads the same
+    way, so both paths give the same encoder input and latents."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import medvae_disentangled_multimodal_amd.disentangled as D
+    dev = torch.device("cuda:0")
+    model = _model(dev)
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(6, 1, 28, 28, generator=g).to(dev).contiguous(memory_format=torch.channels_last)
+    idx = torch.tensor([0, 1, 2, 3, 4, 1], device=dev)
+    with torch.no_grad():
+        mu_k, lv_k = model.encode(x, idx)
+        monkeypatch.setattr(D, "ROUTING_KERNELS", False)
+        mu_g, lv_g = model.encode(x, idx)
+    assert float((mu_k - mu_g).abs().max()) <= 1e-5 * float(mu_g.abs().max()) + 1e-7
+    assert float((lv_k - lv_g).abs().max()) <= 1e-5 * float(lv_g.abs().max()) + 1e-7
