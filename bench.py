@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import socket
 import subprocess
@@ -206,39 +207,110 @@ def launch_ranks(n: int, cmd=None) -> int:
     return rc
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
-    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch override (default: config)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--detail", action="store_true", help="per-shape GEMM launch timings on stderr")
-    ap.add_argument("--eager", action="store_true", help="launch every kernel from Python (no HIP-graph replay)")
-    args = ap.parse_args()
+def cpu_baseline_for(cfg, seconds_budget=20.0):
+    """cpu_baseline() for any config; c5's objective (bf16 + LPIPS-VGG generator loss) is timed as the oracle's fp32
+    LPIPS-VGG objective over the same model (the reference's CPU path has no bf16 autocast for these convs)."""
+    if cfg["loss"]["type"] in ("vae", "disentangled_vae"):
+        return cpu_baseline(cfg, seconds_budget)
+    from oracle import torch_ref as R
+    from medvae_disentangled_multimodal_amd.lpips import LPIPS
+    lp = LPIPS(net=cfg["loss"].get("lpips_net", "alex"), allow_synthetic=True)
+    c = dict(cfg)
+    c["loss"] = dict(cfg["loss"], lpips_weights={k: v.detach() for k, v in lp.internal_weights().items()})
+    out = cpu_baseline(c, seconds_budget)
+    out["sample"] += "; objective: LPIPS-VGG (oracle lpips_vgg, synthetic weights) + 1e-5 * KL.sum()/B"
+    return out
 
-    env_world = os.environ.get("WORLD_SIZE")
-    if env_world is None and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus))
-    if env_world is not None and int(env_world) != args.gpus:
-        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
 
+def _roofline(rec_all, bf16, config, step_ms, detail, rank):
+    """GEMM-family (MFMA) and GroupNorm-family (HBM) rooflines from the HIP-event records of one step."""
+    rec = [r for r in rec_all if r[0] not in ops_hbm_tags()]
+    hbm_rec = [r for r in rec_all if r[0] in ops_hbm_tags()]
+    tot_ms = sum(r[2].elapsed_time(r[3]) for r in rec)
+    tot_fl = sum(r[1] for r in rec)
+    tot_ref = sum(r[5] for r in rec)
+    if detail and rank == 0:
+        agg = {}
+        for tag, f, s_, e, shp, _ in rec:
+            d = agg.setdefault((tag, shp), [0, 0.0, 0.0])
+            d[0] += 1
+            d[1] += f
+            d[2] += s_.elapsed_time(e)
+        for (tag, shp), (cnt, f, ms) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
+            print(f"[detail {config}] {tag:10s} {str(shp):42s} x{cnt:3d} {ms:8.2f} ms {f / (ms * 1e-3) / 1e12:7.1f} TF/s",
+                  file=sys.stderr)
+    by = {}
+    for tag, f, s_, e, _, _ in rec:
+        d = by.setdefault(tag, [0, 0.0, 0.0])
+        d[0] += 1
+        d[1] += f
+        d[2] += s_.elapsed_time(e)
+    ach = tot_fl / (tot_ms * 1e-3) / 1e12
+    alg_bytes = sum(gemm_algorithmic_bytes(r[0], r[4]) for r in rec) / max(len(rec), 1)
+    peak = BF16_DENSE_PEAK_TF if bf16 else PEAK_3XBF16_TF
+    pmc = _pmc_traffic(config)
+    roofline = {"bound": "mfma", "kernel": "gemm3x_kernel (implicit-GEMM conv + attention bmm, all launches)",
+                "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                "frac": round(ach / peak, 4), "traffic": (pmc or {}).get("bytes_per_launch"),
+                "traffic_unit": "HBM bytes per launch (PMC)", "traffic_detail": pmc,
+                "algorithmic_bytes_per_launch": round(alg_bytes),
+                "peak_note": ("bf16 dense MFMA peak 2.5 PF/s (bf16 operands, fp32 accumulate)" if bf16 else
+                              "3xBF16 fp32-emulation ceiling = bf16 dense MFMA 2.5 PF/s / 3; "
+                              "native fp32 MFMA peak is 157.3 TF/s"),
+                "achieved_note": ("algorithmic FLOPs of the algorithms run (Upsample convs in sub-pixel form "
+                                  "count 4/9 of the reference conv's FLOPs)"),
+                "reference_equivalent_TFLOP/s": round(tot_ref / (tot_ms * 1e-3) / 1e12, 2),
+                "launches_per_step": len(rec), "avg_launch_us": round(tot_ms * 1e3 / max(len(rec), 1), 2),
+                "gemm_ms_per_step": round(tot_ms, 2), "instrumented_step_ms": round(step_ms, 2),
+                "gemm_share_of_step": round(tot_ms / step_ms, 3),
+                "by_pass": {k: {"launches": v[0], "ms": round(v[2], 2),
+                                "TFLOP/s": round(v[1] / (v[2] * 1e-3) / 1e12, 1)} for k, v in by.items()}}
+    if not bf16:  # measured ceiling of the main-loop structure (no global traffic): profiles/r02_ceilings.txt
+        for k, v in roofline["by_pass"].items():
+            c = STRUCT_CEIL_TF.get(k)
+            if c is None:
+                continue
+            v["structure_ceiling_TFLOP/s"] = c
+            v["frac_of_structure_ceiling"] = round(v["TFLOP/s"] / c, 3)
+        roofline["structure_ceiling_note"] = (
+            "measured on the box: the kernel's per-wave 3xBF16 LDS-fragment + MFMA loop with one barrier per "
+            "K-tile and no global loads, random operands (tools/micro/mfma_shape.hip): 16x16x32 (fwd / dgrad) "
+            "598 TF/s, 32x32x16 (wgrad / attention) 559 TF/s fp32-equivalent")
+    if hbm_rec:  # the memory-bound GroupNorm(+SiLU) family against the HBM roofline
+        hb = {}
+        for tag, nbytes, s_, e, _, _ in hbm_rec:
+            d = hb.setdefault(tag, [0, 0.0, 0.0])
+            d[0] += 1
+            d[1] += nbytes
+            d[2] += s_.elapsed_time(e)
+        hms = sum(v[2] for v in hb.values())
+        hby = sum(v[1] for v in hb.values())
+        roofline["hbm_kernels"] = {
+            "bound": "hbm", "kernel": "GroupNorm(+SiLU) fwd / bwd (gn_* kernel chains, all launches)",
+            "achieved": round(hby / (hms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(hby / (hms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms_per_step": round(hms, 2),
+            "measured_stream_GB/s": HBM_MEASURED_GBS,
+            "bytes_note": "algorithmic bytes: fwd 8 B/elem (read x, write y), bwd 12 B/elem (read x, dy; write dx) "
+                          "+ 4 B/elem where the residual branch's gradient is summed in (ResnetBlock / AttnBlock "
+                          "norm1); chains include the statistics finalize and parameter-gradient kernels",
+            "by_pass": {k: {"launches": v[0], "ms": round(v[2], 2),
+                            "GB/s": round(v[1] / (v[2] * 1e-3) / 1e9, 1)} for k, v in hb.items()}}
+    return roofline
+
+
+def ops_hbm_tags():
+    from medvae_disentangled_multimodal_amd import ops
+    return ops.HBM_TAGS
+
+
+def run_config(name, args, rank, world, dev, want_cpu=True):
+    """Build the config's model, warm up, time `args.steps` steps (barrier + synchronize on both sides, max over
+    ranks), then one instrumented step for the rooflines. Returns the measured fields of the JSON line."""
     import medvae_disentangled_multimodal_amd as M
     from medvae_disentangled_multimodal_amd import ddp, ops
-
-    # MVAE_BENCH_BACKEND / MVAE_BENCH_ONE_DEVICE: rehearse the multi-rank bench on a 1-GPU box (gloo transport,
-    # every rank on cuda:0); the production path is RCCL with one rank per GPU
-    rank, world, local = ddp.init_from_env(os.environ.get("MVAE_BENCH_BACKEND"))
-    if os.environ.get("MVAE_BENCH_ONE_DEVICE"):
-        local = 0
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    cfg = dict(CONFIGS[args.config])
+    cfg = dict(CONFIGS[name])
     if args.batch:
         cfg["batch"] = args.batch
-
     torch.manual_seed(42)
     model = getattr(M, cfg["cls"])(**cfg["kwargs"]).to(dev)
     mod = M.VAELightningModule(model, cfg["opt"], {"type": "none"}, cfg["loss"], gradient_clip_val=cfg["clip"],
@@ -289,97 +361,144 @@ def main():
         step_ms = (time.perf_counter() - t1) * 1e3
         rec_all = ops.PROFILE
         ops.PROFILE = None
-        rec = [r for r in rec_all if r[0] not in ops.HBM_TAGS]
-        hbm_rec = [r for r in rec_all if r[0] in ops.HBM_TAGS]
-        tot_ms = sum(r[2].elapsed_time(r[3]) for r in rec)
-        tot_fl = sum(r[1] for r in rec)
-        tot_ref = sum(r[5] for r in rec)
-        if args.detail and rank == 0:
-            agg = {}
-            for tag, f, s, e, shp, _ in rec:
-                d = agg.setdefault((tag, shp), [0, 0.0, 0.0])
-                d[0] += 1
-                d[1] += f
-                d[2] += s.elapsed_time(e)
-            for (tag, shp), (cnt, f, ms) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
-                print(f"[detail] {tag:10s} {str(shp):42s} x{cnt:3d} {ms:8.2f} ms {f / (ms * 1e-3) / 1e12:7.1f} TF/s",
-                      file=sys.stderr)
-        by = {}
-        for tag, f, s, e, _, _ in rec:
-            d = by.setdefault(tag, [0, 0.0, 0.0])
-            d[0] += 1
-            d[1] += f
-            d[2] += s.elapsed_time(e)
-        ach = tot_fl / (tot_ms * 1e-3) / 1e12
-        alg_bytes = sum(gemm_algorithmic_bytes(r[0], r[4]) for r in rec) / max(len(rec), 1)
-        peak = BF16_DENSE_PEAK_TF if bf16 else PEAK_3XBF16_TF
-        roofline = {"bound": "mfma", "kernel": "gemm3x_kernel (implicit-GEMM conv + attention bmm, all launches)",
-                    "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-                    "frac": round(ach / peak, 4), "traffic": (_pmc_traffic(args.config) or {}).get("bytes_per_launch"),
-                    "traffic_unit": "HBM bytes per launch (PMC)", "traffic_detail": _pmc_traffic(args.config),
-                    "algorithmic_bytes_per_launch": round(alg_bytes),
-                    "peak_note": ("bf16 dense MFMA peak 2.5 PF/s (bf16 operands, fp32 accumulate)" if bf16 else
-                                  "3xBF16 fp32-emulation ceiling = bf16 dense MFMA 2.5 PF/s / 3; "
-                                  "native fp32 MFMA peak is 157.3 TF/s"),
-                    "achieved_note": ("algorithmic FLOPs of the algorithms run (Upsample convs in sub-pixel form "
-                                      "count 4/9 of the reference conv's FLOPs)"),
-                    "reference_equivalent_TFLOP/s": round(tot_ref / (tot_ms * 1e-3) / 1e12, 2),
-                    "launches_per_step": len(rec), "avg_launch_us": round(tot_ms * 1e3 / len(rec), 2),
-                    "gemm_ms_per_step": round(tot_ms, 2), "instrumented_step_ms": round(step_ms, 2),
-                    "gemm_share_of_step": round(tot_ms / step_ms, 3),
-                    "by_pass": {k: {"launches": v[0], "ms": round(v[2], 2),
-                                    "TFLOP/s": round(v[1] / (v[2] * 1e-3) / 1e12, 1)} for k, v in by.items()}}
-        if not bf16:  # measured ceiling of the main-loop structure (no global traffic): profiles/r02_ceilings.txt
-            for k, v in roofline["by_pass"].items():
-                c = STRUCT_CEIL_TF.get(k)
-                if c is None:
-                    continue
-                v["structure_ceiling_TFLOP/s"] = c
-                v["frac_of_structure_ceiling"] = round(v["TFLOP/s"] / c, 3)
-            roofline["structure_ceiling_note"] = (
-                "measured on the box: the kernel's per-wave 3xBF16 LDS-fragment + MFMA loop with one barrier per "
-                "K-tile and no global loads, random operands (tools/micro/mfma_shape.hip): 16x16x32 (fwd / dgrad) "
-                "598 TF/s, 32x32x16 (wgrad / attention) 559 TF/s fp32-equivalent")
-        if hbm_rec:  # the memory-bound GroupNorm(+SiLU) family against the HBM roofline
-            hb = {}
-            for tag, nbytes, s, e, _, _ in hbm_rec:
-                d = hb.setdefault(tag, [0, 0.0, 0.0])
-                d[0] += 1
-                d[1] += nbytes
-                d[2] += s.elapsed_time(e)
-            hms = sum(v[2] for v in hb.values())
-            hby = sum(v[1] for v in hb.values())
-            roofline["hbm_kernels"] = {
-                "bound": "hbm", "kernel": "GroupNorm(+SiLU) fwd / bwd (gn_* kernel chains, all launches)",
-                "achieved": round(hby / (hms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(hby / (hms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms_per_step": round(hms, 2),
-                "measured_stream_GB/s": HBM_MEASURED_GBS,
-                "bytes_note": "algorithmic bytes: fwd 8 B/elem (read x, write y), bwd 12 B/elem (read x, dy; write dx) "
-                              "+ 4 B/elem where the residual branch's gradient is summed in (ResnetBlock / AttnBlock "
-                              "norm1); chains include the statistics finalize and parameter-gradient kernels",
-                "by_pass": {k: {"launches": v[0], "ms": round(v[2], 2),
-                                "GB/s": round(v[1] / (v[2] * 1e-3) / 1e9, 1)} for k, v in hb.items()}}
+        roofline = _roofline(rec_all, bf16, name, step_ms, args.detail, rank)
+    del mod, model, batches, step
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg["loss"]["type"] in ("vae", "disentangled_vae"):
-        cpu = cpu_baseline(cfg)
+    if rank == 0 and world == 1 and want_cpu and not args.no_cpu_baseline:
+        cpu = cpu_baseline_for(cfg)
+    imgs = cfg["batch"] * world * args.steps
+    return {"value": round(imgs / dt, 3), "unit": "images/s", "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "dtype": ("bf16 (bf16-mixed: bf16 MFMA operands, fp32 accumulate/activations)" if bf16
+                      else "fp32 (3xBF16 MFMA, fp32 accumulate)"),
+            "config": {"workload": f"{cfg['cls']} {cfg['res']}x{cfg['res']}x{cfg['kwargs'].get('input_channels', 3)} "
+                                   f"train step (fwd+loss+bwd+clip+{cfg['opt']['type']})"
+                                   + (" + LPIPS-VGG generator objective" if bf16 else ""),
+                       "model": cfg["cls"], "params": nparams, "global_batch": cfg["batch"] * world,
+                       "per_gpu_batch": cfg["batch"], "resolution": cfg["res"], "parallelism": f"dp{world}",
+                       "rccl_world_size": world, "backend": dist.get_backend() if world > 1 else None,
+                       "step_launch": "hip graph (captured step)" if graphed else "eager"},
+            "loss": round(loss_v, 6), "roofline": roofline, "cpu_baseline": cpu}
+
+
+def parity_block(dev):
+    """ELBO parity of the metric's model at its exact architecture: one training step of the cvae_c4_full golden
+    case (the reference's own src.models ConditionalVAE, 927 M parameters, B=2; tests/golden/make_golden.py) on the
+    HIP path, compared with the reference's outputs, loss terms and global gradient norm (north_star: 1e-3
+    relative), plus the one-hot condition map bitwise. Runs after the timed region."""
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    import medvae_disentangled_multimodal_amd as M
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from cases import CASES
+    from weights import synth_param
+    name = "cvae_c4_full"
+    case = CASES[name]
+    with open(os.path.join(ROOT, "tests", "golden", f"{name}.json")) as f:
+        meta = json.load(f)
+    data = dict(np.load(os.path.join(ROOT, "tests", "golden", f"{name}.npz"), allow_pickle=False))
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(16) as ex:  # the golden weights, regenerated from their names (weights.py)
+        arrs = list(ex.map(lambda ks: synth_param(ks[0], ks[1]), [(k, tuple(s)) for k, s in meta["params"]]))
+    state = {k: torch.from_numpy(a) for (k, _), a in zip(meta["params"], arrs)}
+    model = getattr(M, case["cls"])(**case["kwargs"])
+    model.load_state_dict(state)
+    model = model.to(dev)
+    mod = M.VAELightningModule(model, case["optimizer"], {"type": "none"}, case["loss"], gradient_clip_val=case["clip"])
+    mod.configure_optimizers()
+    x = torch.from_numpy(data["in.x"]).to(dev)
+    batch = (x, torch.zeros(x.shape[0], 1, dtype=torch.long, device=dev), torch.from_numpy(data["in.cond"]).to(dev))
+    eps = torch.from_numpy(data["in.eps"]).to(dev)
+    mod.fit_step(batch, 0, eps=eps)
+    torch.cuda.synchronize()
+    out = mod._last_outputs
+
+    def rel(a, b):
+        a = a.detach().double().cpu().flatten()
+        b = torch.from_numpy(b).double().flatten()
+        return float((a - b).norm() / b.norm())
+
+    errs = {f"out.{k}": rel(out[k], data[f"out.{k}"]) for k in ("reconstruction", "mean", "logvar", "z")}
+    for k in ("loss", "recon_loss", "kl_loss"):
+        ref = float(data[f"loss.{k}"])
+        errs[f"loss.{k}"] = abs(float(mod.logged[f"train/{k}"]) - ref) / abs(ref)
+    has = [k for k, v in meta["param_has_grad"].items() if v]
+    exact = math.sqrt(sum(float(data[f"gradsum.{k}"][1]) for k in has))
+    errs["grad_global_norm_vs_exact"] = abs(float(mod.optimizer.last_total_norm) - exact) / exact
+    lin = model.condition_proj[0]
+    with torch.no_grad():
+        from medvae_disentangled_multimodal_amd import ops
+        xc, _ = ops.condition_concat(x, batch[2], lin.weight, lin.bias)
+    cm = xc[:, x.shape[1]:].detach().cpu().numpy()
+    bitwise = bool(np.array_equal(cm.view(np.int32), data["out.cond_map"].view(np.int32)))
+    del mod, model
+    torch.cuda.empty_cache()
+    worst = max(errs.values())
+    return {"case": f"{name} (reference src.models ConditionalVAE, c4 architecture, B=2, injected eps)",
+            "tolerance": 1e-3, "pass": bool(worst < 1e-3 and bitwise), "max_rel_err": worst,
+            "rel_err": {k: float(f"{v:.3e}") for k, v in errs.items()}, "condition_map_bitwise": bitwise,
+            "seconds": round(time.perf_counter() - t0, 1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="one config alone (default: c4, plus the c2 / c3 / c5 block and the parity block at N=1)")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch override (default: config)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--detail", action="store_true", help="per-shape GEMM launch timings on stderr")
+    ap.add_argument("--eager", action="store_true", help="launch every kernel from Python (no HIP-graph replay)")
+    args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
+
+    from medvae_disentangled_multimodal_amd import ddp
+
+    # MVAE_BENCH_BACKEND / MVAE_BENCH_ONE_DEVICE: rehearse the multi-rank bench on a 1-GPU box (gloo transport,
+    # every rank on cuda:0); the production path is RCCL with one rank per GPU
+    rank, world, local = ddp.init_from_env(os.environ.get("MVAE_BENCH_BACKEND"))
+    if os.environ.get("MVAE_BENCH_ONE_DEVICE"):
+        local = 0
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    head = args.config or "c4"
+    full = args.config is None and world == 1 and args.batch is None
+    line = run_config(head, args, rank, world, dev)
+    extra, parity = None, None
+    if full:  # the other BASELINE configs on the same box, same clock (their own images/s; not summed)
+        extra = {}
+        for c in ("c2", "c3", "c5"):
+            r = run_config(c, args, rank, world, dev)
+            extra[c] = {k: r[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config",
+                                          "loss", "roofline", "cpu_baseline")}
+            print(f"[bench] {c}: {r['value']} images/s ({r['ms_per_step']} ms/step)", file=sys.stderr, flush=True)
+        if not args.no_parity:
+            parity = parity_block(dev)
 
     if rank == 0:
-        imgs = cfg["batch"] * world * args.steps
-        out = {"metric": METRIC_C4 if args.config == "c4" else
-               f"training images/sec (whole node), config {args.config}",
-               "value": round(imgs / dt, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": ("bf16 (bf16-mixed: bf16 MFMA operands, fp32 accumulate/activations)" if bf16
-                                                     else "fp32 (3xBF16 MFMA, fp32 accumulate)"),
+        out = {"metric": METRIC_C4 if head == "c4" else f"training images/sec (whole node), config {head}",
+               "value": line["value"], "unit": "images/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": line["ms_per_step"], "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": line["dtype"],
                "data": "synthetic (MedMNIST-shaped, resident in HBM; random-init weights)",
-               "config": {"workload": f"{cfg['cls']} {cfg['res']}x{cfg['res']}x{cfg['kwargs'].get('input_channels', 3)} "
-                                      f"train step (fwd+loss+bwd+clip+AdamW)", "model": cfg["cls"],
-                          "params": nparams, "global_batch": cfg["batch"] * world, "per_gpu_batch": cfg["batch"],
-                          "resolution": cfg["res"], "parallelism": f"dp{world}", "rccl_world_size": world,
-                          "backend": dist.get_backend() if world > 1 else None,
-                          "step_launch": "hip graph (captured step)" if graphed else "eager"},
-               "loss": round(loss_v, 6), "roofline": roofline, "cpu_baseline": cpu}
+               "config": line["config"], "loss": line["loss"], "roofline": line["roofline"],
+               "cpu_baseline": line["cpu_baseline"]}
+        if extra is not None:
+            out["configs"] = extra
+        if parity is not None:
+            out["parity"] = parity
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -335,6 +335,17 @@ int mvae_modality_route_in_bwd(const float* x, int cx, const long long* idx, int
                                void* workspace, size_t ws_bytes, void* stream);
 size_t mvae_modality_route_in_workspace_bytes(int nb, int c);
 
+/* ConditionalVAE concat conditioning (src/models/conditional_vae.py:65-69 condition_proj = Linear(K -> c*64) + ReLU
+ * + Unflatten(c, 8, 8); :107-127 create_condition_map = bilinear to (h, w), align_corners=False; :131-136
+ * torch.cat([x, map], 1)). x [nb][h][w][c] NHWC, cond [nb][K], w [c*64][K], bias [c*64]; writes m = relu(pre)
+ * [nb][c*64] (kept for the backward) and xcond [nb][h][w][2c]. Bit-exact with the reference's CPU path for a
+ * one-hot condition (the projection is W[:, idx] + bias) and for its bilinear kernel (h + w <= 128). h, w <= 256.
+ * The backward accumulates dw / dbias (beta = 1) from dxcond; dpre is scratch of nb*c*64 floats. */
+int mvae_condition_concat_fwd(const float* x, const float* cond, const float* w, const float* bias, float* m,
+                              float* xcond, int nb, int c, int h, int wd, int K, void* stream);
+int mvae_condition_concat_bwd(const float* dxcond, const float* cond, const float* m, float* dw, float* dbias,
+                              float* dpre, int nb, int c, int h, int wd, int K, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

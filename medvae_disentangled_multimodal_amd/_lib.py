@@ -90,6 +90,8 @@ SIGNATURES = {
     "mvae_modality_route_in_fwd": (I, [P, I, P, I, I, I, I, P, P, P]),
     "mvae_modality_route_in_bwd": (I, [P, I, P, I, I, I, I, P, P, P, P, Z, P]),
     "mvae_modality_route_in_workspace_bytes": (Z, [I, I]),
+    "mvae_condition_concat_fwd": (I, [P, P, P, P, P, P, I, I, I, I, I, P]),
+    "mvae_condition_concat_bwd": (I, [P, P, P, P, P, P, I, I, I, I, I, P]),
 }
 
 

@@ -1343,3 +1343,47 @@ class RouteInFn(torch.autograd.Function):
 
 def modality_route_in(x, idx, c: int, nm: int, params):
     return RouteInFn.apply(x, idx, c, nm, *params)
+
+
+# ------------------------------------------------------------------------------------------
+# ConditionalVAE concat conditioning (conditional_vae.py:65-69, 107-136): Linear + ReLU + bilinear + cat in two
+# launches (csrc/condition.hip); bit-exact with the reference for a one-hot condition
+# ------------------------------------------------------------------------------------------
+class ConditionConcatFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cond, weight, bias):
+        _check(x, "input")
+        x = nhwc(x)
+        n, c, h, w = x.shape
+        cond = cond.to(device=x.device, dtype=torch.float32).contiguous()
+        k = cond.shape[1]
+        if weight.shape != (c * 64, k) or bias.shape != (c * 64,):
+            raise ValueError(f"condition_proj must be Linear({k} -> {c * 64}), got {tuple(weight.shape)}")
+        m = torch.empty((n, c * 64), device=x.device, dtype=torch.float32)
+        xc = torch.empty((n, 2 * c, h, w), device=x.device, dtype=torch.float32, memory_format=CL)
+        _lib.call("mvae_condition_concat_fwd", x.data_ptr(), cond.data_ptr(), weight.contiguous().data_ptr(),
+                  bias.data_ptr(), m.data_ptr(), xc.data_ptr(), n, c, h, w, k, _stream(x))
+        ctx.save_for_backward(cond, m)
+        ctx.mark_non_differentiable(m)
+        ctx.param_refs = (weight, bias)
+        ctx.x_grad = x.requires_grad
+        ctx.shape = (n, c, h, w, k)
+        return xc, m
+
+    @staticmethod
+    def backward(ctx, dxc, dm_unused):
+        cond, m = ctx.saved_tensors
+        n, c, h, w, k = ctx.shape
+        dxc = nhwc(dxc.float())
+        tg, ret = _grad_targets(ctx.param_refs)
+        dpre = ARENA.get("cond", n * c * 64 * 4, dxc.device)
+        _lib.call("mvae_condition_concat_bwd", dxc.data_ptr(), cond.data_ptr(), m.data_ptr(), _ptr(tg[0]),
+                  _ptr(tg[1]), dpre.data_ptr(), n, c, h, w, k, _stream(dxc))
+        _grad_done(*[p for p, r in zip(ctx.param_refs, ret) if r is None])
+        dx = dxc[:, :c] if ctx.x_grad else None
+        return (dx, None, *ret)
+
+
+def condition_concat(x, cond, weight, bias):
+    """(x_cond [B, 2C, H, W] channels_last, relu(condition_proj) [B, C*64])."""
+    return ConditionConcatFn.apply(x, cond, weight, bias)

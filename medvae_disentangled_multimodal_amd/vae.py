@@ -145,6 +145,10 @@ class ConditionalVAE(BaseVAE):
         return F.interpolate(cmap, size=(height, width), mode="bilinear", align_corners=False)
 
     def encode(self, x, condition):
+        if self.condition_method == "concat" and x.is_cuda:  # one fused conditioning op (csrc/condition.hip)
+            lin = self.condition_proj[0]
+            x_cond, _ = ops.condition_concat(x, condition, lin.weight, lin.bias)
+            return super().encode(x_cond)
         if self.condition_method == "concat":
             cmap = self.create_condition_map(condition.to(x.dtype), x.shape[2], x.shape[3])
             x_cond = torch.cat([x, cmap], dim=1).contiguous(memory_format=torch.channels_last)

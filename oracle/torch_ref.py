@@ -291,6 +291,77 @@ def condition_map(P, a: Arch, onehot, H, W):
     return F.interpolate(m, size=(H, W), mode="bilinear", align_corners=False)
 
 
+def _fma32(a, b, c):
+    """Correctly rounded float32 fma(a, b, c) in numpy: the float32 product is exact in float64, TwoSum gives the
+    exact error of the float64 sum, and a float64 sum lying exactly on a float32 rounding midpoint is resolved
+    by that error's sign (no double rounding)."""
+    import numpy as np
+    f32, f64 = np.float32, np.float64
+    a, b, c = (np.asarray(v, f32).astype(f64) for v in (a, b, c))
+    p = a * b
+    s = p + c
+    bb = s - p
+    e = (p - (s - bb)) + (c - bb)
+    r = s.astype(f32)
+    bits = np.ascontiguousarray(s).view(np.uint64)
+    tie = ((bits & np.uint64((1 << 29) - 1)) == np.uint64(1 << 28)) & (e != 0)
+    if np.any(tie):
+        lo = np.where(s.astype(f32).astype(f64) > s, np.nextafter(s.astype(f32), f32(-np.inf)), s.astype(f32))
+        hi = np.nextafter(lo, f32(np.inf))
+        r = np.where(tie, np.where(e > 0, hi, lo), r)
+    return r.astype(f32)
+
+
+def _lerp_exact(in_size: int, out_size: int):
+    """UpSample.h compute_source_index_and_lambda (align_corners=False) in float32, the source index taken with
+    one fma as torch's compiled CPU kernel does: src = fma(in/out, dst + 0.5, -0.5)."""
+    import numpy as np
+    f32 = np.float32
+    d = np.arange(out_size, dtype=f32)
+    if in_size == out_size:
+        i = np.arange(out_size)
+        return i, i, np.ones(out_size, f32), np.zeros(out_size, f32)
+    scale = f32(f32(in_size) / f32(out_size))
+    src = _fma32(np.full_like(d, scale), (d + f32(0.5)).astype(f32), np.full_like(d, f32(-0.5)))
+    src = np.where(src < 0, f32(0), src).astype(f32)
+    i0 = np.minimum(np.floor(src).astype(np.int64), in_size - 1)
+    l1 = np.clip((src - i0.astype(f32)).astype(f32), f32(0), f32(1)).astype(f32)
+    i1 = np.where(i0 < in_size - 1, i0 + 1, i0)
+    return i0, i1, (f32(1) - l1).astype(f32), l1
+
+
+def condition_map_exact(weight, bias, cond, channels: int, H: int, W: int):
+    """Bit-exact float32 restatement of ConditionalVAE.create_condition_map on the reference's CPU path
+    (src/models/conditional_vae.py:65-69 Linear + ReLU + Unflatten(C, 8, 8), :107-127 F.interpolate bilinear,
+    align_corners=False). Returns (projection [B, C*64] before the ReLU, map [B, C, H, W]) as numpy float32.
+    The projection is the fma chain over the condition entries plus the bias (exactly W[:, idx] + b for a one-hot
+    row, torch's addmm result); the interpolation is torch's CPU bilinear kernel for H + W <= 128 (the path it
+    takes for these sizes): corner weights w00 = hl0*wl0, ... and fma(w11, v11, fma(w10, v10, fma(w00, v00,
+    w01*v01))). Pinned bitwise against torch and the reference's own condition maps (tests/test_condition_cpu.py)."""
+    import numpy as np
+    f32 = np.float32
+    w = np.asarray(weight, f32)
+    b = np.asarray(bias, f32)
+    c = np.asarray(cond, f32)
+    B, K = c.shape
+    acc = np.zeros((B, w.shape[0]), f32)
+    for j in range(K):
+        acc = _fma32(np.broadcast_to(c[:, j:j + 1], acc.shape), np.broadcast_to(w[None, :, j], acc.shape), acc)
+    pre = (acc + b[None, :]).astype(f32)
+    m = np.where(np.isnan(pre), pre, np.maximum(pre, f32(0))).reshape(B, channels, 8, 8)
+    h0, h1, hl0, hl1 = _lerp_exact(8, H)
+    w0, w1, wl0, wl1 = _lerp_exact(8, W)
+    v00, v01 = m[:, :, h0][:, :, :, w0], m[:, :, h0][:, :, :, w1]
+    v10, v11 = m[:, :, h1][:, :, :, w0], m[:, :, h1][:, :, :, w1]
+    shp = v00.shape
+    w00 = np.broadcast_to((hl0[:, None] * wl0[None, :]).astype(f32), shp)
+    w01 = np.broadcast_to((hl0[:, None] * wl1[None, :]).astype(f32), shp)
+    w10 = np.broadcast_to((hl1[:, None] * wl0[None, :]).astype(f32), shp)
+    w11 = np.broadcast_to((hl1[:, None] * wl1[None, :]).astype(f32), shp)
+    out = _fma32(w11, v11, _fma32(w10, v10, _fma32(w00, v00, (w01 * v01).astype(f32))))
+    return pre, out
+
+
 def clamp_modality(idx: Tensor, n: int) -> Tensor:
     # disentangled_conditional_vae.py:142-146 and :258-265 (out-of-range -> last modality)
     return torch.where(idx >= n, torch.full_like(idx, n - 1), idx)
@@ -462,6 +533,16 @@ def train_step(P: Dict[str, Tensor], a: Arch, x, cond, eps, loss_cfg: dict, opt_
                                loss_cfg.get("separation_weight", 0.1),
                                loss_cfg.get("contrastive_weight", 0.05),
                                loss_cfg.get("recon_loss_type", "mse"))
+    elif loss_cfg.get("type") == "lpips_discriminator":
+        # LPIPSWithDiscriminator generator objective before discriminator_iter_start (vae_losses.py:274-323):
+        # perceptual_factor * LPIPS(x, rec).mean() + kl_factor * KL.sum() / B (closed-form KL)
+        W = loss_cfg["lpips_weights"]
+        lp = (lpips_vgg if loss_cfg.get("lpips_net", "alex") == "vgg" else lpips_alex)(W, x, out["reconstruction"])
+        mu, lv = out["mean"], out["logvar"]
+        kl = -0.5 * torch.sum(1 + lv - mu.pow(2) - lv.exp()) / x.shape[0]
+        p = lp.mean()
+        ld = {"loss": loss_cfg.get("perceptual_factor", 1.0) * p + loss_cfg.get("kl_factor", 1.0) * kl,
+              "p_loss": p, "kl_loss": kl}
     else:
         ld = vae_loss(out, x, loss_cfg.get("recon_weight", 1.0), loss_cfg.get("kl_weight", 1.0),
                       loss_cfg.get("recon_loss_type", "mse"))

@@ -124,6 +124,15 @@ def run_case(name, case):
         else:
             out = model(x, torch.from_numpy(ins["cond"]))
 
+    cond_rec = {}
+    if case["cond"] == "onehot":
+        # the one-hot conditioning path of ConditionalVAE.encode (src/models/conditional_vae.py:107-136), from
+        # the reference's own modules: the projection (Linear -> W[:, idx] + b for a one-hot row), its ReLU'd
+        # [C, 8, 8] map and the bilinear condition map at the image size
+        with torch.no_grad():
+            c = torch.from_numpy(ins["cond"])
+            cond_rec["out.cond_proj"] = model.condition_proj[0](c).numpy().copy()
+            cond_rec["out.cond_map"] = model.create_condition_map(c, ins["x"].shape[2], ins["x"].shape[3]).numpy().copy()
     lcfg = case["loss"]
     if lcfg["type"] == "vae":
         ld = vae_loss(lcfg, x, out)
@@ -172,6 +181,7 @@ def run_case(name, case):
 
     for k, v in ins.items():
         rec[f"in.{k}"] = v
+    rec.update(cond_rec)
     for k in ("reconstruction", "mean", "logvar", "z"):
         rec[f"out.{k}"] = out[k].detach().numpy().copy()
     for k in ("separation_loss", "contrastive_loss"):

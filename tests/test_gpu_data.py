@@ -109,3 +109,28 @@ def test_loader_sharding_and_epochs(dev):
         assert n == math.ceil(15 / 2)
         seen += dl.sampler.indices()
     assert sorted(set(seen)) == list(range(15))
+
+
+@pytest.mark.parametrize("size", [28, 64])
+def test_eval_batch_vs_reference_fixture(dev, size):
+    """The device pipeline against the vectors the reference's own __getitem__ + mixed_modality_collate_fn produced
+    (tests/golden/make_ref_fixtures.py), evaluation transform = Normalize(0.5, 0.5) applied to them in float32
+    (torchvision's `sub(mean).div(std)`; torchvision itself is unpinned): images bitwise, labels / one-hot / indices
+    exactly."""
+    from medvae_disentangled_multimodal_amd import data
+    ref = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_data.npz"),
+                       allow_pickle=False))
+    p = f"s{size}."
+    items = [str(s).split(":") for s in ref[p + "items"]]
+    names = list(dict.fromkeys(n for n, _ in items))
+    arrays = {n: (ref[f"{p}{n}.u8"], ref[f"{p}{n}.labels"]) for n in names}
+    ds = data.DeviceMedMNIST(names, "train", size, device=dev, arrays=arrays)
+    for b in ("mixed", "gray"):
+        sel = ref[f"{p}collate.{b}.select"].tolist()
+        x, labels, onehot, midx = ds.batch(sel)
+        want = torch.from_numpy(ref[f"{p}collate.{b}.x"]).sub(0.5).div(0.5)
+        assert x.shape == want.shape
+        assert torch.equal(x.cpu().contiguous(), want), b
+        assert labels.cpu().tolist() == ref[f"{p}collate.{b}.labels"].tolist()
+        assert torch.equal(onehot.cpu(), torch.from_numpy(ref[f"{p}collate.{b}.onehot"]))
+        assert midx.cpu().tolist() == ref[f"{p}collate.{b}.idx"].tolist()

@@ -49,3 +49,25 @@ def test_validation_step_logs(dev):
     for k in ("mse", "mae", "psnr", "ssim", "kl_total", "kl_mean", "kl_std", "kl_per_dim_mean", "loss"):
         assert f"val/{k}" in logs and torch.isfinite(torch.as_tensor(logs[f"val/{k}"])).all(), k
     assert model.training
+
+
+def test_kl_mse_mae_vs_reference_fixture(dev):
+    """Device metrics against the reference's own compute_kl_metrics / compute_reconstruction_metrics (MSE, MAE)
+    outputs (tests/golden/make_ref_fixtures.py); PSNR / SSIM stay pinned only to the torchmetrics restatement."""
+    import os
+    import numpy as np
+    from medvae_disentangled_multimodal_amd import metrics
+    ref = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_metrics.npz"),
+                       allow_pickle=False))
+    for tag in ("flat", "spatial"):
+        mu = torch.from_numpy(ref[f"kl.{tag}.mean"]).to(dev)
+        lv = torch.from_numpy(ref[f"kl.{tag}.logvar"]).to(dev)
+        if mu.dim() == 4:
+            mu, lv = mu.contiguous(memory_format=torch.channels_last), lv.contiguous(memory_format=torch.channels_last)
+        got = metrics.compute_kl_metrics(mu, lv)
+        for k in ("kl_total", "kl_mean", "kl_std", "kl_per_dim_mean"):
+            assert float(got[k]) == pytest.approx(float(ref[f"kl.{tag}.{k}"]), rel=1e-5), (tag, k)
+    cl = lambda t: torch.from_numpy(t).to(dev).contiguous(memory_format=torch.channels_last)
+    got = metrics.compute_reconstruction_metrics(cl(ref["recon.x"]), cl(ref["recon.rec"]))
+    assert float(got["mse"]) == pytest.approx(float(ref["recon.mse"]), rel=1e-5)
+    assert float(got["mae"]) == pytest.approx(float(ref["recon.mae"]), rel=1e-5)
