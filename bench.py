@@ -412,6 +412,12 @@ def parity_block(dev):
     x = torch.from_numpy(data["in.x"]).to(dev)
     batch = (x, torch.zeros(x.shape[0], 1, dtype=torch.long, device=dev), torch.from_numpy(data["in.cond"]).to(dev))
     eps = torch.from_numpy(data["in.eps"]).to(dev)
+    lin = model.condition_proj[0]
+    with torch.no_grad():  # the one-hot condition map, before the step updates condition_proj
+        from medvae_disentangled_multimodal_amd import ops
+        xc, _ = ops.condition_concat(x, batch[2], lin.weight, lin.bias)
+    cm = xc[:, x.shape[1]:].detach().cpu().numpy()
+    bitwise = bool(np.array_equal(cm.view(np.int32), data["out.cond_map"].view(np.int32)))
     mod.fit_step(batch, 0, eps=eps)
     torch.cuda.synchronize()
     out = mod._last_outputs
@@ -428,12 +434,6 @@ def parity_block(dev):
     has = [k for k, v in meta["param_has_grad"].items() if v]
     exact = math.sqrt(sum(float(data[f"gradsum.{k}"][1]) for k in has))
     errs["grad_global_norm_vs_exact"] = abs(float(mod.optimizer.last_total_norm) - exact) / exact
-    lin = model.condition_proj[0]
-    with torch.no_grad():
-        from medvae_disentangled_multimodal_amd import ops
-        xc, _ = ops.condition_concat(x, batch[2], lin.weight, lin.bias)
-    cm = xc[:, x.shape[1]:].detach().cpu().numpy()
-    bitwise = bool(np.array_equal(cm.view(np.int32), data["out.cond_map"].view(np.int32)))
     del mod, model
     torch.cuda.empty_cache()
     worst = max(errs.values())

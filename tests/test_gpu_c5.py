@@ -80,19 +80,43 @@ def test_bf16_conv_fwd_dgrad_wgrad_at_c5_shapes(dev, case):
     finally:
         ops.restore_math_mode(prev)
     assert ops._lib.query("mvae_get_math_mode") == 0
-    # float64 reference on the bf16-rounded operands of each GEMM (fwd: x, w; dgrad: dy, w; wgrad: dy, x)
+    # float64 reference on the bf16-rounded operands of each GEMM (fwd: x, w; dgrad: dy, w; wgrad: dy, x). The
+    # Upsample conv runs in sub-pixel form: its fwd / dgrad GEMM operands are the fp32 tap sums of each parity class
+    # (2x2 kernels), rounded to bf16 -- the reference does the same
     xr = bf(x).requires_grad_()
-    wr = bf(wt).requires_grad_()
-    xin = F.interpolate(xr, scale_factor=2.0, mode="nearest") if ups else xr
-    yr = F.conv2d(xin, wr, b.double(), padding=p)
+    if ups:
+        yr = _subpixel_conv(xr, wt, p) + b.double().view(1, -1, 1, 1)
+    else:
+        yr = F.conv2d(xr, bf(wt), b.double(), padding=p)
     assert rel(y, yr) < BF16_CONV_TOL
-    xg = bf(x).requires_grad_()
-    wg = bf(wt).requires_grad_()
+    yr.backward(bf(dy))
+    assert rel(xd.grad, xr.grad) < BF16_CONV_TOL
+    xg = bf(x)
+    wg = bf(wt).requires_grad_()  # wgrad: per-class products of bf16(dy) and bf16(x), taps combined in fp32
     xin = F.interpolate(xg, scale_factor=2.0, mode="nearest") if ups else xg
     F.conv2d(xin, wg, None, padding=p).backward(bf(dy))
-    assert rel(xd.grad, xg.grad) < BF16_CONV_TOL
     assert rel(wd.grad, wg.grad) < BF16_CONV_TOL
     assert rel(bd.grad, dy.double().sum((0, 2, 3))) < 1e-5
+
+
+def _subpixel_conv(x, w, pad):
+    """nearest-x2 upsample + 3x3 conv (pad 1) as 4 parity classes of 2x2 convs on the low-resolution input, with the
+    class kernels summed in fp32 and rounded to bf16 (the bf16 GEMM's operands). x: float64 (already bf16-valued)."""
+    assert pad == 1
+    n, _, h, wd = x.shape
+    co = w.shape[0]
+    # rows feeding output parity 0: source i-1 <- tap 0, source i <- taps 1 + 2; parity 1: i <- 0 + 1, i+1 <- 2
+    groups = {0: ((0,), (1, 2)), 1: ((0, 1), (2,))}
+    y = x.new_zeros(n, co, 2 * h, 2 * wd)
+    for ph in (0, 1):
+        for pw in (0, 1):
+            k = torch.zeros(co, w.shape[1], 2, 2)
+            for a, rs in enumerate(groups[ph]):
+                for c, ss in enumerate(groups[pw]):
+                    k[:, :, a, c] = sum(w[:, :, r, s] for r in rs for s in ss)
+            xp = F.pad(x, (1 - pw, pw, 1 - ph, ph))
+            y[:, :, ph::2, pw::2] = F.conv2d(xp, k.bfloat16().double())
+    return y
 
 
 def _conv_depth(model) -> int:

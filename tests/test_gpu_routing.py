@@ -129,5 +129,7 @@ def test_one_channel_batch_routing_kernel_matches_grouped_form(monkeypatch):
         mu_k, lv_k = model.encode(x, idx)
         monkeypatch.setattr(D, "ROUTING_KERNELS", False)
         mu_g, lv_g = model.encode(x, idx)
-    assert float((mu_k - mu_g).abs().max()) <= 1e-5 * float(mu_g.abs().max()) + 1e-7
-    assert float((lv_k - lv_g).abs().max()) <= 1e-5 * float(lv_g.abs().max()) + 1e-7
+    # same encoder input; the two forms differ only in how the 1x1 projector is evaluated (routing kernel fp32 vs
+    # the 3xBF16 conv), i.e. at the conv tolerance (2e-4) -- before the fix the colour samples differed by O(1)
+    assert float((mu_k - mu_g).norm() / mu_g.norm()) < 2e-4
+    assert float((lv_k - lv_g).norm() / lv_g.norm()) < 2e-4
