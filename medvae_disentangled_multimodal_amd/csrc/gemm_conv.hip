@@ -141,7 +141,8 @@ static int conv2d_impl(const float* x, const float* w, const float* bias, const 
   // samples per launch so that every operand fits one buffer descriptor
   const int chunk = (int)std::min<long long>(nb, MAX_DESC_BYTES / std::max(in_img, out_img));
   hipStream_t st = (hipStream_t)stream;
-  const bool v = (cin % 4 == 0) && al16(x) && al16(w);
+  // the vector gather keeps one bit per filter tap (LoadConvA): kernels of more than 32 taps take the scalar path
+  const bool v = (cin % 4 == 0) && al16(x) && al16(w) && kh * kw <= 32;
   if ((presplit || xsplit) && !v) {
     set_error("conv2d: pre-split operands need cin %% 4 == 0 and 16-B aligned x, w");
     return MVAE_EINVAL;

@@ -341,21 +341,34 @@ struct LoadRowK {
 };
 
 // ROW image, implicit im2col of an NHWC tensor: element (pixel m, k = (r*S+s)*Cx + c)
+// Vector path (VEC 4, every mode but MODE_UPS): the source pixel of row m through tap (r, s) is an affine function
+// base(m) + delta(r, s) in every gather mode -- MODE_FWD: (oh*stride + r - pad_t, ...); MODE_SUBPIX: (oh + r - pt,
+// ...); MODE_DGRAD (stride 2^q): ((oh + pad_t) >> q) - (r >> q) where (oh + pad_t - r) is a multiple of the stride.
+// So init() keeps per row one byte offset of base(m) and a bit mask of the taps whose source pixel exists (tap_src
+// evaluated once per tap), prep() turns the lane's k column into (tap bit, delta bytes) once per K-tile, and a slot
+// load is an AND, a compare, an add and a select -- instead of the per-slot tap decomposition, bounds checks and
+// multiplies of the scalar path.
 template <int ROWS, int VEC, int NT, int MODE, int PREC, bool PRESPLIT = false>
 struct LoadConvA {
   static constexpr bool COL = false;
+  static constexpr bool FAST = VEC == 4 && MODE != MODE_UPS;
   static constexpr int RP = NT / 8;
   static constexpr int NS = ROWS / RP;
-  static constexpr int NE = VEC == 4 ? 1 : 4;  // (c, r, s) decompositions per thread
+  static constexpr int NE = VEC == 4 ? 1 : 4;  // (c, r, s) decompositions per thread (scalar path)
   __amdgpu_buffer_rsrc_t rs;
   int kc, r0, k;
+  float4 v[NS];
+  int pt, pl;  // MODE_SUBPIX: padding of this batch entry's parity class
+  // vector path
+  unsigned rowbase[NS], vmask[NS];
+  unsigned tbit;
+  int delta;
+  // scalar path
   unsigned base[NS];
   int oh[NS], ow[NS];
   bool mv[NS];
   int cc[NE], rr[NE], ss[NE];
   bool kv[NE];
-  float4 v[NS];
-  int pt, pl;  // MODE_SUBPIX: padding of this batch entry's parity class
   __device__ void init(const GemmArgs& a, const float* x, int row0, int kb, int tid, int bidx) {
     rs = make_rsrc(x, a.a_bytes);
     kc = tid & 7; r0 = row_of_tid(tid); k = kb;
@@ -364,31 +377,80 @@ struct LoadConvA {
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const int m = row0 + r0 + RP * i;
-      mv[i] = m < a.M;
-      const int mm = mv[i] ? m : 0;
+      const bool valid = m < a.M;
+      const int mm = valid ? m : 0;
       const int b = mdiv(mm, a.mg_hw);
       const int rem = mm - b * (a.Ho * a.Wo);
-      oh[i] = mdiv(rem, a.mg_wo);
-      ow[i] = rem - oh[i] * a.Wo;
-      base[i] = (unsigned)b * (unsigned)(a.H * a.W);
+      const int h_ = mdiv(rem, a.mg_wo);
+      const int w_ = rem - h_ * a.Wo;
+      if constexpr (FAST) {
+        int bh, bw;
+        if constexpr (MODE == MODE_FWD) {
+          bh = h_ * a.stride;
+          bw = w_ * a.stride;
+        } else if constexpr (MODE == MODE_SUBPIX) {
+          bh = h_;
+          bw = w_;
+        } else {  // MODE_DGRAD
+          bh = (h_ + a.pad_t) >> a.stride_shift;
+          bw = (w_ + a.pad_l) >> a.stride_shift;
+        }
+        rowbase[i] = (((unsigned)b * (unsigned)a.H + (unsigned)bh) * (unsigned)a.W + (unsigned)bw) * (unsigned)a.Cx * 4u;
+        unsigned msk = 0;
+        for (int r = 0; r < a.R; ++r)
+          for (int s_ = 0; s_ < a.S; ++s_) {
+            int ih = 0, iw = 0;
+            if (tap_src<MODE>(a, pt, pl, h_, w_, r, s_, ih, iw)) msk |= 1u << (r * a.S + s_);
+          }
+        vmask[i] = valid ? msk : 0u;
+      } else {
+        mv[i] = valid;
+        oh[i] = h_;
+        ow[i] = w_;
+        base[i] = (unsigned)b * (unsigned)(a.H * a.W);
+      }
     }
   }
   // (c, r, s) of this thread's k columns, by exact multiply-shift division: branch-free, so the
   // steady-state loop stays one basic block
   __device__ void prep(const GemmArgs& a) {
     const int kp = kperm(a, k);
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      const int kk = kp + kc * 4 + e;
+    if constexpr (FAST) {
+      const int kk = kp + kc * 4;
       const int tap = mdiv(kk, a.mg_cx);
-      cc[e] = kk - tap * a.Cx;
-      rr[e] = mdiv(tap, a.mg_s);
-      ss[e] = tap - rr[e] * a.S;
-      kv[e] = kk < a.K;
+      const int c = kk - tap * a.Cx;
+      const int r = mdiv(tap, a.mg_s);
+      const int s_ = tap - r * a.S;
+      int dh, dw;
+      if constexpr (MODE == MODE_FWD) {
+        dh = r - a.pad_t;
+        dw = s_ - a.pad_l;
+      } else if constexpr (MODE == MODE_SUBPIX) {
+        dh = r - pt;
+        dw = s_ - pl;
+      } else {
+        dh = -(r >> a.stride_shift);
+        dw = -(s_ >> a.stride_shift);
+      }
+      delta = ((dh * a.W + dw) * a.Cx + c) * 4;
+      tbit = kk < a.K ? 1u << tap : 0u;
+    } else {
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const int kk = kp + kc * 4 + e;
+        const int tap = mdiv(kk, a.mg_cx);
+        cc[e] = kk - tap * a.Cx;
+        rr[e] = mdiv(tap, a.mg_s);
+        ss[e] = tap - rr[e] * a.S;
+        kv[e] = kk < a.K;
+      }
     }
   }
   __device__ void load_slot(const GemmArgs& a, int i) {
-    if (VEC == 4) {
+    if constexpr (FAST) {
+      const unsigned off = rowbase[i] + (unsigned)delta;
+      v[i] = bload4(rs, (vmask[i] & tbit) ? off : OOB);
+    } else if (VEC == 4) {
       int ih = 0, iw = 0;
       const bool tv = tap_src<MODE>(a, pt, pl, oh[i], ow[i], rr[0], ss[0], ih, iw);
       const bool ok = mv[i] & kv[0] & tv;
