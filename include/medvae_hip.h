@@ -346,6 +346,20 @@ int mvae_condition_concat_fwd(const float* x, const float* cond, const float* w,
 int mvae_condition_concat_bwd(const float* dxcond, const float* cond, const float* m, float* dw, float* dbias,
                               float* dpre, int nb, int c, int h, int wd, int K, void* stream);
 
+/* DisentangledConditionalVAE's batch-coupled latent losses (src/models/disentangled_conditional_vae.py:195-206
+ * partition_latent in NCHW flatten order, :305-349 modality_separation_loss over the sorted distinct ids,
+ * :351-386 contrastive_loss with temperature). z [nb][c][hw] logical (cl = 1: stored NHWC), partition = flat
+ * elements [off, off + d); idx [nb] int64. Forward: out[0] = separation, out[1] = contrastive, out[2] = rows with
+ * positives. Backward: gsep / gcon are device scalars (upstream gradients; a non-finite forward value drops its
+ * term), dz (zero-filled by the caller, same layout as z) receives the partition's gradient. nb <= 1024, d <= 16;
+ * workspace from the query, shared by the forward and its backward. */
+int mvae_latent_aux_fwd(const float* z, const long long* idx, int nb, int c, int hw, int cl, int off, int d,
+                        float temperature, float* out, float* workspace, size_t ws_bytes, void* stream);
+int mvae_latent_aux_bwd(const float* z, const long long* idx, int nb, int c, int hw, int cl, int off, int d,
+                        float temperature, const float* out, const float* gsep, const float* gcon, float* dz,
+                        float* workspace, size_t ws_bytes, void* stream);
+size_t mvae_latent_aux_workspace_bytes(int nb, int d);
+
 #ifdef __cplusplus
 }
 #endif

@@ -92,6 +92,9 @@ SIGNATURES = {
     "mvae_modality_route_in_workspace_bytes": (Z, [I, I]),
     "mvae_condition_concat_fwd": (I, [P, P, P, P, P, P, I, I, I, I, I, P]),
     "mvae_condition_concat_bwd": (I, [P, P, P, P, P, P, I, I, I, I, I, P]),
+    "mvae_latent_aux_fwd": (I, [P, P, I, I, I, I, I, I, F, P, P, Z, P]),
+    "mvae_latent_aux_bwd": (I, [P, P, I, I, I, I, I, I, F, P, P, P, P, P, Z, P]),
+    "mvae_latent_aux_workspace_bytes": (Z, [I, I]),
 }
 
 

@@ -314,12 +314,12 @@ struct LoadRowK {
     const unsigned base = ((unsigned)row * ld + (unsigned)kk) * 4u;
     const bool rv = row < rows;
     if (VEC == 4) {
-      v[i] = bload4(rs, (rv && kk < K) ? base : OOB);
+      v[i] = bload4(rs, (rv & (kk < K)) ? base : OOB);
     } else {
-      v[i].x = bload1(rs, (rv && kk + 0 < K) ? base : OOB);
-      v[i].y = bload1(rs, (rv && kk + 1 < K) ? base + 4 : OOB);
-      v[i].z = bload1(rs, (rv && kk + 2 < K) ? base + 8 : OOB);
-      v[i].w = bload1(rs, (rv && kk + 3 < K) ? base + 12 : OOB);
+      v[i].x = bload1(rs, (rv & (kk + 0 < K)) ? base : OOB);
+      v[i].y = bload1(rs, (rv & (kk + 1 < K)) ? base + 4 : OOB);
+      v[i].z = bload1(rs, (rv & (kk + 2 < K)) ? base + 8 : OOB);
+      v[i].w = bload1(rs, (rv & (kk + 3 < K)) ? base + 12 : OOB);
     }
   }
   __device__ void store_slot(__bf16* img, int i) {
@@ -509,15 +509,15 @@ struct LoadColK {
     const int col = row0 + c4 * 4;
     const int krow = kr + i * (NT / C4);
     const int kk = k + krow;
-    const bool kv = krow < BK && kk < K;
+    const bool kv = (krow < BK) & (kk < K);
     const unsigned base = ((unsigned)kk * ld + (unsigned)col) * 4u;
     if (VEC == 4) {
-      v[i] = bload4(rs, (kv && col < rows) ? base : OOB);
+      v[i] = bload4(rs, (kv & (col < rows)) ? base : OOB);
     } else {
-      v[i].x = bload1(rs, (kv && col + 0 < rows) ? base : OOB);
-      v[i].y = bload1(rs, (kv && col + 1 < rows) ? base + 4 : OOB);
-      v[i].z = bload1(rs, (kv && col + 2 < rows) ? base + 8 : OOB);
-      v[i].w = bload1(rs, (kv && col + 3 < rows) ? base + 12 : OOB);
+      v[i].x = bload1(rs, (kv & (col + 0 < rows)) ? base : OOB);
+      v[i].y = bload1(rs, (kv & (col + 1 < rows)) ? base + 4 : OOB);
+      v[i].z = bload1(rs, (kv & (col + 2 < rows)) ? base + 8 : OOB);
+      v[i].w = bload1(rs, (kv & (col + 3 < rows)) ? base + 12 : OOB);
     }
   }
   bool want_bs = true;  // A side: accumulate the row sums (conv bias gradient) -- wave-uniform
@@ -538,7 +538,9 @@ struct LoadColK {
       } else {
         st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
         if constexpr (IS_A) {
-          bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
+          if (want_bs) {
+            bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
+          }
         }
       }
     }
@@ -581,15 +583,15 @@ struct LoadColPix {
   __device__ void load_slot(const GemmArgs&, int i) {
     const int col = row0 + c4 * 4;
     const int krow = kr + i * (NT / C4);
-    const bool kv = krow < BK && k + krow < K;
+    const bool kv = (krow < BK) & (k + krow < K);
     const unsigned base = (pix[i] * ld + (unsigned)col) * 4u;
     if (VEC == 4) {
-      v[i] = bload4(rs, (kv && col < rows) ? base : OOB);
+      v[i] = bload4(rs, (kv & (col < rows)) ? base : OOB);
     } else {
-      v[i].x = bload1(rs, (kv && col + 0 < rows) ? base : OOB);
-      v[i].y = bload1(rs, (kv && col + 1 < rows) ? base + 4 : OOB);
-      v[i].z = bload1(rs, (kv && col + 2 < rows) ? base + 8 : OOB);
-      v[i].w = bload1(rs, (kv && col + 3 < rows) ? base + 12 : OOB);
+      v[i].x = bload1(rs, (kv & (col + 0 < rows)) ? base : OOB);
+      v[i].y = bload1(rs, (kv & (col + 1 < rows)) ? base + 4 : OOB);
+      v[i].z = bload1(rs, (kv & (col + 2 < rows)) ? base + 8 : OOB);
+      v[i].w = bload1(rs, (kv & (col + 3 < rows)) ? base + 12 : OOB);
     }
   }
   __device__ void store_slot(__bf16* img, int i) {
@@ -597,9 +599,12 @@ struct LoadColPix {
     const int krow = kr + i * (NT / C4);
     if (krow < BK) {
       st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
-      bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
+      if (want_bs) {
+        bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
+      }
     }
   }
+  bool want_bs = true;
   __device__ void advance() { k += BK; }
   __device__ void load(const GemmArgs& a) {
     prep(a);
@@ -614,9 +619,14 @@ struct LoadColPix {
 
 // COL image for the wgrad B operand: rows n' = (r*S+s)*Cx + c (filter element), k = output pixel.
 // element = X[b][src(oh,ow,r,s)][c], contiguous along c.
+// Vector path (VEC 4, MODE_FWD / MODE_SUBPIX): a lane's 4 columns are one tap (r, s) and 4 channels, fixed for the
+// launch, so init() keeps the lane's tap offset ((r*W + s)*Cx + c) * 4 and prep() reduces each k-row (pixel) to
+// wave-uniform values -- the byte offset of its shifted origin (oh*stride - pad, ow*stride - pad) and those two
+// coordinates; a slot load is then two adds and two unsigned compares for the bounds, one add for the address.
 template <int ROWS, int VEC, int NT, int MODE, int PREC, bool PRESPLIT = false>
 struct LoadWgradX {
   static constexpr bool COL = true;
+  static constexpr bool FAST = VEC == 4 && MODE != MODE_UPS;
   static constexpr int C4 = ROWS / 4;
   static constexpr int NS = (BK * C4 + NT - 1) / NT;
   __amdgpu_buffer_rsrc_t rs;
@@ -624,6 +634,10 @@ struct LoadWgradX {
   int cc[4], rr[4], ss[4];
   bool nv[4];
   int pb[NS], poh[NS], pow_[NS];  // pixel decomposition of this thread's k-rows (current tile)
+  // vector path: lane-fixed tap offset, per k-row origin (uniform when C4 % 64 == 0)
+  unsigned ldelta;
+  unsigned sbase[NS];
+  int sh[NS], sw[NS];
   float4 v[NS];
   int pt, pl;
   __device__ void init(const GemmArgs& a, const float* x, int row0, int kb, int tid, int bidx) {
@@ -640,6 +654,7 @@ struct LoadWgradX {
       rr[e] = tap / a.S;
       ss[e] = tap - rr[e] * a.S;
     }
+    if constexpr (FAST) ldelta = (unsigned)(((rr[0] * a.W + ss[0]) * a.Cx + cc[0]) * 4);
     // with 64 column groups the k-row is wave-uniform: keep the pixel walk in scalar registers
     krw = (C4 % 64 == 0) ? __builtin_amdgcn_readfirstlane(kr) : kr;
   }
@@ -651,13 +666,26 @@ struct LoadWgradX {
       const int rem = p - pb[i] * (a.Ho * a.Wo);
       poh[i] = mdiv(rem, a.mg_wo);
       pow_[i] = rem - poh[i] * a.Wo;
+      if constexpr (FAST) {
+        if constexpr (MODE == MODE_FWD) {
+          sh[i] = poh[i] * a.stride - a.pad_t;
+          sw[i] = pow_[i] * a.stride - a.pad_l;
+        } else {
+          sh[i] = poh[i] - pt;
+          sw[i] = pow_[i] - pl;
+        }
+        sbase[i] = (unsigned)((pb[i] * a.H + sh[i]) * a.W + sw[i]) * (unsigned)a.Cx * 4u;
+      }
     }
   }
   __device__ void load_slot(const GemmArgs& a, int i) {
     const unsigned img = (unsigned)(a.H * a.W);
     const int krow = kr + i * (NT / C4);
-    const bool kv = krow < BK && (k + krow < a.K);
-    if (VEC == 4) {
+    const bool kv = (krow < BK) & (k + krow < a.K);
+    if constexpr (FAST) {
+      const bool ok = kv & nv[0] & ((unsigned)(sh[i] + rr[0]) < (unsigned)a.H) & ((unsigned)(sw[i] + ss[0]) < (unsigned)a.W);
+      v[i] = bload4(rs, ok ? sbase[i] + ldelta : OOB);
+    } else if (VEC == 4) {
       int ih = 0, iw = 0;
       const bool tv = tap_src<MODE>(a, pt, pl, poh[i], pow_[i], rr[0], ss[0], ih, iw);
       const bool ok = kv & nv[0] & tv;
@@ -812,7 +840,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 
   LA la;
   LB lb;
-  if constexpr (AK == A_COLM_SPLIT) la.want_bs = a.bias_ws != nullptr && tn == 0;
+  // wgrad: only the first column of tiles publishes the bias gradient (row sums of dY^T): the others skip the sums
+  if constexpr (AK == A_COLM || AK == A_COLM_PIX || AK == A_COLM_SPLIT) la.want_bs = a.bias_ws != nullptr && tn == 0;
   la.init(a, a.A + bidx * a.sA, m0, kb, tid, bidx);
   lb.init(a, a.B + bidx * a.sB, n0, kb, tid, bidx);
 

@@ -230,8 +230,11 @@ class DisentangledConditionalVAE(BaseVAE):
         hint = 1 if x.shape[1] == 1 else max(self.modality_channels.values())
         rec = self._decode_routed(z, modality_indices, hint)
         # gated terms: a NaN/Inf value drops the term's gradient (DisentangledVAELoss replaces it by 0, :540-550)
-        sep = ops.finite_gated(lambda zz: self.modality_separation_loss(zz, modality_indices), z)
-        con = ops.finite_gated(lambda zz: self.contrastive_loss(zz, modality_indices), z)
+        if ops.latent_aux_fits(z, self.modality_latent_dim) and modality_indices.is_cuda:
+            sep, con = ops.latent_aux_losses(z, modality_indices, self.shared_latent_dim, self.modality_latent_dim)
+        else:
+            sep = ops.finite_gated(lambda zz: self.modality_separation_loss(zz, modality_indices), z)
+            con = ops.finite_gated(lambda zz: self.contrastive_loss(zz, modality_indices), z)
         std = torch.clamp(torch.exp(0.5 * logvar), min=1e-6, max=10.0)
         out = {"reconstruction": rec, "mean": mu, "logvar": logvar, "mu": mu, "z": z,
                "prior": _prior(mu, std), "posterior": _posterior(mu, logvar, std),

@@ -1387,3 +1387,52 @@ class ConditionConcatFn(torch.autograd.Function):
 def condition_concat(x, cond, weight, bias):
     """(x_cond [B, 2C, H, W] channels_last, relu(condition_proj) [B, C*64])."""
     return ConditionConcatFn.apply(x, cond, weight, bias)
+
+
+# ------------------------------------------------------------------------------------------
+# DisentangledConditionalVAE's batch-coupled latent losses (disentangled_conditional_vae.py:195-206 partition,
+# :305-349 separation, :351-386 contrastive) fused: two launches forward, two backward (csrc/latent.hip)
+# ------------------------------------------------------------------------------------------
+LATENT_MAX_B, LATENT_MAX_D = 1024, 16
+LATENT_FUSED = os.environ.get("MVAE_NO_LATENT_FUSED") is None
+
+
+def latent_aux_fits(z: torch.Tensor, d: int) -> bool:
+    return LATENT_FUSED and z.is_cuda and z.dim() == 4 and z.shape[0] <= LATENT_MAX_B and 0 < d <= LATENT_MAX_D and \
+        (z.is_contiguous(memory_format=CL) or z.is_contiguous())
+
+
+class LatentAuxFn(torch.autograd.Function):
+    """(separation, contrastive) of the modality partition z.view(B, -1)[:, off:off + d]; a non-finite value drops
+    that term's gradient on the device (the reference's NaN -> 0 replacement, :540-550)."""
+
+    @staticmethod
+    def forward(ctx, z, idx, off: int, d: int, temperature: float):
+        _check(z, "latent")
+        n, c, h, w = z.shape
+        cl = int(z.is_contiguous(memory_format=CL) and not z.is_contiguous())
+        idx = idx.to(device=z.device, dtype=torch.long).contiguous()
+        out = torch.empty(3, device=z.device, dtype=torch.float32)
+        nbytes = _lib.query("mvae_latent_aux_workspace_bytes", n, d)
+        ws = torch.empty(nbytes // 4, device=z.device, dtype=torch.float32)
+        _lib.call("mvae_latent_aux_fwd", z.data_ptr(), idx.data_ptr(), n, c, h * w, cl, off, d, float(temperature),
+                  out.data_ptr(), ws.data_ptr(), nbytes, _stream(z))
+        ctx.save_for_backward(z, idx, out, ws)
+        ctx.geo = (n, c, h * w, cl, off, d, float(temperature))
+        sep, con = out[0], out[1]
+        return sep, con
+
+    @staticmethod
+    def backward(ctx, gsep, gcon):
+        z, idx, out, ws = ctx.saved_tensors
+        n, c, hw, cl, off, d, t = ctx.geo
+        gsep = (gsep if gsep is not None else torch.zeros((), device=z.device)).float().contiguous()
+        gcon = (gcon if gcon is not None else torch.zeros((), device=z.device)).float().contiguous()
+        dz = torch.zeros_like(z)  # same memory format as z; the kernels write the partition's elements only
+        _lib.call("mvae_latent_aux_bwd", z.data_ptr(), idx.data_ptr(), n, c, hw, cl, off, d, t, out.data_ptr(),
+                  gsep.data_ptr(), gcon.data_ptr(), dz.data_ptr(), ws.data_ptr(), ws.numel() * 4, _stream(z))
+        return dz, None, None, None, None
+
+
+def latent_aux_losses(z, idx, off: int, d: int, temperature: float = 0.1):
+    return LatentAuxFn.apply(z, idx, off, d, temperature)

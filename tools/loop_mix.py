@@ -46,7 +46,7 @@ def main():
                         continue
                     tgt = a + 4 + off * 4
                     st = [n for n, (aa, _) in enumerate(ent) if aa == tgt]
-                    if not st or k - st[0] > 600:
+                    if not st or k - st[0] > 2000:
                         continue
                     loop = [x for _, x in ent[st[0]:k + 1]]
                     c = collections.Counter(x.split()[0] for x in loop)
