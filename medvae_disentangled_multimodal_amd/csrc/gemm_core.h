@@ -619,14 +619,15 @@ struct LoadColPix {
 
 // COL image for the wgrad B operand: rows n' = (r*S+s)*Cx + c (filter element), k = output pixel.
 // element = X[b][src(oh,ow,r,s)][c], contiguous along c.
-// Vector path (VEC 4, MODE_FWD / MODE_SUBPIX): a lane's 4 columns are one tap (r, s) and 4 channels, fixed for the
-// launch, so init() keeps the lane's tap offset ((r*W + s)*Cx + c) * 4 and prep() reduces each k-row (pixel) to
-// wave-uniform values -- the byte offset of its shifted origin (oh*stride - pad, ow*stride - pad) and those two
-// coordinates; a slot load is then two adds and two unsigned compares for the bounds, one add for the address.
+// Affine variant (FAST): a lane's 4 columns are one tap (r, s) and 4 channels, fixed for the launch, so init() keeps
+// the lane's tap offset ((r*W + s)*Cx + c) * 4 and prep() reduces each k-row (pixel) to wave-uniform values -- the
+// byte offset of its shifted origin (oh*stride - pad, ow*stride - pad) and those two coordinates.
 template <int ROWS, int VEC, int NT, int MODE, int PREC, bool PRESPLIT = false>
 struct LoadWgradX {
   static constexpr bool COL = true;
-  static constexpr bool FAST = VEC == 4 && MODE != MODE_UPS;
+  // (measured: the affine form moves index math from the VALU to the SALU here -- the k-rows are wave-uniform --
+  // and ran the c4 wgrad GEMMs 3 % slower; kept off)
+  static constexpr bool FAST = false;
   static constexpr int C4 = ROWS / 4;
   static constexpr int NS = (BK * C4 + NT - 1) / NT;
   __amdgpu_buffer_rsrc_t rs;

@@ -39,13 +39,21 @@ __device__ __forceinline__ long long lat_pos(const LatentArgs& a, int b, int j) 
   return (long long)b * a.C * a.HW + (a.cl ? (long long)p * a.C + c : (long long)c * a.HW + p);
 }
 
-// zn of every row into LDS (fp32 norm in index order, F.normalize eps 1e-12); returns nothing
+// zn of every row into LDS (fp32 norm in index order, F.normalize eps 1e-12)
 __device__ void lat_load_zn(const LatentArgs& a, float* zn, float* nrm) {
+  __shared__ int offs[LAT_MAXD];
+  if (threadIdx.x < a.D) {
+    const int f = a.off + threadIdx.x;
+    const int c = f / a.HW, p = f - c * a.HW;
+    offs[threadIdx.x] = a.cl ? p * a.C + c : c * a.HW + p;
+  }
+  __syncthreads();
+  const long long per = (long long)a.C * a.HW;
   for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
     float v[LAT_MAXD];
     float ss = 0.f;
     for (int j = 0; j < a.D; ++j) {
-      v[j] = a.z[lat_pos(a, b, j)];
+      v[j] = a.z[b * per + offs[j]];
       ss += v[j] * v[j];
     }
     const float n = fmaxf(sqrtf(ss), 1e-12f);
@@ -97,44 +105,81 @@ __global__ void __launch_bounds__(LAT_THREADS) latent_fwd_rows_kernel(LatentArgs
   }
 }
 
-// distinct ids in ascending order (torch.unique): fst[b] = no earlier sample has id_b; seg[b] = #distinct ids < id_b;
-// for the first sample of each id: cnt[seg] = its multiplicity, rep[seg] = that sample. O(B^2 / threads).
+// distinct ids in ascending order (torch.unique): fst[b] = no earlier sample has id_b (early exit: with few distinct
+// ids almost every sample finds its match within a few entries); the K first samples take their rank among the
+// distinct ids (O(B) each), every sample its segment by a scan of the K-entry sorted list, and each segment its
+// multiplicity. seg[b] = #distinct ids < id_b; cnt[s], rep[s] = multiplicity and first sample of segment s.
 __device__ void lat_segments(const LatentArgs& a, const long long* ids, int* fst, int* seg, int* cnt, int* rep,
                              int& K) {
+  __shared__ long long dist[LAT_MAXB];
   for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
-    bool first = true;
-    for (int j = 0; j < b; ++j) first &= ids[j] != ids[b];
+    const long long v = ids[b];
+    int first = 1;
+    for (int j = 0; j < b; ++j)
+      if (ids[j] == v) {
+        first = 0;
+        break;
+      }
     fst[b] = first;
   }
   __syncthreads();
   K = 0;
   for (int j = 0; j < a.B; ++j) K += fst[j];
   for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
-    int rnk = 0, c = 0;
-    for (int j = 0; j < a.B; ++j) {
-      rnk += fst[j] & (ids[j] < ids[b]);
-      c += ids[j] == ids[b];
+    if (!fst[b]) continue;
+    int rnk = 0;
+    for (int j = 0; j < a.B; ++j) rnk += fst[j] & (ids[j] < ids[b]);
+    dist[rnk] = ids[b];
+    rep[rnk] = b;
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
+    int lo = 0, hi = K - 1;  // binary search of id_b in the sorted distinct ids
+    const long long v = ids[b];
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (dist[mid] < v) lo = mid + 1;
+      else hi = mid;
     }
-    seg[b] = rnk;
-    if (fst[b]) {
-      cnt[rnk] = c;
-      rep[rnk] = b;
-    }
+    seg[b] = lo;
+  }
+  __syncthreads();
+  for (int s_ = threadIdx.x; s_ < K; s_ += blockDim.x) {
+    int c = 0;
+    for (int b = 0; b < a.B; ++b) c += seg[b] == s_;
+    cnt[s_] = c;
   }
   __syncthreads();
 }
 
-// centroid of segment s (samples of its id in index order), fp32 like torch's mean
-__device__ void lat_centroids(const LatentArgs& a, const long long* ids, const int* cnt, const int* rep, int K,
-                              float* cen) {
-  for (int s = threadIdx.x; s < K; s += blockDim.x) {
-    float acc[LAT_MAXD];
-    for (int j = 0; j < a.D; ++j) acc[j] = 0.f;
+// zm[b][j] of every sample into LDS (coalesced over the B*D elements; the NCHW offsets of the D partition elements
+// computed once)
+__device__ void lat_load_zm(const LatentArgs& a, float* zm) {
+  __shared__ int offs[LAT_MAXD];
+  if (threadIdx.x < a.D) {
+    const int f = a.off + threadIdx.x;
+    const int c = f / a.HW, p = f - c * a.HW;
+    offs[threadIdx.x] = a.cl ? p * a.C + c : c * a.HW + p;
+  }
+  __syncthreads();
+  const long long per = (long long)a.C * a.HW;
+  for (int e = threadIdx.x; e < a.B * a.D; e += blockDim.x) {
+    const int b = e / a.D, j = e - (e / a.D) * a.D;
+    zm[e] = a.z[b * per + offs[j]];
+  }
+  __syncthreads();
+}
+
+// centroid of segment s (its samples in index order), fp32 like torch's mean: one thread per (segment, dim)
+__device__ void lat_centroids(const LatentArgs& a, const long long* ids, const float* zm, const int* cnt,
+                              const int* rep, int K, float* cen) {
+  for (int e = threadIdx.x; e < K * a.D; e += blockDim.x) {
+    const int s = e / a.D, q = e - (e / a.D) * a.D;
     const long long id = ids[rep[s]];
+    float acc = 0.f;
     for (int b = 0; b < a.B; ++b)
-      if (ids[b] == id)
-        for (int j = 0; j < a.D; ++j) acc[j] += a.z[lat_pos(a, b, j)];
-    for (int j = 0; j < a.D; ++j) cen[s * a.D + j] = acc[j] / (float)cnt[s];
+      if (ids[b] == id) acc += zm[b * a.D + q];
+    cen[e] = acc / (float)cnt[s];
   }
   __syncthreads();
 }
@@ -154,12 +199,13 @@ __global__ void __launch_bounds__(1024) latent_fwd_final_kernel(LatentArgs a) {
   __shared__ long long ids[LAT_MAXB];
   __shared__ int fst[LAT_MAXB], seg[LAT_MAXB], cnt[LAT_MAXB], rep[LAT_MAXB];
   __shared__ float cen[LAT_MAXB * LAT_MAXD];
+  __shared__ float zm[LAT_MAXB * LAT_MAXD / 2];
   __shared__ double sh[16];
   for (int b = threadIdx.x; b < a.B; b += blockDim.x) ids[b] = a.idx[b];
-  __syncthreads();
+  lat_load_zm(a, zm);
   int K = 0;
   lat_segments(a, ids, fst, seg, cnt, rep, K);
-  lat_centroids(a, ids, cnt, rep, K, cen);
+  lat_centroids(a, ids, zm, cnt, rep, K, cen);
   // pairwise distances (i < j), summed in fp64
   double dsum = 0.0;
   const long long npair = (long long)K * (K - 1) / 2;
@@ -197,11 +243,12 @@ __global__ void __launch_bounds__(1024) latent_bwd_prep_kernel(LatentArgs a, con
   __shared__ long long ids[LAT_MAXB];
   __shared__ int fst[LAT_MAXB], seg[LAT_MAXB], cnt[LAT_MAXB], rep[LAT_MAXB];
   __shared__ float cen[LAT_MAXB * LAT_MAXD];
+  __shared__ float zm[LAT_MAXB * LAT_MAXD / 2];
   for (int b = threadIdx.x; b < a.B; b += blockDim.x) ids[b] = a.idx[b];
-  __syncthreads();
+  lat_load_zm(a, zm);
   int K = 0;
   lat_segments(a, ids, fst, seg, cnt, rep, K);
-  lat_centroids(a, ids, cnt, rep, K, cen);
+  lat_centroids(a, ids, zm, cnt, rep, K, cen);
   float* dzsep = a.ws + (long long)LAT_ROWW * a.B;
   float* A = dzsep + (long long)a.B * a.D;
   float* Bc = A + a.B;
@@ -209,6 +256,7 @@ __global__ void __launch_bounds__(1024) latent_bwd_prep_kernel(LatentArgs a, con
   const float gs = (K >= 2 && isfinite(sepv)) ? gsep[0] : 0.f;
   const float gc = (nvalid > 0.f && isfinite(conv_)) ? gcon[0] : 0.f;
   const float npair = (float)((long long)K * (K - 1) / 2);
+  if (threadIdx.x == 0) Bc[a.B] = gc != 0.f ? 1.f : 0.f;  // contrastive gradient live (read by the rows pass)
   // d(-mean dist)/dc_s = -(1/npair) sum_{t != s} (c_s - c_t) / |c_s - c_t|, then / cnt_s to every member
   for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
     const int s = seg[b];
@@ -257,9 +305,10 @@ __global__ void __launch_bounds__(LAT_THREADS) latent_bwd_rows_kernel(LatentArgs
   __syncthreads();
   const int r = threadIdx.x >> 4, l = threadIdx.x & 15;
   const int i = blockIdx.x * LAT_ROWS + r;
+  const bool live = Bc[a.B] != 0.f;  // a gated (non-finite) contrastive term contributes nothing, NaN latents included
   float g[LAT_MAXD];
   for (int q = 0; q < LAT_MAXD; ++q) g[q] = 0.f;
-  if (i < a.B) {
+  if (i < a.B && live) {
     const float* zi = zn + i * a.D;
     for (int j = l; j < a.B; j += 16) {
       if (j == i) continue;  // d tot / d e_ii = 0 (tot = sum - e_ii), and e_ii is never positive
@@ -281,7 +330,7 @@ __global__ void __launch_bounds__(LAT_THREADS) latent_bwd_rows_kernel(LatentArgs
     float dot = 0.f;
     for (int q = 0; q < a.D; ++q) dot += zi[q] * g[q];
     for (int q = 0; q < a.D; ++q) {
-      const float dx = n > 1e-12f ? (g[q] - zi[q] * dot) / n : g[q] / 1e-12f;
+      const float dx = !live ? 0.f : n > 1e-12f ? (g[q] - zi[q] * dot) / n : g[q] / 1e-12f;
       dz[lat_pos(a, i, q)] = dx + dzsep[i * a.D + q];
     }
   }
@@ -293,11 +342,12 @@ using namespace mvae;
 
 extern "C" {
 
-size_t mvae_latent_aux_workspace_bytes(int nb, int d) { return (size_t)nb * (LAT_ROWW + d + 2) * sizeof(float); }
+size_t mvae_latent_aux_workspace_bytes(int nb, int d) { return ((size_t)nb * (LAT_ROWW + d + 2) + 1) * sizeof(float); }
 
 static bool lat_args(LatentArgs& a, const float* z, const long long* idx, int nb, int c, int hw, int cl, int off,
                      int d, float temperature, float* out, float* ws, size_t ws_bytes, const char* who) {
-  if (!z || !idx || !out || !ws || nb <= 0 || nb > LAT_MAXB || d <= 0 || d > LAT_MAXD || c <= 0 || hw <= 0 ||
+  if (!z || !idx || !out || !ws || nb <= 0 || nb > LAT_MAXB || d <= 0 || d > LAT_MAXD || nb * d > LAT_MAXB * LAT_MAXD / 2 ||
+      c <= 0 || hw <= 0 ||
       off < 0 || off + d > c * hw || !(temperature > 0.f)) {
     set_error("%s: bad arguments (nb=%d d=%d; needs nb <= %d, d <= %d)", who, nb, d, LAT_MAXB, LAT_MAXD);
     return false;

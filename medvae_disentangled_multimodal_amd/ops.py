@@ -1399,6 +1399,7 @@ LATENT_FUSED = os.environ.get("MVAE_NO_LATENT_FUSED") is None
 
 def latent_aux_fits(z: torch.Tensor, d: int) -> bool:
     return LATENT_FUSED and z.is_cuda and z.dim() == 4 and z.shape[0] <= LATENT_MAX_B and 0 < d <= LATENT_MAX_D and \
+        z.shape[0] * d <= LATENT_MAX_B * LATENT_MAX_D // 2 and \
         (z.is_contiguous(memory_format=CL) or z.is_contiguous())
 
 
