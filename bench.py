@@ -166,7 +166,14 @@ def cpu_baseline(cfg, seconds_budget=20.0):
         if time.perf_counter() - t0 > seconds_budget / 2 or steps >= 3:
             break
     dt = (time.perf_counter() - t0) / steps
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return {"value": round(bs / dt, 4), "unit": "images/s", "cores": threads, "host_nproc": os.cpu_count(),
+            "cores_note": (f"torch intra-op threads = {threads} (OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}, "
+                           f"the GPU box's CPU share for one GPU); process CPU affinity {affinity} of "
+                           f"{os.cpu_count()} host CPUs"),
             "kind": "port",
             "sample": f"{steps} oracle training step(s) at batch {bs} of the same model (fp32, CPU), "
                       f"{dt:.2f} s/step"}

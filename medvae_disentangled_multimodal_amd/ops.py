@@ -268,7 +268,9 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
     sub = _subpixel_upsample(g)
     alg = ref * 4 / 9 if sub else ref
     st = _stream(x)
-    split = WEIGHT_SPLIT and _splits_ok() and c % 4 == 0 and _al16(x) and not g.pointwise
+    # (the vector gather keeps one validity bit per filter tap: kernels of more than 32 taps take the scalar path,
+    # which reads unsplit weights)
+    split = WEIGHT_SPLIT and _splits_ok() and c % 4 == 0 and _al16(x) and not g.pointwise and g.kh * g.kw <= 32
     if x_split and (g.pointwise or g.upsample or c % 4 or not _al16(x)):
         raise RuntimeError("conv2d: a pre-split input needs a non-pointwise, non-upsample conv with cin % 4 == 0")
     wg = w
@@ -342,7 +344,7 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None):
                       0, 0.0, dx.data_ptr(), c, 0, 1, None, None, 0, 0, None, 0, st)
         return dx
     # the dgrad GEMM's K runs over cout: transposed weights [cin][taps][cout], pre-split when cout % 4 == 0
-    split = WEIGHT_SPLIT and _splits_ok() and co % 4 == 0 and _al16(dy)
+    split = WEIGHT_SPLIT and _splits_ok() and co % 4 == 0 and _al16(dy) and g.kh * g.kw <= 32
     wflag = MVAE_CONV_WSPLIT if split else 0
     xflag = MVAE_CONV_XSPLIT if dys is not None else 0
     if g.upsample:
