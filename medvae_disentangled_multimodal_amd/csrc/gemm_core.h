@@ -856,122 +856,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 
   const int nt = ke > kb ? (ke - kb + BK - 1) / BK : 0;
   const int arow = wm * (BM / WGM), brow = wn * (BN / WGN);
-  // bf16 mode (PREC 1) on row images: the lo planes are free, so each stage carries TWO K-tiles (plane 0: k, plane 1:
-  // k + 32) -- twice the MFMAs per barrier and twice the time for the stage's global loads to land (the single-tile
-  // loop is latency-bound: 32 MFMAs per barrier). Loaders la2 / lb2 stage the odd K-tiles.
-  constexpr bool DUAL = PREC == 1 && !LA::COL && !LB::COL && KS == 1;
-  if constexpr (DUAL) {
-    LA la2;
-    LB lb2;
-    la2.init(a, a.A + bidx * a.sA, m0, kb + BK, tid, bidx);
-    lb2.init(a, a.B + bidx * a.sB, n0, kb + BK, tid, bidx);
-    const int nst = (nt + 1) / 2;
-    auto adv2 = [&]() {
-      la.advance(); la.advance(); lb.advance(); lb.advance();
-      la2.advance(); la2.advance(); lb2.advance(); lb2.advance();
-    };
-    auto compute2 = [&](const __bf16* Ai, bool second) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && !second) break;
-        const __bf16* Ah = Ai + h * IA::PLANE;
-        const __bf16* Bh = Ai + IA::SIZE + h * IB::PLANE;
-        bf16x8 bh[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bh[j] = read_frag<BN, false, MF>(Bh, brow + j * MF, 0, lane);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const bf16x8 ah = read_frag<BM, false, MF>(Ah, arow + i * MF, 0, lane);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(ah, bh[j], acc[i][j]);
-        }
-      }
-    };
-    // prologue: stage 0 -> LDS buffer 0 (both planes), stage 1 -> registers
-    if (nst > 0) {
-      la.load(a);
-      lb.load(a);
-      la2.load(a);
-      lb2.load(a);
-      la.store(lds);
-      lb.store(lds + IA::SIZE);
-      la2.store(lds + IA::PLANE);
-      lb2.store(lds + IA::SIZE + IB::PLANE);
-    }
-    if (nst > 1) {
-      adv2();
-      la.load(a);
-      lb.load(a);
-      la2.load(a);
-      lb2.load(a);
-    }
-    __syncthreads();
-    int s2 = 0;
-    constexpr int STEPS2 = 2 * TM;
-    constexpr int NSL1 = LA::NS + LB::NS, NSL2 = 2 * NSL1;
-#ifndef MVAE_NO_PRIO
-    if (NT >= 512 && wid >= (NT / 64) / 2) __builtin_amdgcn_s_setprio(1);
-#endif
-    for (; s2 + 2 < nst; ++s2) {
-      __bf16* nb = lds + ((s2 & 1) ^ 1) * BUF;
-      const __bf16* Ai = lds + (s2 & 1) * BUF;
-      adv2();
-      la.prep(a);
-      lb.prep(a);
-      la2.prep(a);
-      lb2.prep(a);
-      bf16x8 bh[TN], ah[2];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bh[j] = read_frag<BN, false, MF>(Ai + IA::SIZE, brow + j * MF, 0, lane);
-      ah[0] = read_frag<BM, false, MF>(Ai, arow, 0, lane);
-      auto stage = [&](int st) {
-#pragma unroll
-        for (int q = st * NSL2 / STEPS2; q < (st + 1) * NSL2 / STEPS2; ++q) {
-          const int q1 = q % NSL1;
-          const int pl = q / NSL1;  // 0: even K-tile -> plane 0, 1: odd K-tile -> plane 1
-          if (q1 < LA::NS) {
-            if (pl == 0) { la.store_slot(nb, q1); la.load_slot(a, q1); }
-            else { la2.store_slot(nb + IA::PLANE, q1); la2.load_slot(a, q1); }
-          } else {
-            if (pl == 0) { lb.store_slot(nb + IA::SIZE, q1 - LA::NS); lb.load_slot(a, q1 - LA::NS); }
-            else { lb2.store_slot(nb + IA::SIZE + IB::PLANE, q1 - LA::NS); lb2.load_slot(a, q1 - LA::NS); }
-          }
-        }
-      };
-#pragma unroll
-      for (int st = 0; st < STEPS2; ++st) {
-        const int i = st % TM, cur = st & 1;
-        if (st + 1 < STEPS2) {
-          const int h1 = (st + 1) / TM, i1 = (st + 1) % TM;
-          ah[cur ^ 1] = read_frag<BM, false, MF>(Ai + h1 * IA::PLANE, arow + i1 * MF, 0, lane);
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(ah[cur], bh[j], acc[i][j]);
-        if (st == TM - 1) {  // B fragments of the odd K-tile (plane 1)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            bh[j] = read_frag<BN, false, MF>(Ai + IA::SIZE + IB::PLANE, brow + j * MF, 0, lane);
-        }
-        stage(st);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      __syncthreads();
-    }
-#ifndef MVAE_NO_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
-    if (s2 + 1 < nst) {  // last staged stage: write it, nothing left to load (stage s2 is full: 2*s2 + 1 < nt)
-      __bf16* nb = lds + ((s2 & 1) ^ 1) * BUF;
-      la.store(nb);
-      lb.store(nb + IA::SIZE);
-      la2.store(nb + IA::PLANE);
-      lb2.store(nb + IA::SIZE + IB::PLANE);
-      compute2(lds + (s2 & 1) * BUF, true);
-      __syncthreads();
-      ++s2;
-    }
-    if (s2 < nst) compute2(lds + (s2 & 1) * BUF, 2 * s2 + 1 < nt);  // the odd K-tile only if it is in range
-  } else {
+  // (Measured and removed: in bf16 mode, two K-tiles per stage in the free lo planes -- twice the MFMAs per barrier
+  // and twice the load-latency budget -- ran the c5 fwd / dgrad GEMMs 3 % slower: the single-tile bf16 loop is not
+  // bound by the barrier count or the global-load latency.)
+  {
   // Prologue: tile 0 -> LDS buffer 0, tile 1 -> registers.
   if (nt > 0) {
     la.load(a);
@@ -1124,7 +1012,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
     ++t;
   }
   if (t < nt) compute(lds + (t & 1) * BUF);
-  }  // !DUAL
+  }
 
   // wgrad: the conv bias gradient (row sums of A = dY^T over this split's pixels) falls out of the
   // A staging for free; one column of tiles (tn == 0) publishes it, fixed-order reduction in LDS.

@@ -11,7 +11,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--shape", type=int, default=1)
 ap.add_argument("--pass_", default="fwd")
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--precision", default="32")
 a = ap.parse_args()
+ops.set_precision(a.precision)
 n, ci, co, h, k, s, pads, ups = SHAPES[a.shape]
 dev = torch.device("cuda:0")
 g = ops.ConvGeom(k, k, s, pads[0], pads[1], pads[2], pads[3], ups)

@@ -5,7 +5,7 @@ import collections, csv, glob, sys
 tot = collections.defaultdict(float)
 disp = set()
 for pat in sys.argv[1:]:
-    for f in glob.glob(pat):
+    for f in glob.glob(pat, recursive=True):
         for r in csv.DictReader(open(f)):
             tot[r["Counter_Name"]] += float(r["Counter_Value"])
             disp.add((f, r["Dispatch_Id"]))
