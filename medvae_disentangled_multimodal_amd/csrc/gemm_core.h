@@ -660,13 +660,34 @@ struct LoadWgradX {
     krw = (C4 % 64 == 0) ? __builtin_amdgcn_readfirstlane(kr) : kr;
   }
   __device__ void prep(const GemmArgs& a) {
+    // slot 0's pixel by division; the others step from it (pixels NT / C4 apart: usually the same or the next image
+    // row), so each K-tile costs one decomposition instead of NS -- the k-rows are wave-uniform, this is scalar work
+    // on every wave of the workgroup, and the wgrad loop is short of scalar issue (PMC: 16 % of wave cycles in the
+    // bf16 mode)
+    const int p0 = min(k + krw, a.K - 1);  // clamp: rows past K are masked
+    pb[0] = mdiv(p0, a.mg_hw);
+    {
+      const int rem = p0 - pb[0] * (a.Ho * a.Wo);
+      poh[0] = mdiv(rem, a.mg_wo);
+      pow_[0] = rem - poh[0] * a.Wo;
+    }
+#pragma unroll
+    for (int i = 1; i < NS; ++i) {
+      int w_ = pow_[i - 1] + NT / C4, h_ = poh[i - 1], b_ = pb[i - 1];
+      while (w_ >= a.Wo) {
+        w_ -= a.Wo;
+        ++h_;
+      }
+      while (h_ >= a.Ho) {
+        h_ -= a.Ho;
+        ++b_;
+      }
+      pb[i] = b_;  // (past K only for masked rows: any in-range decomposition will do)
+      poh[i] = h_;
+      pow_[i] = w_;
+    }
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
-      const int p = min(k + krw + i * (NT / C4), a.K - 1);  // clamp: rows past K are masked
-      pb[i] = mdiv(p, a.mg_hw);
-      const int rem = p - pb[i] * (a.Ho * a.Wo);
-      poh[i] = mdiv(rem, a.mg_wo);
-      pow_[i] = rem - poh[i] * a.Wo;
       if constexpr (FAST) {
         if constexpr (MODE == MODE_FWD) {
           sh[i] = poh[i] * a.stride - a.pad_t;

@@ -197,11 +197,12 @@ class DisentangledConditionalVAE(BaseVAE):
         cnt = oh.sum(0)
         present = cnt > 0
         cent = (oh.t() @ zm) / cnt.clamp_min(1.0)[:, None]
-        diff = cent[:, None, :] - cent[None, :, :]
-        sq = (diff * diff).sum(-1)
+        # direct-difference distances without a [B, B, D] tensor (torch.pdist's arithmetic; cdist's backward gives
+        # the zero-distance pairs of absent slots a zero gradient, and they are masked out anyway)
+        d = torch.cdist(cent[None], cent[None], compute_mode="donot_use_mm_for_euclid_dist")[0]
         iu = torch.triu(torch.ones(nb, nb, dtype=torch.bool, device=z.device), diagonal=1)
         pair = iu & present[:, None] & present[None, :]
-        dist = torch.where(pair, torch.where(pair, sq, torch.ones_like(sq)).sqrt(), torch.zeros_like(sq))
+        dist = torch.where(pair, d, torch.zeros_like(d))
         npair = pair.sum()
         loss = -dist.sum() / npair.clamp_min(1).to(zm.dtype)
         return torch.where(present.sum() >= 2, loss, torch.zeros_like(loss))
