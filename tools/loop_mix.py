@@ -59,6 +59,11 @@ def main():
                           f"ds_write {sum(v for kk, v in c.items() if kk.startswith('ds_write'))} "
                           f"vmem {sum(v for kk, v in c.items() if kk.startswith('buffer_'))} "
                           f"salu {sum(v for kk, v in c.items() if kk.startswith('s_'))}")
+                    if os.environ.get("LOOP_DUMP"):  # per-opcode histogram, or the whole loop with LOOP_DUMP=asm
+                        if os.environ["LOOP_DUMP"] == "asm":
+                            print("\n".join(loop))
+                        else:
+                            print("  " + ", ".join(f"{kk} {v}" for kk, v in c.most_common()))
                     break
 
 
