@@ -95,7 +95,7 @@ def _pmc_traffic(config):
     """HBM bytes per gemm3x_kernel launch from the committed PMC passes (tools/pmc_traffic.sh:
     FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc, separate passes) -- counters cannot be read inside
     this timed run, so the profile of the same command is attached (newest round first)."""
-    for tag in ("r02", "r01"):
+    for tag in ("r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", f"{tag}_{config}_gemm_traffic.json")
         if os.path.exists(path):
             break
