@@ -58,6 +58,11 @@ int mvae_set_dropout_salt(const void* salt_dev);
  * (mvae_split_bf16 of the conv's output gradient, done once for both backward GEMMs). */
 /* wgrad mode | MVAE_CONV_DYSPLIT: dy (the dY^T operand) is pre-split; the fused bias gradient sums hi + lo. */
 #define MVAE_CONV_DYSPLIT 64
+/* mode | MVAE_CONV_BF16 (modes 0 and 2, bf16 math mode only): the gathered operand (x, or dy for mode 2) and w are
+ * packed bf16 (mvae_pack_bf16 / the weight-prep entry points with split = 2; cin % 8 == 0): the GEMM stages them
+ * into LDS by DMA (no staging registers or conversion) in 64-deep K-tiles -- Lightning's bf16-mixed convolution
+ * (configs/config.yaml precision, main.py:86-99) with fp32 accumulation and fp32 output. */
+#define MVAE_CONV_BF16 128
 int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y,
                      int nb, int h, int w_, int cin, int cout, int kh, int kw, int stride, int pad_t,
                      int pad_l, int ho, int wo, int mode, void* stream);
@@ -122,7 +127,7 @@ size_t mvae_conv2d_wgrad_direct_workspace_bytes(int nb, int h, int w, int cin, i
  * (mvae_conv_weight_transpose), written interleaved into dx [nb][h][w_][cin] (h, w_ even): the useful
  * MACs only, vs mode 2's transposed gather where 3/4 of the taps hit stride holes.
  * workspace >= 4*kh*kw*cin*cout bytes (per-class weights). w_split flags: bit 0 = wt pre-split, bit 1 = dy
- * pre-split (mvae_split_bf16 layout; cout % 4 == 0). */
+ * pre-split (mvae_split_bf16 layout; cout % 4 == 0); w_split = 4: dy and wt packed bf16 (MVAE_CONV_BF16). */
 int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, int nb, int h, int w_, int cin,
                                    int cout, int kh, int kw, int pad_t, int pad_l, int ho, int wo, int w_split,
                                    float* workspace, size_t workspace_bytes, void* stream);
@@ -131,7 +136,8 @@ int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, 
  * output parity class (ph, pw) is a 2x2 conv of the low-resolution x [nb][h][w_][cin] with the tap-summed
  * weights w4 [4][cout][2][2][cin] (mvae_conv_weight_upsample_fwd), written interleaved into
  * y [nb][2h][2w_][cout] -- 4/9 of the reference's MACs, no upsampled intermediate. Same result as
- * mvae_conv2d_nhwc mode 1 up to fp32 summation order. */
+ * mvae_conv2d_nhwc mode 1 up to fp32 summation order. w_split = 1: w4 pre-split; 2: x and w4 packed bf16
+ * (MVAE_CONV_BF16). */
 int mvae_conv2d_upsample_nhwc(const float* x, const float* w4, const float* bias, const float* residual, float* y,
                               int nb, int h, int w_, int cin, int cout, int w_split, void* stream);
 int mvae_conv_weight_upsample_fwd(const float* w, float* w4, int cout, int cin, int split, void* stream);
@@ -146,6 +152,9 @@ size_t mvae_conv2d_wgrad_upsample_workspace_bytes(int nb, int h, int w_, int cin
  * hi = bf16(x) (round to nearest even), lo = bf16(x - hi). The weight-prep entry points below take
  * `split` to emit this layout directly (along their contiguous dimension, which must be % 4). */
 int mvae_split_bf16(const float* x, void* y, long long n, void* stream);
+/* Packed bf16 (round to nearest even) of n fp32 values (n % 8 == 0, 16-B aligned): the bf16-mixed mode's GEMM
+ * operands (MVAE_CONV_BF16). The weight-prep entry points take split = 2 to emit it directly. */
+int mvae_pack_bf16(const float* x, void* y, long long n, void* stream);
 
 /* Weight re-layouts for the input gradient: KRSC -> [cin][kh][kw][cout]; and the 4x4 tap-summed
  * kernel [cin][4][4][cout] for Upsample's conv (encoder_decoder.py:205-209). */

@@ -15,6 +15,17 @@ __global__ void __launch_bounds__(256) tap_select_kernel(const float* __restrict
     wc[e] = wt[((long long)ci * rs + tap) * cout + co];
   }
 }
+__global__ void __launch_bounds__(256) tap_select_bf16_kernel(const __bf16* __restrict__ wt, __bf16* __restrict__ wc,
+                                                              int cin, int rs, int cout, int nt, int4 taps) {
+  const long long tot = (long long)cin * nt * cout;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < tot; e += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(e % cout);
+    const long long r = e / cout;
+    const int t = (int)(r % nt), ci = (int)(r / nt);
+    const int tap = t == 0 ? taps.x : t == 1 ? taps.y : t == 2 ? taps.z : taps.w;
+    wc[e] = wt[((long long)ci * rs + tap) * cout + co];
+  }
+}
 
 static bool kperm_enabled() {  // MVAE_NO_KPERM=1: reference K order (A/B experiments)
   static const bool on = getenv("MVAE_NO_KPERM") == nullptr;
@@ -121,7 +132,13 @@ static int conv2d_impl(const float* x, const float* w, const float* bias, const 
                        size_t ws_bytes) {
   const bool presplit = (mode & MVAE_CONV_WSPLIT) != 0;
   const bool xsplit = (mode & MVAE_CONV_XSPLIT) != 0;
-  mode &= ~(MVAE_CONV_WSPLIT | MVAE_CONV_XSPLIT);
+  const bool bf = (mode & MVAE_CONV_BF16) != 0;
+  mode &= ~(MVAE_CONV_WSPLIT | MVAE_CONV_XSPLIT | MVAE_CONV_BF16);
+  if (bf && (presplit || xsplit || mode == 1 || cin % 8 || !al16(x) || !al16(w) || kh * kw > 32 || math_mode() != MATH_BF16)) {
+    set_error("conv2d: bf16-packed operands need the bf16 math mode, mode 0 or 2, cin %% 8 == 0, <= 32 taps, 16-B "
+              "aligned x, w");
+    return MVAE_EINVAL;
+  }
   if (xsplit && mode == 1) { set_error("conv2d: a pre-split input needs mode 0 or 2"); return MVAE_EINVAL; }
   if ((xsplit || presplit) && split_forbidden()) {
     set_error("conv2d: pre-split operands are not allowed in the exact-fp32 math mode");
@@ -153,15 +170,15 @@ static int conv2d_impl(const float* x, const float* w, const float* bias, const 
     const int n = std::min(chunk, nb - b0);
     GemmArgs a{};
     a.M = n * ho * wo; a.N = cout; a.K = kh * kw * cin; a.batch = 1; a.splits = 1; a.k_split = a.K;
-    a.A = x + (long long)b0 * (in_img / 4);
+    a.A = bf ? (const float*)((const __bf16*)x + (long long)b0 * (in_img / 4)) : x + (long long)b0 * (in_img / 4);
     a.B = w; a.ldb = a.K;
     a.C = y + (long long)b0 * (out_img / 4); a.ldc = cout; a.bias = bias;
     a.res = residual ? residual + (long long)b0 * (out_img / 4) : nullptr; a.ldr = cout;
     a.alpha = 1.f; a.beta = 0.f;
-    a.a_bytes = (unsigned)(in_img * n); a.b_bytes = (unsigned)wbytes;
+    a.a_bytes = (unsigned)(in_img * n / (bf ? 2 : 1)); a.b_bytes = (unsigned)(wbytes / (bf ? 2 : 1));
     a.c_bytes = (unsigned)(out_img * n); a.r_bytes = a.c_bytes;
     a.H = h; a.W = wd; a.Cx = cin; a.Ho = ho; a.Wo = wo; a.R = kh; a.S = kw;
-    a.perm_rs = (v && cin % BK == 0 && kh * kw > 1 && kperm_enabled()) ? kh * kw : 1;
+    a.perm_rs = (v && cin % (bf ? DBK : BK) == 0 && kh * kw > 1 && kperm_enabled()) ? kh * kw : 1;
     set_gather_magic(a);
     a.stride = stride; a.stride_shift = shift; a.pad_t = pad_t; a.pad_l = pad_l;
     a.gn_part = gn_part ? gn_part + (long long)b0 * (ho * wo / 32) * (cout / 4) * 2 : nullptr;
@@ -188,7 +205,10 @@ static int conv2d_impl(const float* x, const float* w, const float* bias, const 
       set_error("conv2d_gnstats: needs the vector (16-B) operand path");
       return MVAE_EINVAL;
     }
-    if (xsplit && mode == 2) {  // dy (the gathered operand of the input gradient) holds split4_bf16 groups
+    if (bf) {  // packed bf16 x (dy) and weights: LDS-DMA main loop
+      if (mode == 0) conv_dma(A_CONV_FWD, a, st, cfg);
+      else conv_dma(A_CONV_DGRAD, a, st, cfg);
+    } else if (xsplit && mode == 2) {  // dy (the gathered operand of the input gradient) holds split4_bf16 groups
       if (presplit) launch_big<A_CONV_DGRAD_SPLIT, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
       else launch_big<A_CONV_DGRAD_SPLIT, 4, B_ROWK, 4>(a, st, cfg);
     } else if (xsplit) {  // x (and w) hold split4_bf16 groups: no staging split at all
@@ -241,6 +261,12 @@ int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, 
   const int chunk = (int)std::min<long long>(nb, MAX_DESC_BYTES / std::max(in_img, out_img));
   hipStream_t st = (hipStream_t)stream;
   const int hc = h / 2, wc = wd / 2;
+  // w_split 4: dy and wt are packed bf16 (bf16-mixed mode, LDS-DMA main loop)
+  const bool bf = (w_split & 4) != 0;
+  if (bf && (w_split != 4 || cout % 8 || !al16(dy) || !al16(wt) || math_mode() != MATH_BF16)) {
+    set_error("dgrad_stride2: bf16-packed operands need the bf16 math mode, cout %% 8 == 0, aligned dy / wt");
+    return MVAE_EINVAL;
+  }
   float* wcls = workspace;
   bool empty_class = false;  // a kernel too small to reach every parity: those dx pixels are 0
   for (int p = 0; p < 2; ++p) {
@@ -265,8 +291,13 @@ int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, 
       for (int b = 0; b < ns; ++b) tp[a * ns + b] = rl[a] * kw + sl[b];
     if (nt > 4) { set_error("dgrad_stride2: class with more than 4 taps"); return MVAE_EINVAL; }
     const long long tot = (long long)cin * nt * cout;
-    hipLaunchKernelGGL(tap_select_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 8192)), dim3(256), 0,
-                       st, wt, wcls, cin, kh * kw, cout, nt, make_int4(tp[0], tp[1], tp[2], tp[3]));
+    if (bf)
+      hipLaunchKernelGGL(tap_select_bf16_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 8192)), dim3(256),
+                         0, st, (const __bf16*)wt, (__bf16*)wcls, cin, kh * kw, cout, nt,
+                         make_int4(tp[0], tp[1], tp[2], tp[3]));
+    else
+      hipLaunchKernelGGL(tap_select_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 8192)), dim3(256), 0,
+                         st, wt, wcls, cin, kh * kw, cout, nt, make_int4(tp[0], tp[1], tp[2], tp[3]));
     // dY row of class row m for tap a: m - pt + a with pt = (r_max - p - pad_t) / 2
     const int pt = (rl[0] - p - pad_t) / 2, pl = (sl[0] - q - pad_l) / 2;
     const bool v = (cout % 4 == 0) && al16(dy) && al16(wcls);
@@ -276,19 +307,20 @@ int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, 
       const int n = std::min(chunk, nb - b0);
       GemmArgs a{};
       a.M = n * hc * wc; a.N = cin; a.K = nt * cout; a.batch = 1; a.splits = 1; a.k_split = a.K;
-      a.A = dy + (long long)b0 * (in_img / 4);
+      a.A = bf ? (const float*)((const __bf16*)dy + (long long)b0 * (in_img / 4)) : dy + (long long)b0 * (in_img / 4);
       a.B = wcls; a.ldb = a.K;
       a.C = dx + (long long)b0 * (out_img / 4); a.ldc = cin;
       a.alpha = 1.f; a.beta = 0.f;
-      a.a_bytes = (unsigned)(in_img * n); a.b_bytes = (unsigned)(tot * 4);
+      a.a_bytes = (unsigned)(in_img * n / (bf ? 2 : 1)); a.b_bytes = (unsigned)(tot * (bf ? 2 : 4));
       a.c_bytes = (unsigned)(out_img * n); a.r_bytes = 0;
       a.H = ho; a.W = wo; a.Cx = cout; a.Ho = hc; a.Wo = wc; a.R = nr; a.S = ns;
-      a.perm_rs = (v && cout % BK == 0 && nt > 1 && kperm_enabled()) ? nt : 1;
+      a.perm_rs = (v && cout % (bf ? DBK : BK) == 0 && nt > 1 && kperm_enabled()) ? nt : 1;
       set_gather_magic(a);
       a.stride = 1; a.stride_shift = 0; a.pad_t = pt; a.pad_l = pl;
       a.sub_w2 = wd; a.sub_par = cls; a.out_remap = 1;
       const int cfg = choose_tile(a, v, false);
-      if ((w_split & 3) == 3) launch_big<A_CONV_FWD_SPLIT, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
+      if (bf) conv_dma(A_CONV_FWD, a, st, cfg);
+      else if ((w_split & 3) == 3) launch_big<A_CONV_FWD_SPLIT, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
       else if (w_split & 2) launch_big<A_CONV_FWD_SPLIT, 4, B_ROWK, 4>(a, st, cfg);
       else if (w_split) launch_big<A_CONV_FWD, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
       else if (v) launch_big<A_CONV_FWD, 4, B_ROWK, 4>(a, st, cfg);
@@ -296,7 +328,7 @@ int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, 
       const int rc = gemm_finish(a, st);
       if (rc) return rc;
     }
-    wcls += tot;
+    wcls = bf ? (float*)((__bf16*)wcls + tot) : wcls + tot;
   }
   return MVAE_OK;
 }
@@ -322,26 +354,34 @@ int mvae_conv2d_upsample_nhwc(const float* x, const float* w4, const float* bias
   const int chunk = (int)std::min<long long>(nb, MAX_DESC_BYTES / std::max(in_img, out_img));
   hipStream_t st = (hipStream_t)stream;
   const bool v = (cin % 4 == 0) && al16(x) && al16(w4);
+  // w_split 2: x and w4 are packed bf16 (bf16-mixed mode, LDS-DMA main loop)
+  const bool bf = w_split == 2;
+  if (bf && (cin % 8 || !v || math_mode() != MATH_BF16)) {
+    set_error("conv2d_upsample: bf16-packed operands need the bf16 math mode, cin %% 8 == 0, aligned x / w4");
+    return MVAE_EINVAL;
+  }
   if (w_split && !v) { set_error("conv2d_upsample: pre-split weights need cin %% 4 == 0"); return MVAE_EINVAL; }
   if (w_split && split_forbidden()) { set_error("conv2d_upsample: pre-split weights in exact-fp32 mode"); return MVAE_EINVAL; }
   for (int b0 = 0; b0 < nb; b0 += chunk) {
     const int n = std::min(chunk, nb - b0);
     GemmArgs a{};
     a.M = n * h * wd; a.N = cout; a.K = 4 * cin; a.batch = 4; a.splits = 1; a.k_split = a.K;
-    a.A = x + (long long)b0 * (in_img / 4); a.sA = 0;
+    a.A = bf ? (const float*)((const __bf16*)x + (long long)b0 * (in_img / 4)) : x + (long long)b0 * (in_img / 4);
+    a.sA = 0;
     a.B = w4; a.ldb = a.K; a.sB = (long long)cout * a.K;
     a.C = y + (long long)b0 * (out_img / 4); a.ldc = cout; a.sC = 0; a.bias = bias;
     a.res = residual ? residual + (long long)b0 * (out_img / 4) : nullptr; a.ldr = cout; a.sR = 0;
     a.alpha = 1.f; a.beta = 0.f;
-    a.a_bytes = (unsigned)(in_img * n); a.b_bytes = (unsigned)(wbytes / 4);
+    a.a_bytes = (unsigned)(in_img * n / (bf ? 2 : 1)); a.b_bytes = (unsigned)(wbytes / 4 / (bf ? 2 : 1));
     a.c_bytes = (unsigned)(out_img * n); a.r_bytes = a.c_bytes;
     a.H = h; a.W = wd; a.Cx = cin; a.Ho = h; a.Wo = wd; a.R = 2; a.S = 2;
-    a.perm_rs = (v && cin % BK == 0 && kperm_enabled()) ? 4 : 1;
+    a.perm_rs = (v && cin % (bf ? DBK : BK) == 0 && kperm_enabled()) ? 4 : 1;
     set_gather_magic(a);
     a.stride = 1; a.stride_shift = 0; a.pad_t = 1; a.pad_l = 1;
     a.sub_w2 = 2 * wd; a.sub_par = 0; a.out_remap = 1;
     const int cfg = choose_tile(a, v, false);
-    if (w_split) launch_big<A_CONV_SUBPIX, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
+    if (bf) conv_dma(A_CONV_SUBPIX, a, st, cfg);
+    else if (w_split) launch_big<A_CONV_SUBPIX, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
     else if (v) launch_big<A_CONV_SUBPIX, 4, B_ROWK, 4>(a, st, cfg);
     else launch_small<A_CONV_SUBPIX, 1, B_ROWK, 1>(a, st, cfg);
     const int rc = gemm_finish(a, st);

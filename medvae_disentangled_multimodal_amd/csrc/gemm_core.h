@@ -68,6 +68,7 @@ __device__ __forceinline__ int row_off(int r, int kc) { return r * 40 + (((kc >>
 constexpr int MVAE_CONV_WSPLIT = 16;  // conv mode flag: weights hold split4_bf16 groups
 constexpr int MVAE_CONV_XSPLIT = 32;  // conv mode flag: the input activation x holds split4_bf16 groups
 constexpr int MVAE_CONV_DYSPLIT = 64;  // wgrad mode flag: the output gradient dy holds split4_bf16 groups
+constexpr int MVAE_CONV_BF16 = 128;    // conv mode flag: the gathered operand and the weights are packed bf16 (PREC 4)
 
 // Exact division by a runtime constant d for 0 <= n < 2^31 (Granlund-Montgomery, N = 31):
 // q = (n * m) >> (31 + l), l = ceil(log2 d), m = floor(2^(31+l) / d) + 1 (< 2^32).
@@ -749,6 +750,274 @@ struct LoadWgradX {
   }
 };
 
+// ------------------------------------------------------------------------------------------
+// PREC 4: bf16 operands STORED as bf16 in HBM (the bf16-mixed mode's conv inputs, weights and output gradients are
+// packed by their producers), staged by LDS-DMA (buffer_load_dwordx4 ... lds): no staging registers, no VALU split,
+// no ds_write. K-tile DBK = 64; ROW images [ROWS][64] bf16 with 128-B rows, filled lane-linearly (one DMA
+// instruction = 1 KB = 8 rows, lane l -> row l/8, 16-B slot l%8) and swizzled on the SOURCE side: physical slot
+// p of row r holds the row's logical 8-element chunk p ^ dswz(r), and fragment reads apply the same involution
+// (ds_read_b128 lane groups {0-3,12-15,20-27}, ... then hit 16 distinct 16-B bank windows).
+// ------------------------------------------------------------------------------------------
+constexpr int DBK = 64;
+__device__ __forceinline__ int dswz(int r) { return (r >> 1) & 7; }
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// (permuted) K-tile starting at k (k % 64 == 0): channel chunk t / RS of tap t % RS, 64 channels wide
+__device__ __forceinline__ int kperm64(const GemmArgs& a, int k) {
+  const int t = k >> 6;
+  const int chunk = mdiv(t, a.mg_rs);
+  return (t - chunk * a.perm_rs) * a.Cx + chunk * DBK;
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, __bf16* dst, unsigned off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)dst, 16, off, 0, 0, 0);
+}
+
+// Piece q of a ROWS-row image (8 rows, 1 KB) is filled by wave (q % (NT/64)) as its instruction q / (NT/64); with
+// an even wave count the piece parity equals the wave parity, so a lane's logical chunk (slot ^ dswz(row)) is the
+// same for all its pieces.
+template <int ROWS, int NT>
+struct DmaShape {
+  static constexpr int NW = NT / 64;
+  static constexpr int NI = ROWS * 8 / NT;  // DMA instructions per thread per K-tile
+  static_assert(NI >= 1 && NI * NT == ROWS * 8 && NW % 2 == 0, "DMA image shape");
+};
+
+// ROW image of a row-major bf16 matrix: element (row, k) at P[row*ld + kperm(k)]
+template <int ROWS, int NT, bool IS_A>
+struct DmaRowK {
+  using S = DmaShape<ROWS, NT>;
+  __amdgpu_buffer_rsrc_t rs;
+  unsigned rowoff[S::NI];
+  bool rv[S::NI];
+  int cb, k, K, w;
+  unsigned kb2;
+  bool kv;
+  __device__ void init(const GemmArgs& a, const __bf16* p, int row0, int kb, int tid, int) {
+    rs = make_rsrc(p, IS_A ? a.a_bytes : a.b_bytes);
+    const int lane = tid & 63;
+    w = tid >> 6;
+    cb = (lane & 7) ^ (((lane >> 4) & 3) | ((w & 1) << 2));
+    const unsigned ld = (unsigned)(IS_A ? a.lda : a.ldb);
+    const int rows = IS_A ? a.M : a.N;
+    K = a.K; k = kb;
+#pragma unroll
+    for (int i = 0; i < S::NI; ++i) {
+      const int row = row0 + (i * S::NW + w) * 8 + (lane >> 3);
+      rv[i] = row < rows;
+      rowoff[i] = (unsigned)row * ld * 2u;
+    }
+  }
+  __device__ void prep(const GemmArgs& a) {
+    const int kk = kperm64(a, k) + cb * 8;
+    kv = kk < K;
+    kb2 = (unsigned)kk * 2u;
+  }
+  __device__ void issue(const GemmArgs&, __bf16* img, int i) {
+    dma16(rs, img + (i * S::NW + w) * 512, (rv[i] & kv) ? rowoff[i] + kb2 : OOB);
+  }
+  __device__ void advance() { k += DBK; }
+};
+
+// ROW image of the implicit im2col of a bf16 NHWC tensor (affine gather of LoadConvA's vector path, in bf16
+// bytes); needs Cx % 8 == 0 (a 16-B chunk never straddles two taps) and <= 32 taps
+template <int ROWS, int NT, int MODE>
+struct DmaConvA {
+  using S = DmaShape<ROWS, NT>;
+  __amdgpu_buffer_rsrc_t rs;
+  unsigned rowbase[S::NI], vmask[S::NI];
+  unsigned tbit;
+  int delta;
+  int cb, k, w, pt, pl;
+  __device__ void init(const GemmArgs& a, const __bf16* x, int row0, int kb, int tid, int bidx) {
+    rs = make_rsrc(x, a.a_bytes);
+    const int lane = tid & 63;
+    w = tid >> 6;
+    cb = (lane & 7) ^ (((lane >> 4) & 3) | ((w & 1) << 2));
+    k = kb;
+    pt = a.pad_t - ((bidx + a.sub_par) >> 1);
+    pl = a.pad_l - ((bidx + a.sub_par) & 1);
+#pragma unroll
+    for (int i = 0; i < S::NI; ++i) {
+      const int m = row0 + (i * S::NW + w) * 8 + (lane >> 3);
+      const bool valid = m < a.M;
+      const int mm = valid ? m : 0;
+      const int b = mdiv(mm, a.mg_hw);
+      const int rem = mm - b * (a.Ho * a.Wo);
+      const int h_ = mdiv(rem, a.mg_wo);
+      const int w_ = rem - h_ * a.Wo;
+      int bh, bw;
+      if constexpr (MODE == MODE_FWD) {
+        bh = h_ * a.stride;
+        bw = w_ * a.stride;
+      } else if constexpr (MODE == MODE_SUBPIX) {
+        bh = h_;
+        bw = w_;
+      } else {  // MODE_DGRAD
+        bh = (h_ + a.pad_t) >> a.stride_shift;
+        bw = (w_ + a.pad_l) >> a.stride_shift;
+      }
+      rowbase[i] = (((unsigned)b * (unsigned)a.H + (unsigned)bh) * (unsigned)a.W + (unsigned)bw) * (unsigned)a.Cx * 2u;
+      unsigned msk = 0;
+      for (int r = 0; r < a.R; ++r)
+        for (int s_ = 0; s_ < a.S; ++s_) {
+          int ih = 0, iw = 0;
+          if (tap_src<MODE>(a, pt, pl, h_, w_, r, s_, ih, iw)) msk |= 1u << (r * a.S + s_);
+        }
+      vmask[i] = valid ? msk : 0u;
+    }
+  }
+  __device__ void prep(const GemmArgs& a) {
+    const int kk = kperm64(a, k) + cb * 8;
+    const int tap = mdiv(kk, a.mg_cx);
+    const int c = kk - tap * a.Cx;
+    const int r = mdiv(tap, a.mg_s);
+    const int s_ = tap - r * a.S;
+    int dh, dw;
+    if constexpr (MODE == MODE_FWD) {
+      dh = r - a.pad_t;
+      dw = s_ - a.pad_l;
+    } else if constexpr (MODE == MODE_SUBPIX) {
+      dh = r - pt;
+      dw = s_ - pl;
+    } else {
+      dh = -(r >> a.stride_shift);
+      dw = -(s_ >> a.stride_shift);
+    }
+    delta = ((dh * a.W + dw) * a.Cx + c) * 2;
+    tbit = kk < a.K ? 1u << tap : 0u;
+  }
+  __device__ void issue(const GemmArgs&, __bf16* img, int i) {
+    dma16(rs, img + (i * S::NW + w) * 512, (vmask[i] & tbit) ? rowbase[i] + (unsigned)delta : OOB);
+  }
+  __device__ void advance() { k += DBK; }
+};
+
+// COL images (weight gradient: K = pixels, both operands contiguous along their rows): [64 k-rows][ROWS] bf16, k-row
+// pitch ROWS, element (kr, col) at kr * ROWS + (col ^ dcswz(kr)). The 32x32x16 transpose reads (ds_read_b64_tr_b16)
+// of a lane group touch 4 consecutive k-rows x 32 columns: the XOR moves the 4 k-rows' 64-B runs into the 4 quarters
+// of a 256-B bank row (conflict-free for ROWS >= 128; 2-way at ROWS 64). One DMA instruction fills KPI k-rows; a
+// lane's 16-B slot holds the logical chunk slot ^ (dcswz(kr) / 8), the same chunk in every instruction of the lane.
+template <int ROWS>
+__device__ __forceinline__ int dcswz(int kr) {
+  return ROWS >= 128 ? (kr & 3) << 5 : (kr & 1) << 5;
+}
+template <int ROWS, int NT>
+struct DmaColShape {
+  static constexpr int CPR = ROWS / 8;  // 16-B chunks per k-row
+  static constexpr int KPI = 64 / CPR;  // k-rows per DMA instruction
+  static constexpr int NW = NT / 64;
+  static constexpr int NI = ROWS * 8 / NT;  // DMA instructions per thread per K-tile
+  static_assert(ROWS >= 64 && NI >= 1 && NI * NT == ROWS * 8, "DMA COL image shape");
+};
+
+// A = dY^T: element (m, k) at P[k * lda + m]
+template <int ROWS, int NT>
+struct DmaColK {
+  using S = DmaColShape<ROWS, NT>;
+  __amdgpu_buffer_rsrc_t rs;
+  unsigned colb, ld2;
+  bool cv;
+  int kr0, k, K, w;
+  __device__ void init(const GemmArgs& a, const __bf16* p, int row0, int kb, int tid, int) {
+    rs = make_rsrc(p, a.a_bytes);
+    const int lane = tid & 63;
+    w = tid >> 6;
+    kr0 = w * S::KPI + lane / S::CPR;
+    const int lc = (lane % S::CPR) ^ (dcswz<ROWS>(kr0) >> 3);
+    const int col = row0 + lc * 8;
+    cv = col < a.M;
+    colb = (unsigned)col * 2u;
+    ld2 = (unsigned)a.lda * 2u;
+    k = kb; K = a.K;
+  }
+  __device__ void prep(const GemmArgs&) {}
+  __device__ void issue(const GemmArgs&, __bf16* img, int i) {
+    const int kk = k + kr0 + i * S::NW * S::KPI;
+    dma16(rs, img + (i * S::NW + w) * 512, (cv & (kk < K)) ? (unsigned)kk * ld2 + colb : OOB);
+  }
+  __device__ void advance() { k += DBK; }
+};
+
+// B = im2col of the bf16 NHWC input X: element (n = (r*S+s)*Cx + c, k = output pixel) = X[b][src(oh, ow, r, s)][c]
+template <int ROWS, int NT, int MODE>
+struct DmaWgradX {
+  using S = DmaColShape<ROWS, NT>;
+  __amdgpu_buffer_rsrc_t rs;
+  int kr0, k, K, w;
+  int rr, ss, pt, pl;
+  unsigned cb;
+  bool nv;
+  __device__ void init(const GemmArgs& a, const __bf16* x, int row0, int kb, int tid, int bidx) {
+    rs = make_rsrc(x, a.b_bytes);
+    const int lane = tid & 63;
+    w = tid >> 6;
+    kr0 = w * S::KPI + lane / S::CPR;
+    const int lc = (lane % S::CPR) ^ (dcswz<ROWS>(kr0) >> 3);
+    const int n = row0 + lc * 8;
+    nv = n < a.N;
+    const int nn = nv ? n : 0;
+    const int tap = nn / a.Cx;
+    cb = (unsigned)(nn - tap * a.Cx) * 2u;
+    rr = tap / a.S;
+    ss = tap - rr * a.S;
+    pt = a.pad_t - ((bidx + a.sub_par) >> 1);
+    pl = a.pad_l - ((bidx + a.sub_par) & 1);
+    k = kb; K = a.K;
+  }
+  __device__ void prep(const GemmArgs&) {}
+  __device__ void issue(const GemmArgs& a, __bf16* img, int i) {
+    const int kk = k + kr0 + i * S::NW * S::KPI;
+    const int p = min(kk, K - 1);
+    const int b = mdiv(p, a.mg_hw);
+    const int rem = p - b * (a.Ho * a.Wo);
+    const int oh = mdiv(rem, a.mg_wo);
+    const int ow = rem - oh * a.Wo;
+    int ih = 0, iw = 0;
+    const bool ok = nv & (kk < K) & tap_src<MODE>(a, pt, pl, oh, ow, rr, ss, ih, iw);
+    const unsigned off = (((unsigned)b * (unsigned)a.H + (unsigned)ih) * (unsigned)a.W + (unsigned)iw) * (unsigned)a.Cx * 2u + cb;
+    dma16(rs, img + (i * S::NW + w) * 512, ok ? off : OOB);
+  }
+  __device__ void advance() { k += DBK; }
+};
+
+// 32x32x16 fragment (k-step ks of 16) from a DMA COL image: two transpose reads, k-rows kr and kr + 4
+template <int ROWS>
+__device__ __forceinline__ bf16x8 dcfrag(const __bf16* img, int row0, int ks, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  const int kr = ks * 16 + (g >> 1) * 8 + (li >> 2);
+  const int col = row0 + (g & 1) * 16 + 4 * (li & 3);
+  const __bf16* p = img + kr * ROWS + (col ^ dcswz<ROWS>(kr));
+  const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)p);
+  const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(p + 4 * ROWS));
+  return __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int KIND, int ROWS, int NT, bool IS_A>
+struct DmaLoader;
+template <int ROWS, int NT, bool IS_A>
+struct DmaLoader<0, ROWS, NT, IS_A> : DmaRowK<ROWS, NT, IS_A> {};
+template <int ROWS, int NT>
+struct DmaLoader<A_CONV_FWD, ROWS, NT, true> : DmaConvA<ROWS, NT, MODE_FWD> {};
+template <int ROWS, int NT>
+struct DmaLoader<A_CONV_DGRAD, ROWS, NT, true> : DmaConvA<ROWS, NT, MODE_DGRAD> {};
+template <int ROWS, int NT>
+struct DmaLoader<A_CONV_SUBPIX, ROWS, NT, true> : DmaConvA<ROWS, NT, MODE_SUBPIX> {};
+template <int ROWS, int NT>
+struct DmaLoader<A_COLM, ROWS, NT, true> : DmaColK<ROWS, NT> {};
+// B operands (IS_A false): weights (ROW) and the weight gradient's im2col gathers (COL)
+template <int ROWS, int NT>
+struct DmaLoader<B_WGRAD_FWD, ROWS, NT, false> : DmaWgradX<ROWS, NT, MODE_FWD> {};
+template <int ROWS, int NT>
+struct DmaLoader<B_WGRAD_SUBPIX, ROWS, NT, false> : DmaWgradX<ROWS, NT, MODE_SUBPIX> {};
+
+// 16x16x32 fragment (8 consecutive k of one row) of k-step ks from a DMA ROW image
+__device__ __forceinline__ bf16x8 dfrag(const __bf16* img, int row0, int ks, int lane) {
+  const int r = row0 + (lane & 15);
+  const int c = 4 * ks + (lane >> 4);
+  return *(const bf16x8*)(img + r * DBK + ((c ^ dswz(r)) << 3));
+}
+
 // one MFMA product step: 3xBF16 (lo*hi + hi*lo + hi*hi, small terms first) or plain bf16
 __device__ __forceinline__ f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -830,13 +1099,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int MF = mf_of(AK), KS = ks_of<MF>(), NR = nr_of<MF>();
   using acc_t = acc_of<MF>;
-  using LA = Loader<AK, BM, VA, NT, true, PREC>;
-  using LB = Loader<BKIND, BN, VB, NT, false, PREC>;
+  constexpr int LP = PREC == 4 ? 1 : PREC;  // arithmetic of the register-staged loaders
+  using LA = Loader<AK, BM, VA, NT, true, LP>;
+  using LB = Loader<BKIND, BN, VB, NT, false, LP>;
   using IA = Img<BM, LA::COL>;
   using IB = Img<BN, LB::COL>;
   constexpr int BUF = IA::SIZE + IB::SIZE;
+  constexpr int DBUF = (BM + BN) * DBK;  // PREC 4: one stage of the A and B DMA images
   constexpr int TM = BM / WGM / MF, TN = BN / WGN / MF;  // MFMA tiles per wave
-  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * BUF];
+  __shared__ __attribute__((aligned(16))) __bf16 lds[(PREC == 4 && DBUF > BUF) ? 2 * DBUF : 2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WGN, wn = wid - wm * WGN;
@@ -860,13 +1131,6 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   const int kb = split * a.k_split;
   const int ke = min(a.K, kb + a.k_split);
 
-  LA la;
-  LB lb;
-  // wgrad: only the first column of tiles publishes the bias gradient (row sums of dY^T): the others skip the sums
-  if constexpr (AK == A_COLM || AK == A_COLM_PIX || AK == A_COLM_SPLIT) la.want_bs = a.bias_ws != nullptr && tn == 0;
-  la.init(a, a.A + bidx * a.sA, m0, kb, tid, bidx);
-  lb.init(a, a.B + bidx * a.sB, n0, kb, tid, bidx);
-
   acc_t acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -874,9 +1138,75 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
+  const int arow = wm * (BM / WGM), brow = wn * (BN / WGN);
+
+  if constexpr (PREC == 4) {
+    // LDS-DMA main loop over 64-deep K-tiles, two stages: at the top of iteration t each wave waits for its own
+    // DMA of tile t (vmcnt 0), the barrier makes every wave's DMA of tile t visible and guarantees that every wave
+    // has finished reading stage (t+1)&1 (tile t-1; its fragment reads were all consumed by tile t-1's MFMAs), then
+    // the DMA of tile t+1 is issued into that stage and tile t is multiplied: the DMA has one compute phase to land.
+    // Only LDS-DMA loads are in flight in the loop (no VGPR-destination load the compiler would drain with them).
+    // ROW images (fwd / dgrad) feed 16x16x32 MFMAs, COL images (weight gradient) 32x32x16 MFMAs.
+    constexpr bool ACOL = AK == A_COLM, BCOL = BKIND == B_WGRAD_FWD || BKIND == B_WGRAD_SUBPIX;
+    static_assert(ACOL == BCOL && MF == (ACOL ? 32 : 16), "DMA main loop: ROW x ROW (MF 16) or COL x COL (MF 32)");
+    using DA = DmaLoader<AK == A_ROWK ? 0 : AK, BM, NT, true>;
+    using DB = DmaLoader<BKIND == B_ROWK ? 0 : BKIND, BN, NT, false>;
+    DA da;
+    DB db;
+    da.init(a, (const __bf16*)a.A + bidx * a.sA, m0, kb, tid, bidx);
+    db.init(a, (const __bf16*)a.B + bidx * a.sB, n0, kb, tid, bidx);
+    const int nt = ke > kb ? (ke - kb + DBK - 1) / DBK : 0;
+    auto issue = [&](__bf16* stage) {
+      da.prep(a);
+      db.prep(a);
+#pragma unroll
+      for (int i = 0; i < DA::S::NI; ++i) da.issue(a, stage, i);
+#pragma unroll
+      for (int i = 0; i < DB::S::NI; ++i) db.issue(a, stage + BM * DBK, i);
+    };
+    auto frag_a = [&](const __bf16* img, int row0, int ks) {
+      if constexpr (ACOL) return dcfrag<BM>(img, row0, ks, lane);
+      else return dfrag(img, row0, ks, lane);
+    };
+    auto frag_b = [&](const __bf16* img, int row0, int ks) {
+      if constexpr (BCOL) return dcfrag<BN>(img, row0, ks, lane);
+      else return dfrag(img, row0, ks, lane);
+    };
+    if (nt > 0) issue(lds);
+    for (int t = 0; t < nt; ++t) {
+      __bf16* cur = lds + (t & 1) * DBUF;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (t + 1 < nt) {
+        da.advance();
+        db.advance();
+        issue(lds + ((t + 1) & 1) * DBUF);
+      }
+      const __bf16* Ai = cur;
+      const __bf16* Bi = cur + BM * DBK;
+#pragma unroll
+      for (int ks = 0; ks < DBK / (MF == 32 ? 16 : 32); ++ks) {
+        bf16x8 bh[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bh[j] = frag_b(Bi, brow + j * MF, ks);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const bf16x8 ah = frag_a(Ai, arow + i * MF, ks);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(ah, bh[j], acc[i][j]);
+        }
+      }
+    }
+  } else {
+  LA la;
+  LB lb;
+  // wgrad: only the first column of tiles publishes the bias gradient (row sums of dY^T): the others skip the sums
+  if constexpr (AK == A_COLM || AK == A_COLM_PIX || AK == A_COLM_SPLIT) la.want_bs = a.bias_ws != nullptr && tn == 0;
+  la.init(a, a.A + bidx * a.sA, m0, kb, tid, bidx);
+  lb.init(a, a.B + bidx * a.sB, n0, kb, tid, bidx);
 
   const int nt = ke > kb ? (ke - kb + BK - 1) / BK : 0;
-  const int arow = wm * (BM / WGM), brow = wn * (BN / WGN);
   // (Measured and removed: in bf16 mode, two K-tiles per stage in the free lo planes -- twice the MFMAs per barrier
   // and twice the load-latency budget -- ran the c5 fwd / dgrad GEMMs 3 % slower: the single-tile bf16 loop is not
   // bound by the barrier count or the global-load latency.)
@@ -1056,6 +1386,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
       }
     }
   }
+  }  // register-staged main loop
 
   // 16-B epilogue (16x16x32 kernels, one split, plain row order, N / ldc / ldr multiples of 4): each wave
   // stages half of its accumulator block at a time in LDS (free after the main loop) as fp32 rows and
@@ -1333,7 +1664,8 @@ inline bool vec_epi_disabled() {
   return v != 0;
 }
 
-template <int CFG, int AK, int VA, int BKIND, int VB>
+// PO >= 0 forces the kernel arithmetic (PREC 4: bf16-stored operands through the LDS-DMA main loop)
+template <int CFG, int AK, int VA, int BKIND, int VB, int PO = -1>
 void launch_cfg(GemmArgs& a, hipStream_t st) {
   constexpr int BM = CFG == T256x256 || CFG == T256x128 ? 256 : CFG == T64x64 ? 64 : 128;
   constexpr int BN = CFG == T256x256 || CFG == T128x256 ? 256 : CFG == T64x64 ? 64 : CFG == T128x16 ? 16 : 128;
@@ -1352,7 +1684,9 @@ void launch_cfg(GemmArgs& a, hipStream_t st) {
   constexpr bool presplit = AK == A_CONV_FWD_SPLIT || AK == A_CONV_DGRAD_SPLIT || AK == A_COLM_SPLIT ||
                             BKIND == B_ROWK_SPLIT || BKIND == B_WGRAD_FWD_SPLIT;
   const int mm = math_mode();
-  if (mm == MATH_BF16)
+  if constexpr (PO >= 0)
+    hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, PO>), grid, dim3(64 * WGM * WGN), 0, st, a);
+  else if (mm == MATH_BF16)
     hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, 1>), grid, dim3(64 * WGM * WGN), 0, st, a);
   else if (mm == MATH_FP32 && !presplit)  // (pre-split operands are value splits: never launched in this mode)
     hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, 0>), grid, dim3(64 * WGM * WGN), 0, st, a);
@@ -1375,6 +1709,24 @@ void launch_big(GemmArgs& a, hipStream_t st, int cfg) {
   }
 }
 
+// bf16-stored operands (MVAE_CONV_BF16): every tile config on the LDS-DMA main loop
+template <int AK>
+void launch_dma(GemmArgs& a, hipStream_t st, int cfg) {
+  switch (cfg) {
+    case T256x256: launch_cfg<T256x256, AK, 4, B_ROWK, 4, 4>(a, st); break;
+    case T256x128: launch_cfg<T256x128, AK, 4, B_ROWK, 4, 4>(a, st); break;
+    case T128x256: launch_cfg<T128x256, AK, 4, B_ROWK, 4, 4>(a, st); break;
+    case T128x128: launch_cfg<T128x128, AK, 4, B_ROWK, 4, 4>(a, st); break;
+    case T128x16: launch_cfg<T128x16, AK, 4, B_ROWK, 4, 4>(a, st); break;
+    default: launch_cfg<T64x64, AK, 4, B_ROWK, 4, 4>(a, st); break;
+  }
+}
+
+// gemm_dma.hip: launch_dma for AK in {A_ROWK, A_CONV_FWD, A_CONV_DGRAD, A_CONV_SUBPIX} (own translation unit)
+void conv_dma(int ak, GemmArgs& a, hipStream_t st, int cfg);
+// weight gradient on packed bf16 dY^T (COL) x im2col of bf16 X (B_WGRAD_FWD / B_WGRAD_SUBPIX)
+void wgrad_dma(int bkind, GemmArgs& a, hipStream_t st, int cfg);
+
 template <int AK, int VA, int BKIND, int VB>
 void launch_small(GemmArgs& a, hipStream_t st, int cfg) {
   if (cfg == T128x128) launch_cfg<T128x128, AK, VA, BKIND, VB>(a, st);
@@ -1387,7 +1739,7 @@ inline size_t splitk_ws_bytes(const GemmArgs& a) {
 
 inline void set_splits(GemmArgs& a, int splits) {
   a.splits = std::max(1, splits);
-  a.k_split = ((cdiv(a.K, a.splits) + BK - 1) / BK) * BK;
+  a.k_split = ((cdiv(a.K, a.splits) + DBK - 1) / DBK) * DBK;  // whole K-tiles of either main loop
   a.splits = std::max(1, cdiv(a.K, a.k_split));
 }
 

@@ -66,7 +66,14 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
                            size_t workspace_bytes, void* stream) {
   const bool xsplit = (mode & MVAE_CONV_XSPLIT) != 0;   // x holds split4_bf16 groups
   const bool dysplit = (mode & MVAE_CONV_DYSPLIT) != 0;  // dy holds split4_bf16 groups
-  mode &= ~(MVAE_CONV_XSPLIT | MVAE_CONV_DYSPLIT);
+  const bool bf = (mode & MVAE_CONV_BF16) != 0;          // dy and x packed bf16 (LDS-DMA main loop)
+  mode &= ~(MVAE_CONV_XSPLIT | MVAE_CONV_DYSPLIT | MVAE_CONV_BF16);
+  if (bf && (xsplit || dysplit || mode != 0 || dbias || cin % 8 || cout % 8 || !al16(dy) || !al16(x) ||
+             math_mode() != MATH_BF16)) {
+    set_error("wgrad: bf16-packed operands need the bf16 math mode, mode 0, cin %% 8 == 0, cout %% 8 == 0, aligned "
+              "dy / x, no fused bias");
+    return MVAE_EINVAL;
+  }
   if (dysplit && (cout % 4 != 0 || !al16(dy))) {
     set_error("wgrad: a pre-split dy needs cout %% 4 == 0, 16-B alignment");
     return MVAE_EINVAL;
@@ -94,10 +101,11 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
     const int n = std::min(chunk, nb - b0);
     GemmArgs a{};
     wgrad_shape(a, n, cin, cout, kh, kw, ho, wo);
-    a.A = dy + (long long)b0 * (out_img / 4); a.lda = cout;
-    a.B = x + (long long)b0 * (in_img / 4);
+    a.A = bf ? (const float*)((const __bf16*)dy + (long long)b0 * (out_img / 4)) : dy + (long long)b0 * (out_img / 4);
+    a.lda = cout;
+    a.B = bf ? (const float*)((const __bf16*)x + (long long)b0 * (in_img / 4)) : x + (long long)b0 * (in_img / 4);
     a.C = dw; a.ldc = a.N; a.alpha = 1.f; a.beta = b0 == 0 ? beta : 1.f;
-    a.a_bytes = (unsigned)(out_img * n); a.b_bytes = (unsigned)(in_img * n);
+    a.a_bytes = (unsigned)(out_img * n / (bf ? 2 : 1)); a.b_bytes = (unsigned)(in_img * n / (bf ? 2 : 1));
     a.c_bytes = (unsigned)((long long)a.M * a.N * 4);
     a.H = h; a.W = wd; a.Cx = cin; a.Ho = ho; a.Wo = wo; a.R = kh; a.S = kw;
     set_gather_magic(a);
@@ -108,7 +116,9 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
     plan_splits(a, cfg, workspace, workspace_bytes - bias_bytes);
     // bias partials live after the split-K partials
     a.bias_ws = dbias ? (float*)((char*)workspace + ((splitk_ws_bytes(a) + 255) & ~(size_t)255)) : nullptr;
-    if (dysplit) {
+    if (bf) {
+      wgrad_dma(B_WGRAD_FWD, a, st, cfg);
+    } else if (dysplit) {
       if (xsplit) launch_big<A_COLM_SPLIT, 4, B_WGRAD_FWD_SPLIT, 4>(a, st, cfg);
       else if (mode == 0 && vb) launch_big<A_COLM_SPLIT, 4, B_WGRAD_FWD, 4>(a, st, cfg);
       else if (mode == 0) launch_small<A_COLM_SPLIT, 4, B_WGRAD_FWD, 1>(a, st, cfg);

@@ -13,10 +13,26 @@ namespace mvae {
 // per tap t: [cout][cin] (row stride rs*cin) -> [cin][cout] (row stride rs*cout), 64x64 tiles through
 // LDS so both the reads (along cin) and the writes (along cout) are coalesced
 // write phase of a transposed 64x64 tile: tile[o_local][c_local] -> wt rows c (row stride rs*cout, tap t)
-// along o; split: groups of 4 consecutive o as split4_bf16 (needs cout % 4 == 0)
+// along o; split 1: groups of 4 consecutive o as split4_bf16 (needs cout % 4 == 0); split 2: packed bf16 (RNE; the
+// bf16-mixed mode's GEMM operand, 2 B per element at the same element offsets)
 __device__ __forceinline__ void write_transposed(const float (*tile)[65], float* __restrict__ wt, int c0, int o0, int t,
                                                  int rs, int cin, int cout, int split) {
-  if (!split) {
+  if (split == 2) {
+    const int g = threadIdx.x & 31, cr = threadIdx.x >> 5;
+    __bf16* wb = (__bf16*)wt;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int cl = cr + 8 * i, c = c0 + cl, o = o0 + 2 * g;
+      if (c < cin && o < cout) {
+        const long long e = ((long long)c * rs + t) * cout + o;
+        if (o + 1 < cout && (e & 1) == 0) *(unsigned*)(wb + e) = pk_bf16x2(tile[2 * g][cl], tile[2 * g + 1][cl]);
+        else {
+          wb[e] = (__bf16)tile[2 * g][cl];
+          if (o + 1 < cout) wb[e + 1] = (__bf16)tile[2 * g + 1][cl];
+        }
+      }
+    }
+  } else if (!split) {
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -88,7 +104,7 @@ __device__ __forceinline__ int sub_mask(int p, int a) { return p == 0 ? (a == 0 
 
 __global__ void __launch_bounds__(256) w_ups_fwd_kernel(const float* __restrict__ w, float* __restrict__ w4, int cout,
                                                         int cin, int split) {
-  // one thread per (co, group of 4 ci) (split; cin % 4 == 0) or per (co, ci)
+  // one thread per (co, group of 4 ci) (split 1: split4_bf16, split 2: packed bf16; cin % 4 == 0) or per (co, ci)
   const int gw = split ? 4 : 1, ng = cin / gw;
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long long)cout * ng) return;
@@ -116,14 +132,28 @@ __global__ void __launch_bounds__(256) w_ups_fwd_kernel(const float* __restrict_
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] += t[r][s][e];
         float* o = w4 + ((((long long)cls * cout + co) * 2 + a) * 2 + b) * cin + ci;
-        if (split) *(uint4*)o = split4_bf16(float4{v[0], v[1], v[2], v[3]});
-        else *o = v[0];
+        if (split == 2) {
+          __bf16* ob = (__bf16*)w4 + (o - w4);
+          *(uint2*)ob = uint2{pk_bf16x2(v[0], v[1]), pk_bf16x2(v[2], v[3])};
+        } else if (split) {
+          *(uint4*)o = split4_bf16(float4{v[0], v[1], v[2], v[3]});
+        } else {
+          *o = v[0];
+        }
       }
 }
 
 __global__ void __launch_bounds__(256) split_bf16_kernel(const float4* __restrict__ x, uint4* __restrict__ y, long long n4) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x)
     y[i] = split4_bf16(x[i]);
+}
+
+// packed bf16 (RNE) of 8 fp32 values per thread step
+__global__ void __launch_bounds__(256) pack_bf16_kernel(const float4* __restrict__ x, uint4* __restrict__ y, long long n8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const float4 a = x[2 * i], b = x[2 * i + 1];
+    y[i] = uint4{pk_bf16x2(a.x, a.y), pk_bf16x2(a.z, a.w), pk_bf16x2(b.x, b.y), pk_bf16x2(b.z, b.w)};
+  }
 }
 
 // column sums: part[chunk][n] = sum over rows in chunk ; then out[n] += sum_chunks (fixed order)
@@ -168,7 +198,7 @@ using namespace mvae;
 extern "C" {
 
 int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int kw, int cin, int split, void* stream) {
-  if (cout <= 0 || kh <= 0 || kw <= 0 || cin <= 0 || (split && (cout & 3))) {
+  if (cout <= 0 || kh <= 0 || kw <= 0 || cin <= 0 || split < 0 || split > 2 || (split && (cout & 3))) {
     set_error("w_transpose: bad sizes");
     return MVAE_EINVAL;
   }
@@ -179,7 +209,7 @@ int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int 
 
 // wt [cin][4][4][cout] for the dgrad of "nearest-x2 upsample then 3x3 conv"
 int mvae_conv_weight_upsample_dgrad(const float* w, float* wt, int cout, int cin, int split, void* stream) {
-  if (cout <= 0 || cin <= 0 || (split && (cout & 3))) { set_error("w_ups: bad sizes"); return MVAE_EINVAL; }
+  if (cout <= 0 || cin <= 0 || split < 0 || split > 2 || (split && (cout & 3))) { set_error("w_ups: bad sizes"); return MVAE_EINVAL; }
   hipLaunchKernelGGL(w_ups_dgrad_kernel, dim3((cin + 63) / 64, (cout + 63) / 64, 16), dim3(256), 0,
                      (hipStream_t)stream, w, wt, cout, cin, split);
   return launch_status();
@@ -187,7 +217,7 @@ int mvae_conv_weight_upsample_dgrad(const float* w, float* wt, int cout, int cin
 
 // w4 [4][cout][2][2][cin] for the sub-pixel forward of "nearest-x2 upsample then 3x3 conv"
 int mvae_conv_weight_upsample_fwd(const float* w, float* w4, int cout, int cin, int split, void* stream) {
-  if (cout <= 0 || cin <= 0 || (split && (cin & 3))) { set_error("w_ups_fwd: bad sizes"); return MVAE_EINVAL; }
+  if (cout <= 0 || cin <= 0 || split < 0 || split > 2 || (split && (cin & 3))) { set_error("w_ups_fwd: bad sizes"); return MVAE_EINVAL; }
   const long long tot = (long long)cout * (split ? cin / 4 : cin);
   hipLaunchKernelGGL(w_ups_fwd_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, w, w4,
                      cout, cin, split);
@@ -198,6 +228,17 @@ int mvae_split_bf16(const float* x, void* y, long long n, void* stream) {
   if (n <= 0 || (n & 3)) { set_error("split_bf16: n must be a positive multiple of 4"); return MVAE_EINVAL; }
   hipLaunchKernelGGL(split_bf16_kernel, dim3(egrid(n / 4)), dim3(256), 0, (hipStream_t)stream, (const float4*)x, (uint4*)y,
                      n / 4);
+  return launch_status();
+}
+
+// y (bf16, n elements) = x (fp32) rounded to nearest even: the bf16-mixed mode's packed GEMM operands
+int mvae_pack_bf16(const float* x, void* y, long long n, void* stream) {
+  if (n <= 0 || (n & 7) || ((uintptr_t)x & 15) || ((uintptr_t)y & 15)) {
+    set_error("pack_bf16: n must be a positive multiple of 8, x / y 16-B aligned");
+    return MVAE_EINVAL;
+  }
+  hipLaunchKernelGGL(pack_bf16_kernel, dim3(egrid(n / 8)), dim3(256), 0, (hipStream_t)stream, (const float4*)x, (uint4*)y,
+                     n / 8);
   return launch_status();
 }
 

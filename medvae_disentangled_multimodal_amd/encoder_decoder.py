@@ -112,9 +112,10 @@ class ResnetBlock(nn.Module):
             raise NotImplementedError("timestep embeddings are not used by the VAE (temb_channels=0)")
         # x's two gradient branches (norm1 and the residual / shortcut) are summed inside norm1's backward
         sink = ops.GradSink() if torch.is_grad_enabled() and x.requires_grad else None
-        h = self.conv1(self.norm1(x, silu=True, for_conv=True, grad_sink=sink), gn_stats=True)
+        # for_conv = the consuming conv's output channels (bf16-mixed: packed bf16 GroupNorm outputs, ops.group_norm)
+        h = self.conv1(self.norm1(x, silu=True, for_conv=self.out_channels, grad_sink=sink), gn_stats=True)
         p = self.dropout.p if self.training else 0.0
-        h = self.norm2(h, silu=True, drop_p=p, for_conv=True)
+        h = self.norm2(h, silu=True, drop_p=p, for_conv=self.out_channels)
         if self.in_channels != self.out_channels:
             sc = self.conv_shortcut if self.use_conv_shortcut else self.nin_shortcut
             return self.conv2(h, residual=sc(x, x_sink=sink), gn_stats=True)
@@ -222,7 +223,7 @@ class Encoder(nn.Module):
             if i_level != self.num_resolutions - 1:
                 h = lvl.downsample(h)
         h = self.mid.block_2(self.mid.attn_1(self.mid.block_1(h)))
-        return self.conv_out(self.norm_out(h, silu=True, for_conv=True))
+        return self.conv_out(self.norm_out(h, silu=True, for_conv=self.conv_out.out_channels))
 
 
 class Decoder(nn.Module):
@@ -278,7 +279,7 @@ class Decoder(nn.Module):
                 h = lvl.upsample(h)
         if self.give_pre_end:
             return h
-        h = self.conv_out(self.norm_out(h, silu=True, for_conv=True))
+        h = self.conv_out(self.norm_out(h, silu=True, for_conv=self.conv_out.out_channels))
         if self.tanh_out:
             h = torch.tanh(h)
         return h

@@ -203,6 +203,25 @@ def _al16(*ts) -> bool:
     return all(t.data_ptr() % 16 == 0 for t in ts)
 
 
+# bf16-mixed convolutions on packed bf16 operands (MVAE_CONV_BF16: the GEMM stages them into LDS by DMA in 64-deep
+# K-tiles, no staging registers or conversion). MVAE_NO_BF16_DMA=1 keeps the register-staged bf16 loop on fp32
+# operands.
+BF16_DMA = os.environ.get("MVAE_NO_BF16_DMA") is None
+MVAE_CONV_BF16 = 128
+
+
+def _bf16_dma() -> bool:
+    return BF16_DMA and _MATH[0] == 1
+
+
+def pack_bf16(t: torch.Tensor, key: str) -> torch.Tensor:
+    """Packed bf16 (round to nearest even) copy of an fp32 tensor in arena scratch `key` (2 B per element, same
+    element order)."""
+    out = ARENA.get(key, t.numel() * 2, t.device)
+    _lib.call("mvae_pack_bf16", t.data_ptr(), out.data_ptr(), t.numel(), _stream(t))
+    return out
+
+
 # current GEMM arithmetic (mirror of mvae_get_math_mode, kept by set_precision / math_scope): 0 = 3xBF16,
 # 1 = bf16, 2 = exact fp32 (f32-input MFMA). The 3xBF16 pre-split operand layouts are value splits and are
 # not used in the exact mode.
@@ -257,9 +276,10 @@ def _conv_call(x, w, b, res, y, n, h, wd, c, co, kh, kw, stride, pad_t, pad_l, h
                   mode, st)
 
 
-def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part=None):
+def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part=None, x_bf16: bool = False):
     """gn_part (fp64 [n*ho*wo/32 * cout/4 * 2]): also emit the GroupNorm statistics of y from the GEMM
-    epilogue (mvae_conv2d_gnstats_nhwc; only on the plain implicit-GEMM path -- the caller checks)."""
+    epilogue (mvae_conv2d_gnstats_nhwc; only on the plain implicit-GEMM path -- the caller checks).
+    x_bf16: x holds packed bf16 (BF16_ATTR; bf16-mixed mode)."""
     n, c, h, wd = x.shape
     co = w.shape[0]
     ho, wo = g.out_hw(h, wd)
@@ -273,6 +293,11 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
     split = WEIGHT_SPLIT and _splits_ok() and c % 4 == 0 and _al16(x) and not g.pointwise and g.kh * g.kw <= 32
     if x_split and (g.pointwise or g.upsample or c % 4 or not _al16(x)):
         raise RuntimeError("conv2d: a pre-split input needs a non-pointwise, non-upsample conv with cin % 4 == 0")
+    if _bf16_dma() and c % 8 == 0 and not x_split and _al16(x) and not g.pointwise and g.kh * g.kw <= 32 and \
+            (sub or not g.upsample):
+        return _conv_fwd_bf16(x, w, b, res, g, y, n, c, h, wd, co, ho, wo, sub, alg, ref, gn_part, st, x_bf16)
+    if x_bf16:
+        raise RuntimeError("conv2d: a packed bf16 input needs the bf16-mixed LDS-DMA conv path")
     wg = w
     if sub:  # tap-summed per-class weights (prepared outside the timed GEMM launch)
         wg = ARENA.get("w4", 16 * co * c * 4, x.device)
@@ -299,6 +324,36 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
     return y
 
 
+def _conv_fwd_bf16(x, w, b, res, g, y, n, c, h, wd, co, ho, wo, sub, alg, ref, gn_part, st, x_bf16=False):
+    """bf16-mixed forward on packed bf16 x and weights (MVAE_CONV_BF16)."""
+    xb = x if x_bf16 else pack_bf16(x, "xbf")
+    if sub:
+        wg = ARENA.get("w4", 16 * co * c * 2, x.device)
+        _lib.call("mvae_conv_weight_upsample_fwd", w.data_ptr(), wg.data_ptr(), co, c, 2, st)
+    else:
+        wg = pack_bf16(w, "wsplit")
+    with _timed("conv_fwd", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
+        if sub:
+            _lib.call("mvae_conv2d_upsample_nhwc", xb.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n,
+                      h, wd, c, co, 2, st)
+        elif gn_part is not None:
+            _lib.call("mvae_conv2d_gnstats_nhwc", xb.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(),
+                      n, h, wd, c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, MVAE_CONV_BF16,
+                      gn_part.data_ptr(), st)
+        else:
+            _conv_call(xb.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y, n, h, wd, c, co, g.kh, g.kw, g.stride,
+                       g.pad_t, g.pad_l, ho, wo, MVAE_CONV_BF16, st)
+    return y
+
+
+def pack_dy(dy: torch.Tensor, g: ConvGeom) -> Optional[torch.Tensor]:
+    """dy as packed bf16 for the input-gradient GEMM of the bf16-mixed mode, or None when that path does not apply."""
+    if not _bf16_dma() or g.pointwise or dy.dim() != 4 or dy.shape[1] % 8 or g.kh * g.kw > 32 or not _al16(dy) or \
+            not dy.is_contiguous(memory_format=CL):
+        return None
+    return pack_bf16(dy, "dybf")
+
+
 def split_dy(dy: torch.Tensor) -> Optional[torch.Tensor]:
     """dy in the 3xBF16 operand layout (split4_bf16 groups), or None when the conv cannot use it."""
     if not DY_SPLIT or not _splits_ok() or dy.dim() != 4 or dy.shape[1] % 4 or dy.numel() < DY_SPLIT_MIN or not _al16(dy) or \
@@ -309,10 +364,11 @@ def split_dy(dy: torch.Tensor) -> Optional[torch.Tensor]:
     return ds
 
 
-def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None):
+def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=None):
     """gn_link (GnBwdLink): the conv's input was silu?(GroupNorm(x)) -- also emit that GroupNorm's backward
     partials from the GEMM epilogue (mvae_conv2d_dgrad_gnbwd_nhwc) into gn_link.part when the launch allows it.
-    dys: dy pre-split by split_dy (same values; used as the gathered GEMM operand when given)."""
+    dys: dy pre-split by split_dy (same values; used as the gathered GEMM operand when given).
+    dyb: dy as packed bf16 (pack_dy; bf16-mixed mode)."""
     n, c, h, wd = x_shape
     co = w.shape[0]
     _, _, ho, wo = dy.shape
@@ -320,6 +376,8 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None):
     st = _stream(dy)
     flops = 2.0 * n * ho * wo * co * c * g.kh * g.kw  # reference count
     shp = (n, c, h, wd, co, g.kh, g.stride, g.upsample)
+    if dyb is not None and (gn_link is None or not gn_link.usable(dx)):
+        return _conv_dgrad_bf16(dyb, w, dx, g, n, c, h, wd, co, ho, wo, flops, shp, st)
     if dys is not None and (g.pointwise or co % 4):
         dys = None
     dya = dy if dys is None else dys
@@ -371,14 +429,55 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None):
     return dx
 
 
-def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool = False, dys=None):
+def _conv_dgrad_bf16(dyb, w, dx, g, n, c, h, wd, co, ho, wo, flops, shp, st):
+    """bf16-mixed input gradient on packed bf16 dy and weights (MVAE_CONV_BF16)."""
+    dev = dx.device
+    if g.upsample:
+        wt = ARENA.get("wt", c * 16 * co * 2, dev)
+        _lib.call("mvae_conv_weight_upsample_dgrad", w.data_ptr(), wt.data_ptr(), co, c, 2, st)
+        with _timed("conv_dgrad", flops * 4 / 9, shp, flops):
+            # dX = stride-2, pad-1 4x4 (forward-gather) conv of dY with the tap-summed kernel
+            _lib.call("mvae_conv2d_nhwc", dyb.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
+                      4, 4, 2, 1, 1, h, wd, MVAE_CONV_BF16, st)
+        return dx
+    wt = ARENA.get("wt", c * g.kh * g.kw * co * 2, dev)
+    _lib.call("mvae_conv_weight_transpose", w.data_ptr(), wt.data_ptr(), co, g.kh, g.kw, c, 2, st)
+    if g.stride == 2 and h % 2 == 0 and wd % 2 == 0 and g.kh <= 4 and g.kw <= 4 and STRIDE2_CLASSES:
+        wc = ARENA.get("wcls", c * g.kh * g.kw * co * 4, dev)
+        with _timed("conv_dgrad", flops, shp):
+            _lib.call("mvae_conv2d_dgrad_stride2_nhwc", dyb.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, h, wd, c, co,
+                      g.kh, g.kw, g.pad_t, g.pad_l, ho, wo, 4, wc.data_ptr(), wc.numel(), st)
+        return dx
+    with _timed("conv_dgrad", flops, shp):
+        _conv_call(dyb.data_ptr(), wt.data_ptr(), None, None, dx, n, ho, wo, co, c, g.kh, g.kw, g.stride, g.pad_t,
+                   g.pad_l, h, wd, 2 | MVAE_CONV_BF16, st)
+    return dx
+
+
+def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool = False, dys=None, dyb=None,
+                     x_bf16: bool = False):
     """dw (+ db when given and the conv is not pointwise) accumulate with `beta`. Returns True when
-    the bias gradient was produced by the fused wgrad kernel. dys: dy pre-split by split_dy."""
+    the bias gradient was produced by the fused wgrad kernel. dys: dy pre-split by split_dy; dyb: dy as packed bf16
+    (pack_dy, bf16-mixed mode)."""
     n, c, h, wd = x.shape
     co = dy.shape[1]
     _, _, ho, wo = dy.shape
     ref = 2.0 * n * ho * wo * co * c * g.kh * g.kw
     alg = ref * 4 / 9 if _subpixel_upsample(g) else ref
+    if dyb is not None and not x_split and not g.upsample and c % 8 == 0 and co % 8 == 0 and _al16(x):
+        # bf16-mixed weight gradient on packed bf16 dy and x (LDS-DMA main loop); the bias gradient is summed from the
+        # fp32 dy by the caller
+        xb = x if x_bf16 else pack_bf16(x, "xbf")
+        st = _stream(dy)
+        nbytes = _lib.query("mvae_conv2d_wgrad_workspace_bytes", n, c, co, g.kh, g.kw, ho, wo)
+        ws = ARENA.get("ws", nbytes, dy.device)
+        with _timed("conv_wgrad", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
+            _lib.call("mvae_conv2d_wgrad_nhwc", dyb.data_ptr(), xb.data_ptr(), dw.data_ptr(), None, float(beta), n, h,
+                      wd, c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, MVAE_CONV_BF16, ws.data_ptr(),
+                      ws.numel(), st)
+        return False
+    if x_bf16:
+        raise RuntimeError("conv2d wgrad: a packed bf16 input needs the bf16-mixed LDS-DMA path (packed dy, cout % 8)")
     with _timed("conv_wgrad", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
         return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db, x_split, dys)
 
@@ -471,15 +570,17 @@ class Conv2dFn(torch.autograd.Function):
                 gn_link=None):
         _check(x, "conv input")
         xs = bool(getattr(x, XSPLIT_ATTR, False))
-        if xs and not x.is_contiguous(memory_format=CL):
-            raise RuntimeError("conv2d: a pre-split input must not be re-laid out")
+        xb16 = bool(getattr(x, BF16_ATTR, False))
+        if (xs or xb16) and not x.is_contiguous(memory_format=CL):
+            raise RuntimeError("conv2d: a pre-split / packed input must not be re-laid out")
         x = nhwc(x)
         w = _krsc(weight)
         res = nhwc(residual) if residual is not None else None
-        y = conv2d_forward_raw(x, w, bias, res, geom, xs, gn_part)
+        y = conv2d_forward_raw(x, w, bias, res, geom, xs, gn_part, x_bf16=xb16)
         ctx.math = _MATH[0]  # the backward GEMMs run in the forward's arithmetic
         ctx.geom = geom
         ctx.x_split = xs
+        ctx.x_bf16 = xb16
         ctx.has_bias = bias is not None
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, w)
@@ -503,9 +604,10 @@ class Conv2dFn(torch.autograd.Function):
         link = ctx.gn_link
         if link is not None:
             link.part = link.dx = None  # partials of an earlier pass are never reused
-        dys = split_dy(dy) if not g.pointwise and not _subpixel_upsample(g) else None
+        dyb = pack_dy(dy, g) if (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]) else None
+        dys = split_dy(dy) if not g.pointwise and not _subpixel_upsample(g) and dyb is None else None
         if ctx.needs_input_grad[0]:
-            dx = conv2d_dgrad_raw(dy, w, x.shape, g, link if ctx.x_sink is None else None, dys=dys)
+            dx = conv2d_dgrad_raw(dy, w, x.shape, g, link if ctx.x_sink is None else None, dys=dys, dyb=dyb)
             if ctx.x_sink is not None and ctx.x_sink.park(dx):
                 dx = None
         bias_done = False
@@ -513,14 +615,14 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             tgt = _main_grad(ctx.weight_ref)
             btgt = _main_grad(ctx.bias_ref) if want_b else None
-            xs = ctx.x_split
+            xs, xb16 = ctx.x_split, ctx.x_bf16
             if tgt is not None and (not want_b or btgt is not None):
-                bias_done = conv2d_wgrad_raw(dy, x, tgt, 1.0, g, btgt, x_split=xs, dys=dys)
+                bias_done = conv2d_wgrad_raw(dy, x, tgt, 1.0, g, btgt, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16)
             elif tgt is not None:
-                conv2d_wgrad_raw(dy, x, tgt, 1.0, g, x_split=xs, dys=dys)
+                conv2d_wgrad_raw(dy, x, tgt, 1.0, g, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16)
             else:
                 dw_ret = torch.empty_like(w, memory_format=CL)
-                conv2d_wgrad_raw(dy, x, dw_ret, 0.0, g, x_split=xs, dys=dys)
+                conv2d_wgrad_raw(dy, x, dw_ret, 0.0, g, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16)
         if ctx.has_bias and ctx.needs_input_grad[2] and not bias_done:
             tgt = _main_grad(ctx.bias_ref)
             n, co, ho, wo = dy.shape
@@ -682,13 +784,21 @@ class GroupNormFn(torch.autograd.Function):
 # (the bytes are bf16 hi/lo pairs, not fp32 values): only Conv2dFn consumes them.
 XSPLIT_ATTR = "_mvae_xsplit"
 ACT_SPLIT = os.environ.get("MVAE_NO_ACT_SPLIT") is None
+# bf16-mixed mode: a GroupNorm output whose consuming conv runs on packed bf16 operands (MVAE_CONV_BF16) is written
+# packed (2 B per element in the first half of the fp32 tensor's bytes); only Conv2dFn consumes it, forward and
+# weight gradient reading the same bytes
+BF16_ATTR = "_mvae_bf16"
 
 
 def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0, for_conv=False, grad_sink=None):
-    """for_conv=True: the caller feeds the result straight into ops.conv2d (3x3/stride-1, C % 4 == 0) -- the
-    output is then written pre-split for the GEMM (GroupNorm -> conv is the ResnetBlock / norm_out pattern,
-    encoder_decoder.py:141-163, :318-328)."""
-    split = bool(for_conv and ACT_SPLIT and _splits_ok() and x.shape[1] % 4 == 0)
+    """for_conv (True, or the consuming conv's output channel count): the caller feeds the result straight into
+    ops.conv2d (3x3/stride-1, C % 4 == 0) -- the output is then written pre-split for the GEMM (GroupNorm -> conv is
+    the ResnetBlock / norm_out pattern, encoder_decoder.py:141-163, :318-328); in the bf16-mixed mode, with a known
+    output channel count that is a multiple of 8, packed bf16 for the LDS-DMA GEMM."""
+    packed = bool(for_conv and not isinstance(for_conv, bool) and int(for_conv) % 8 == 0 and _bf16_dma() and
+                  x.shape[1] % 8 == 0 and _al16(x))
+    split = 2 if packed else int(bool(for_conv and ACT_SPLIT and _splits_ok() and not _bf16_dma() and
+                                      x.shape[1] % 4 == 0))
     part = getattr(x, GN_PART_ATTR, None)
     if part is not None:
         delattr(x, GN_PART_ATTR)  # consumed once; frees the statistics with the next allocation cycle
@@ -698,7 +808,9 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
         part = part[0] if ok else None
     link = GnBwdLink(groups, silu) if (for_conv and GN_BWD_FUSED and drop_p == 0.0 and x.requires_grad) else None
     y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink, part, link)
-    if split:
+    if split == 2:
+        setattr(y, BF16_ATTR, True)
+    elif split:
         setattr(y, XSPLIT_ATTR, True)
     if link is not None:
         link.bind_output(y)
