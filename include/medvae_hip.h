@@ -155,6 +155,10 @@ int mvae_split_bf16(const float* x, void* y, long long n, void* stream);
 /* Packed bf16 (round to nearest even) of n fp32 values (n % 8 == 0, 16-B aligned): the bf16-mixed mode's GEMM
  * operands (MVAE_CONV_BF16). The weight-prep entry points take split = 2 to emit it directly. */
 int mvae_pack_bf16(const float* x, void* y, long long n, void* stream);
+/* Packed bf16 of a conv output gradient dy [rows][n] (n % 4 == 0) and, from the same pass, its bias gradient
+ * out[n] = beta*out[n] + sum_rows dy (fp64 partials, fixed order; workspace mvae_bias_grad_workspace_bytes). */
+int mvae_pack_bf16_colsum(const float* x, void* y, long long rows, int n, float* out, float beta, void* workspace,
+                          size_t workspace_bytes, void* stream);
 
 /* Weight re-layouts for the input gradient: KRSC -> [cin][kh][kw][cout]; and the 4x4 tap-summed
  * kernel [cin][4][4][cout] for Upsample's conv (encoder_decoder.py:205-209). */

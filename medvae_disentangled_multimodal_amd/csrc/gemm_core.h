@@ -753,35 +753,52 @@ struct LoadWgradX {
 // ------------------------------------------------------------------------------------------
 // PREC 4: bf16 operands STORED as bf16 in HBM (the bf16-mixed mode's conv inputs, weights and output gradients are
 // packed by their producers), staged by LDS-DMA (buffer_load_dwordx4 ... lds): no staging registers, no VALU split,
-// no ds_write. K-tile DBK = 64; ROW images [ROWS][64] bf16 with 128-B rows, filled lane-linearly (one DMA
-// instruction = 1 KB = 8 rows, lane l -> row l/8, 16-B slot l%8) and swizzled on the SOURCE side: physical slot
-// p of row r holds the row's logical 8-element chunk p ^ dswz(r), and fragment reads apply the same involution
-// (ds_read_b128 lane groups {0-3,12-15,20-27}, ... then hit 16 distinct 16-B bank windows).
+// no ds_write. Stage depth DKT (32 in the 4-stage ring, 64 in the 2-stage loop); ROW images [ROWS][DKT] bf16,
+// filled lane-linearly (one DMA instruction = 1 KB = DPR rows, lane l -> row l / DCH, 16-B slot l % DCH) and
+// swizzled on the SOURCE side: physical slot p of row r holds the row's logical 8-element chunk p ^ dswz(r), and
+// fragment reads apply the same involution (ds_read_b128 lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...
+// then hit 16 distinct 16-B bank windows: 64-B rows use [0,3,2,1][(r >> 2) & 3], 128-B rows (r >> 1) & 7).
 // ------------------------------------------------------------------------------------------
-constexpr int DBK = 64;
-__device__ __forceinline__ int dswz(int r) { return (r >> 1) & 7; }
+constexpr int DBK = 64;  // split-K granularity (whole stages of either loop)
+#ifndef MVAE_DMA_EXP
+#define MVAE_DMA_EXP 0
+#endif
+#ifndef MVAE_DMA_RING
+#define MVAE_DMA_RING 0
+#endif
+#ifndef MVAE_DMA_SPREAD  // 1: COL (weight-gradient) loops spread their DMA issue over the k-steps; 2: every loop
+#define MVAE_DMA_SPREAD 1
+#endif
+constexpr int DKT = MVAE_DMA_RING ? 32 : 64;  // K depth of one DMA stage
+constexpr int DCH = DKT / 8;                  // 16-B chunks per ROW-image row
+constexpr int DPR = 64 / DCH;                 // rows per 1-KB DMA piece
+constexpr int DNST = MVAE_DMA_RING ? 4 : 2;   // LDS stages
+__device__ __forceinline__ int dswz(int r) { return DKT == 64 ? (r >> 1) & 7 : (4 - ((r >> 2) & 3)) & 3; }
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// (permuted) K-tile starting at k (k % 64 == 0): channel chunk t / RS of tap t % RS, 64 channels wide
+// (permuted) stage starting at k (k % DKT == 0): channel chunk t / RS of tap t % RS, DKT channels wide
 __device__ __forceinline__ int kperm64(const GemmArgs& a, int k) {
-  const int t = k >> 6;
+  const int t = k / DKT;
   const int chunk = mdiv(t, a.mg_rs);
-  return (t - chunk * a.perm_rs) * a.Cx + chunk * DBK;
+  return (t - chunk * a.perm_rs) * a.Cx + chunk * DKT;
 }
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, __bf16* dst, unsigned off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)dst, 16, off, 0, 0, 0);
 }
 
-// Piece q of a ROWS-row image (8 rows, 1 KB) is filled by wave (q % (NT/64)) as its instruction q / (NT/64); with
-// an even wave count the piece parity equals the wave parity, so a lane's logical chunk (slot ^ dswz(row)) is the
-// same for all its pieces.
+// Piece q of a ROWS-row image (DPR rows, 1 KB) is filled by wave (q % (NT/64)) as its instruction q / (NT/64); with
+// an even wave count a lane's logical chunk (slot ^ dswz(row)) is the same for all its pieces.
 template <int ROWS, int NT>
 struct DmaShape {
   static constexpr int NW = NT / 64;
-  static constexpr int NI = ROWS * 8 / NT;  // DMA instructions per thread per K-tile
-  static_assert(NI >= 1 && NI * NT == ROWS * 8 && NW % 2 == 0, "DMA image shape");
+  static constexpr int NI = ROWS * DKT / (NT * 8);  // DMA instructions per thread per stage
+  static_assert(NI >= 1 && NI * NT * 8 == ROWS * DKT && NW % 2 == 0, "DMA image shape");
 };
+__device__ __forceinline__ int dma_chunk(int lane, int w) {
+  const int row = w * DPR + lane / DCH;  // any of the lane's rows: the swizzle is the same
+  return (lane % DCH) ^ dswz(row);
+}
 
 // ROW image of a row-major bf16 matrix: element (row, k) at P[row*ld + kperm(k)]
 template <int ROWS, int NT, bool IS_A>
@@ -797,13 +814,13 @@ struct DmaRowK {
     rs = make_rsrc(p, IS_A ? a.a_bytes : a.b_bytes);
     const int lane = tid & 63;
     w = tid >> 6;
-    cb = (lane & 7) ^ (((lane >> 4) & 3) | ((w & 1) << 2));
+    cb = dma_chunk(lane, w);
     const unsigned ld = (unsigned)(IS_A ? a.lda : a.ldb);
     const int rows = IS_A ? a.M : a.N;
     K = a.K; k = kb;
 #pragma unroll
     for (int i = 0; i < S::NI; ++i) {
-      const int row = row0 + (i * S::NW + w) * 8 + (lane >> 3);
+      const int row = row0 + (i * S::NW + w) * DPR + lane / DCH;
       rv[i] = row < rows;
       rowoff[i] = (unsigned)row * ld * 2u;
     }
@@ -816,7 +833,7 @@ struct DmaRowK {
   __device__ void issue(const GemmArgs&, __bf16* img, int i) {
     dma16(rs, img + (i * S::NW + w) * 512, (rv[i] & kv) ? rowoff[i] + kb2 : OOB);
   }
-  __device__ void advance() { k += DBK; }
+  __device__ void advance() { k += DKT; }
 };
 
 // ROW image of the implicit im2col of a bf16 NHWC tensor (affine gather of LoadConvA's vector path, in bf16
@@ -833,13 +850,13 @@ struct DmaConvA {
     rs = make_rsrc(x, a.a_bytes);
     const int lane = tid & 63;
     w = tid >> 6;
-    cb = (lane & 7) ^ (((lane >> 4) & 3) | ((w & 1) << 2));
+    cb = dma_chunk(lane, w);
     k = kb;
     pt = a.pad_t - ((bidx + a.sub_par) >> 1);
     pl = a.pad_l - ((bidx + a.sub_par) & 1);
 #pragma unroll
     for (int i = 0; i < S::NI; ++i) {
-      const int m = row0 + (i * S::NW + w) * 8 + (lane >> 3);
+      const int m = row0 + (i * S::NW + w) * DPR + lane / DCH;
       const bool valid = m < a.M;
       const int mm = valid ? m : 0;
       const int b = mdiv(mm, a.mg_hw);
@@ -890,7 +907,7 @@ struct DmaConvA {
   __device__ void issue(const GemmArgs&, __bf16* img, int i) {
     dma16(rs, img + (i * S::NW + w) * 512, (vmask[i] & tbit) ? rowbase[i] + (unsigned)delta : OOB);
   }
-  __device__ void advance() { k += DBK; }
+  __device__ void advance() { k += DKT; }
 };
 
 // COL images (weight gradient: K = pixels, both operands contiguous along their rows): [64 k-rows][ROWS] bf16, k-row
@@ -907,8 +924,8 @@ struct DmaColShape {
   static constexpr int CPR = ROWS / 8;  // 16-B chunks per k-row
   static constexpr int KPI = 64 / CPR;  // k-rows per DMA instruction
   static constexpr int NW = NT / 64;
-  static constexpr int NI = ROWS * 8 / NT;  // DMA instructions per thread per K-tile
-  static_assert(ROWS >= 64 && NI >= 1 && NI * NT == ROWS * 8, "DMA COL image shape");
+  static constexpr int NI = ROWS * DKT / (NT * 8);  // DMA instructions per thread per stage
+  static_assert(ROWS >= 64 && NI >= 1 && NI * NT * 8 == ROWS * DKT, "DMA COL image shape");
 };
 
 // A = dY^T: element (m, k) at P[k * lda + m]
@@ -936,7 +953,7 @@ struct DmaColK {
     const int kk = k + kr0 + i * S::NW * S::KPI;
     dma16(rs, img + (i * S::NW + w) * 512, (cv & (kk < K)) ? (unsigned)kk * ld2 + colb : OOB);
   }
-  __device__ void advance() { k += DBK; }
+  __device__ void advance() { k += DKT; }
 };
 
 // B = im2col of the bf16 NHWC input X: element (n = (r*S+s)*Cx + c, k = output pixel) = X[b][src(oh, ow, r, s)][c]
@@ -978,7 +995,7 @@ struct DmaWgradX {
     const unsigned off = (((unsigned)b * (unsigned)a.H + (unsigned)ih) * (unsigned)a.W + (unsigned)iw) * (unsigned)a.Cx * 2u + cb;
     dma16(rs, img + (i * S::NW + w) * 512, ok ? off : OOB);
   }
-  __device__ void advance() { k += DBK; }
+  __device__ void advance() { k += DKT; }
 };
 
 // 32x32x16 fragment (k-step ks of 16) from a DMA COL image: two transpose reads, k-rows kr and kr + 4
@@ -991,6 +1008,39 @@ __device__ __forceinline__ bf16x8 dcfrag(const __bf16* img, int row0, int ks, in
   const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)p);
   const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(p + 4 * ROWS));
   return __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// Fragment reads of the DMA main loop as inline asm: the compiler then neither sinks them to just ahead of their
+// MFMAs nor waits for the in-flight LDS-DMA before them (it cannot tell a transpose read of stage t from the DMA
+// writing stage t+1); the loop places its own counted lgkmcnt waits (LDS reads return in order).
+__device__ __forceinline__ unsigned lds_addr(const void* p) { return (unsigned)(uintptr_t)(const lds_void_t*)p; }
+__device__ __forceinline__ bf16x8 ads_b128(const __bf16* p) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr(p)));
+  return v;
+}
+__device__ __forceinline__ bf16x4 ads_tr(const __bf16* p) {
+  bf16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(lds_addr(p)));
+  return v;
+}
+__device__ __forceinline__ bf16x8 dfrag_asm(const __bf16* img, int row0, int ks, int lane) {
+  const int r = row0 + (lane & 15);
+  const int c = 4 * ks + (lane >> 4);
+  return ads_b128(img + r * DKT + ((c ^ dswz(r)) << 3));
+}
+template <int ROWS>
+__device__ __forceinline__ bf16x8 dcfrag_asm(const __bf16* img, int row0, int ks, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  const int kr = ks * 16 + (g >> 1) * 8 + (li >> 2);
+  const int col = row0 + (g & 1) * 16 + 4 * (li & 3);
+  const __bf16* p = img + kr * ROWS + (col ^ dcswz<ROWS>(kr));
+  const bf16x4 v0 = ads_tr(p), v1 = ads_tr(p + 4 * ROWS);
+  return __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N > 15 ? 15 : N));
 }
 
 template <int KIND, int ROWS, int NT, bool IS_A>
@@ -1015,7 +1065,7 @@ struct DmaLoader<B_WGRAD_SUBPIX, ROWS, NT, false> : DmaWgradX<ROWS, NT, MODE_SUB
 __device__ __forceinline__ bf16x8 dfrag(const __bf16* img, int row0, int ks, int lane) {
   const int r = row0 + (lane & 15);
   const int c = 4 * ks + (lane >> 4);
-  return *(const bf16x8*)(img + r * DBK + ((c ^ dswz(r)) << 3));
+  return *(const bf16x8*)(img + r * DKT + ((c ^ dswz(r)) << 3));
 }
 
 // one MFMA product step: 3xBF16 (lo*hi + hi*lo + hi*hi, small terms first) or plain bf16
@@ -1105,9 +1155,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   using IA = Img<BM, LA::COL>;
   using IB = Img<BN, LB::COL>;
   constexpr int BUF = IA::SIZE + IB::SIZE;
-  constexpr int DBUF = (BM + BN) * DBK;  // PREC 4: one stage of the A and B DMA images
+  constexpr int DBUF = (BM + BN) * DKT;  // PREC 4: one stage of the A and B DMA images
   constexpr int TM = BM / WGM / MF, TN = BN / WGN / MF;  // MFMA tiles per wave
-  __shared__ __attribute__((aligned(16))) __bf16 lds[(PREC == 4 && DBUF > BUF) ? 2 * DBUF : 2 * BUF];
+  __shared__ __attribute__((aligned(16))) __bf16 lds[(PREC == 4 && DNST * DBUF > 2 * BUF) ? DNST * DBUF : 2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WGN, wn = wid - wm * WGN;
@@ -1141,12 +1191,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   const int arow = wm * (BM / WGM), brow = wn * (BN / WGN);
 
   if constexpr (PREC == 4) {
-    // LDS-DMA main loop over 64-deep K-tiles, two stages: at the top of iteration t each wave waits for its own
-    // DMA of tile t (vmcnt 0), the barrier makes every wave's DMA of tile t visible and guarantees that every wave
-    // has finished reading stage (t+1)&1 (tile t-1; its fragment reads were all consumed by tile t-1's MFMAs), then
-    // the DMA of tile t+1 is issued into that stage and tile t is multiplied: the DMA has one compute phase to land.
-    // Only LDS-DMA loads are in flight in the loop (no VGPR-destination load the compiler would drain with them).
-    // ROW images (fwd / dgrad) feed 16x16x32 MFMAs, COL images (weight gradient) 32x32x16 MFMAs.
+    // LDS-DMA main loops. Only LDS-DMA loads are in flight in the loop (no VGPR-destination load the compiler would
+    // drain with them); fragment reads are inline asm with counted lgkmcnt waits (dfrag_asm). ROW images (fwd /
+    // dgrad) feed 16x16x32 MFMAs, COL images (weight gradient) 32x32x16 MFMAs.
     constexpr bool ACOL = AK == A_COLM, BCOL = BKIND == B_WGRAD_FWD || BKIND == B_WGRAD_SUBPIX;
     static_assert(ACOL == BCOL && MF == (ACOL ? 32 : 16), "DMA main loop: ROW x ROW (MF 16) or COL x COL (MF 32)");
     using DA = DmaLoader<AK == A_ROWK ? 0 : AK, BM, NT, true>;
@@ -1155,49 +1202,161 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
     DB db;
     da.init(a, (const __bf16*)a.A + bidx * a.sA, m0, kb, tid, bidx);
     db.init(a, (const __bf16*)a.B + bidx * a.sB, n0, kb, tid, bidx);
-    const int nt = ke > kb ? (ke - kb + DBK - 1) / DBK : 0;
-    auto issue = [&](__bf16* stage) {
+    const int nt = ke > kb ? (ke - kb + DKT - 1) / DKT : 0;
+    constexpr int NID = DA::S::NI + DB::S::NI;  // DMA instructions per thread per stage
+    auto issue = [&](__bf16* stage) {  // DMA of the loaders' current stage, then advance them
       da.prep(a);
       db.prep(a);
 #pragma unroll
       for (int i = 0; i < DA::S::NI; ++i) da.issue(a, stage, i);
 #pragma unroll
-      for (int i = 0; i < DB::S::NI; ++i) db.issue(a, stage + BM * DBK, i);
+      for (int i = 0; i < DB::S::NI; ++i) db.issue(a, stage + BM * DKT, i);
+      da.advance();
+      db.advance();
     };
     auto frag_a = [&](const __bf16* img, int row0, int ks) {
-      if constexpr (ACOL) return dcfrag<BM>(img, row0, ks, lane);
-      else return dfrag(img, row0, ks, lane);
+      if constexpr (ACOL) return dcfrag_asm<BM>(img, row0, ks, lane);
+      else return dfrag_asm(img, row0, ks, lane);
     };
     auto frag_b = [&](const __bf16* img, int row0, int ks) {
-      if constexpr (BCOL) return dcfrag<BN>(img, row0, ks, lane);
-      else return dfrag(img, row0, ks, lane);
+      if constexpr (BCOL) return dcfrag_asm<BN>(img, row0, ks, lane);
+      else return dfrag_asm(img, row0, ks, lane);
     };
+    constexpr int DKS = DKT / (MF == 32 ? 16 : 32);    // MFMA k-steps per stage
+    constexpr int RPS = (ACOL ? 2 : 1) * (TM + TN);  // LDS read instructions per k-step
+    auto barrier = [&]() {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+#if MVAE_DMA_RING
+    // 4-stage ring, 32-deep stages, fragments read one stage ahead. Phase t: wait for this wave's DMA of stage t+1
+    // (stage t+2's stays in flight), barrier (every wave's stage t+1 has landed; every wave has finished reading
+    // stage t-1, whose fragments it read during phase t-2), DMA stage t+3 into ring slot (t+3)&3 = (t-1)&3, read
+    // stage t+1's fragments, multiply stage t (fragments read during phase t-1). The DMA has two phases to land;
+    // the LDS reads run under the previous stage's MFMAs.
+    static_assert(DKT == 32 && DNST == 4, "ring geometry");
+    bf16x8 fa[2][DKS][TM], fb[2][DKS][TN];
+    auto read_stage = [&](int slot, int f, int ks) {
+      const __bf16* Ai = lds + slot * DBUF;
+      const __bf16* Bi = Ai + BM * DKT;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[f][ks][j] = frag_b(Bi, brow + j * MF, ks);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[f][ks][i] = frag_a(Ai, arow + i * MF, ks);
+    };
+    auto mma_stage = [&](int f, int ks) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(fa[f][ks][i], fb[f][ks][j], acc[i][j]);
+    };
+    // prologue: stages 0..2 in flight, stage 0 landed and read
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (q < nt) issue(lds + q * DBUF);
+    if (nt > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NID) : "memory");
+    else if (nt > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NID) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+    if (nt > 0) {
+#pragma unroll
+      for (int ks = 0; ks < DKS; ++ks) read_stage(0, 0, ks);
+    }
+    // t even / odd as two unrolled halves: the fragment register sets alternate without runtime indexing
+    auto phase = [&](int t, auto fcur) {
+      constexpr int F = decltype(fcur)::value;
+      if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NID) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      barrier();
+      if (t + 3 < nt) issue(lds + ((t + 3) & 3) * DBUF);
+      const bool more = t + 1 < nt;
+      if (more) read_stage((t + 1) & 3, F ^ 1, 0);
+      if (more) wait_lgkm<RPS>();
+      else wait_lgkm<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      mma_stage(F, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 1; ks < DKS; ++ks) {
+        if (more) read_stage((t + 1) & 3, F ^ 1, ks);
+        __builtin_amdgcn_sched_barrier(0);
+        mma_stage(F, ks);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    int t = 0;
+    for (; t + 1 < nt; t += 2) {
+      phase(t, std::integral_constant<int, 0>{});
+      phase(t + 1, std::integral_constant<int, 1>{});
+    }
+    if (t < nt) phase(t, std::integral_constant<int, 0>{});
+#else
+    // 2 stages of 64: at the top of iteration t each wave waits for its own DMA of stage t (vmcnt 0), the barrier
+    // makes every wave's DMA of stage t visible and guarantees that every wave has finished reading stage t-1, then
+    // the DMA of stage t+1 is issued into that slot and stage t is multiplied: the DMA has one phase to land.
     if (nt > 0) issue(lds);
     for (int t = 0; t < nt; ++t) {
       __bf16* cur = lds + (t & 1) * DBUF;
+#if MVAE_DMA_EXP != 1  // (experiment 1: no wait for the DMA -- timing only, wrong results)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (t + 1 < nt) {
+#endif
+      barrier();
+      __bf16* nxt = lds + ((t + 1) & 1) * DBUF;
+      const bool more = t + 1 < nt;
+      // (measured, c5 shapes: the spread issue gains 3-6 % on the weight-gradient loops and loses 0-3 % on fwd / dgrad)
+      constexpr bool SPREAD = MVAE_DMA_SPREAD == 2 || (MVAE_DMA_SPREAD == 1 && ACOL);
+#if MVAE_DMA_EXP != 2  // (experiment 2: no DMA in the loop -- timing only, wrong results)
+      // SPREAD: the stage's DMA instructions are issued in DKS slices, one ahead of each k-step's MFMAs, instead of
+      // in one burst after the barrier
+      if (SPREAD && more) {
+        da.prep(a);
+        db.prep(a);
+      }
+      if (!SPREAD && more) issue(nxt);
+#endif
+      const __bf16* Ai = cur;
+      const __bf16* Bi = cur + BM * DKT;
+      // fragments double-buffered over the k-steps: the reads of k-step ks+1 are issued ahead of k-step ks's MFMAs
+      bf16x8 fa[2][TM], fb[2][TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[0][j] = frag_b(Bi, brow + j * MF, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[0][i] = frag_a(Ai, arow + i * MF, 0);
+#pragma unroll
+      for (int ks = 0; ks < DKS; ++ks) {
+        const int c = ks & 1;
+        if (ks + 1 < DKS) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) fb[c ^ 1][j] = frag_b(Bi, brow + j * MF, ks + 1);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) fa[c ^ 1][i] = frag_a(Ai, arow + i * MF, ks + 1);
+        }
+        if (ks + 1 < DKS) wait_lgkm<RPS>();  // k-step ks's reads are done; ks+1's stay in flight
+        else wait_lgkm<0>();
+        __builtin_amdgcn_sched_barrier(0);
+#if MVAE_DMA_EXP != 2
+        if (SPREAD && more) {
+#pragma unroll
+          for (int q = ks * NID / DKS; q < (ks + 1) * NID / DKS; ++q) {
+            if (q < DA::S::NI) da.issue(a, nxt, q);
+            else db.issue(a, nxt + BM * DKT, q - DA::S::NI);
+          }
+        }
+#endif
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(fa[c][i], fb[c][j], acc[i][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#if MVAE_DMA_EXP != 2
+      if (SPREAD && more) {
         da.advance();
         db.advance();
-        issue(lds + ((t + 1) & 1) * DBUF);
       }
-      const __bf16* Ai = cur;
-      const __bf16* Bi = cur + BM * DBK;
-#pragma unroll
-      for (int ks = 0; ks < DBK / (MF == 32 ? 16 : 32); ++ks) {
-        bf16x8 bh[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bh[j] = frag_b(Bi, brow + j * MF, ks);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const bf16x8 ah = frag_a(Ai, arow + i * MF, ks);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(ah, bh[j], acc[i][j]);
-        }
-      }
+#endif
     }
+#endif
   } else {
   LA la;
   LB lb;
@@ -1717,8 +1876,7 @@ void launch_dma(GemmArgs& a, hipStream_t st, int cfg) {
     case T256x128: launch_cfg<T256x128, AK, 4, B_ROWK, 4, 4>(a, st); break;
     case T128x256: launch_cfg<T128x256, AK, 4, B_ROWK, 4, 4>(a, st); break;
     case T128x128: launch_cfg<T128x128, AK, 4, B_ROWK, 4, 4>(a, st); break;
-    case T128x16: launch_cfg<T128x16, AK, 4, B_ROWK, 4, 4>(a, st); break;
-    default: launch_cfg<T64x64, AK, 4, B_ROWK, 4, 4>(a, st); break;
+    default: launch_cfg<T64x64, AK, 4, B_ROWK, 4, 4>(a, st); break;  // (and the skinny-N 128x16 choice)
   }
 }
 

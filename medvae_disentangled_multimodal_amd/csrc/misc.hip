@@ -156,6 +156,39 @@ __global__ void __launch_bounds__(256) pack_bf16_kernel(const float4* __restrict
   }
 }
 
+// packed bf16 of x [rows][n] (n % 4 == 0, row stride n) plus the fp64 column sums of the fp32 values per chunk of
+// rows: part[chunk][n] (the conv bias gradient of a dy that the bf16-mixed GEMMs read packed: one pass over dy for
+// both). 256 threads = 64 column groups of 4 x 4 row phases; fixed summation order.
+__global__ void __launch_bounds__(256) pack_colsum_kernel(const float* __restrict__ x, uint2* __restrict__ y,
+                                                          long long rows, int n, int rows_per_chunk,
+                                                          double* __restrict__ part) {
+  __shared__ double sh[4][64][4];
+  const int cg = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const int c = cg * 4;
+  const long long r0 = (long long)blockIdx.y * rows_per_chunk;
+  const long long r1 = std::min<long long>(rows, r0 + rows_per_chunk);
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (c < n) {
+    for (long long r = r0 + rg; r < r1; r += 4) {
+      const float4 v = *(const float4*)(x + r * n + c);
+      y[(r * n + c) >> 2] = uint2{pk_bf16x2(v.x, v.y), pk_bf16x2(v.z, v.w)};
+      a0 += v.x; a1 += v.y; a2 += v.z; a3 += v.w;
+    }
+  }
+  sh[rg][threadIdx.x & 63][0] = a0;
+  sh[rg][threadIdx.x & 63][1] = a1;
+  sh[rg][threadIdx.x & 63][2] = a2;
+  sh[rg][threadIdx.x & 63][3] = a3;
+  __syncthreads();
+  if (rg == 0 && c < n) {
+    double* o = part + (long long)blockIdx.y * n + c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      o[e] = sh[0][threadIdx.x][e] + sh[1][threadIdx.x][e] + sh[2][threadIdx.x][e] + sh[3][threadIdx.x][e];
+  }
+}
+
 // column sums: part[chunk][n] = sum over rows in chunk ; then out[n] += sum_chunks (fixed order)
 __global__ void __launch_bounds__(256) colsum_partial_kernel(const float* __restrict__ x, long long rows, int n,
                                                              long long ld, int rows_per_chunk,
@@ -239,6 +272,26 @@ int mvae_pack_bf16(const float* x, void* y, long long n, void* stream) {
   }
   hipLaunchKernelGGL(pack_bf16_kernel, dim3(egrid(n / 8)), dim3(256), 0, (hipStream_t)stream, (const float4*)x, (uint4*)y,
                      n / 8);
+  return launch_status();
+}
+
+// y = packed bf16 of x [rows][n] (fp32, row stride n) and out[n] = beta*out[n] + sum_rows x (the conv bias gradient,
+// fp64 partials in a fixed order): the bf16-mixed mode's output-gradient pack (MVAE_CONV_BF16) and bias gradient in
+// one pass over dy. Workspace: mvae_bias_grad_workspace_bytes(rows, n).
+int mvae_pack_bf16_colsum(const float* x, void* y, long long rows, int n, float* out, float beta, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  if (rows <= 0 || n <= 0 || (n & 3) || ((uintptr_t)x & 15) || ((uintptr_t)y & 7)) {
+    set_error("pack_bf16_colsum: n %% 4 == 0, 16-B aligned x, 8-B aligned y");
+    return MVAE_EINVAL;
+  }
+  const int chunks = colsum_chunks(rows, n);
+  if (workspace_bytes < (size_t)chunks * n * sizeof(double)) { set_error("pack_bf16_colsum: workspace"); return MVAE_EWORKSPACE; }
+  const int rpc = (int)((rows + chunks - 1) / chunks);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(pack_colsum_kernel, dim3((n / 4 + 63) / 64, chunks), dim3(256), 0, st, x, (uint2*)y, rows, n, rpc,
+                     (double*)workspace);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((n + 255) / 256), dim3(256), 0, st, (const double*)workspace, chunks, n,
+                     out, beta);
   return launch_status();
 }
 

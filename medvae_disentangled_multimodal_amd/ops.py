@@ -346,12 +346,22 @@ def _conv_fwd_bf16(x, w, b, res, g, y, n, c, h, wd, co, ho, wo, sub, alg, ref, g
     return y
 
 
-def pack_dy(dy: torch.Tensor, g: ConvGeom) -> Optional[torch.Tensor]:
-    """dy as packed bf16 for the input-gradient GEMM of the bf16-mixed mode, or None when that path does not apply."""
+def pack_dy(dy: torch.Tensor, g: ConvGeom, bias_out=None, beta: float = 1.0):
+    """dy as packed bf16 for the backward GEMMs of the bf16-mixed mode, or None when that path does not apply.
+    bias_out: also accumulate the conv bias gradient (beta * bias_out + column sums of the fp32 dy) from the same pass
+    (mvae_pack_bf16_colsum). Returns (packed dy or None, whether the bias gradient was produced)."""
     if not _bf16_dma() or g.pointwise or dy.dim() != 4 or dy.shape[1] % 8 or g.kh * g.kw > 32 or not _al16(dy) or \
             not dy.is_contiguous(memory_format=CL):
-        return None
-    return pack_bf16(dy, "dybf")
+        return None, False
+    if bias_out is None:
+        return pack_bf16(dy, "dybf"), False
+    n, co, ho, wo = dy.shape
+    rows = n * ho * wo
+    out = ARENA.get("dybf", dy.numel() * 2, dy.device)
+    ws = ARENA.get("bias", _lib.query("mvae_bias_grad_workspace_bytes", rows, co), dy.device)
+    _lib.call("mvae_pack_bf16_colsum", dy.data_ptr(), out.data_ptr(), rows, co, bias_out.data_ptr(), float(beta),
+              ws.data_ptr(), ws.numel(), _stream(dy))
+    return out, True
 
 
 def split_dy(dy: torch.Tensor) -> Optional[torch.Tensor]:
@@ -604,20 +614,30 @@ class Conv2dFn(torch.autograd.Function):
         link = ctx.gn_link
         if link is not None:
             link.part = link.dx = None  # partials of an earlier pass are never reused
-        dyb = pack_dy(dy, g) if (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]) else None
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        bias_done = False
+        dyb = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            # bf16-mixed: pack dy once for both GEMMs; the bias gradient comes out of the same pass
+            bt = _main_grad(ctx.bias_ref) if want_b else None
+            if want_b and bt is None:
+                db_ret = torch.empty(dy.shape[1], device=dy.device, dtype=torch.float32)
+            dyb, bias_done = pack_dy(dy, g, bt if bt is not None else db_ret, 1.0 if bt is not None else 0.0)
+            if not bias_done:
+                db_ret = None
         dys = split_dy(dy) if not g.pointwise and not _subpixel_upsample(g) and dyb is None else None
         if ctx.needs_input_grad[0]:
             dx = conv2d_dgrad_raw(dy, w, x.shape, g, link if ctx.x_sink is None else None, dys=dys, dyb=dyb)
             if ctx.x_sink is not None and ctx.x_sink.park(dx):
                 dx = None
-        bias_done = False
-        want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             tgt = _main_grad(ctx.weight_ref)
-            btgt = _main_grad(ctx.bias_ref) if want_b else None
+            btgt = _main_grad(ctx.bias_ref) if want_b and not bias_done else None
+            want_b_w = want_b and not bias_done
             xs, xb16 = ctx.x_split, ctx.x_bf16
-            if tgt is not None and (not want_b or btgt is not None):
-                bias_done = conv2d_wgrad_raw(dy, x, tgt, 1.0, g, btgt, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16)
+            if tgt is not None and (not want_b_w or btgt is not None):
+                fused = conv2d_wgrad_raw(dy, x, tgt, 1.0, g, btgt, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16)
+                bias_done = bias_done or fused
             elif tgt is not None:
                 conv2d_wgrad_raw(dy, x, tgt, 1.0, g, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16)
             else:

@@ -3,7 +3,7 @@
 TAG=${1:-dma}; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/$TAG
-timeout -k 10 600 python -u -m pytest tests/test_gpu_bf16_dma.py tests/test_gpu_c5.py tests/test_gpu_bench_geometry.py tests/test_gpu_parity.py -m gpu -v -x --timeout 200 --timeout-method thread > gpurun_out/$TAG/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest ${DMA_TESTS:-tests/test_gpu_bf16_dma.py tests/test_gpu_c5.py tests/test_gpu_bench_geometry.py tests/test_gpu_parity.py} -m gpu -v -x --timeout 200 --timeout-method thread > gpurun_out/$TAG/pytest.log 2>&1
 rc=$?; grep -E "PASS|FAIL|Error|error|passed|failed" gpurun_out/$TAG/pytest.log | tail -30
 [ $rc -eq 0 ] || exit $rc
 for c in "$@"; do
