@@ -63,6 +63,10 @@ int mvae_set_dropout_salt(const void* salt_dev);
  * into LDS by DMA (no staging registers or conversion) in 64-deep K-tiles -- Lightning's bf16-mixed convolution
  * (configs/config.yaml precision, main.py:86-99) with fp32 accumulation and fp32 output. */
 #define MVAE_CONV_BF16 128
+/* mode | MVAE_CONV_PLANAR (modes 0 and 2, default 3xBF16 math mode): the gathered operand and w are planar 3xBF16 --
+ * a bf16 hi plane (hi = bf16(v)) followed by the lo plane (lo = bf16(v - hi)) of the same element count
+ * (mvae_split_planar, GroupNorm y_split 3, weight prep split 3) -- staged by LDS-DMA into hi and lo images. */
+#define MVAE_CONV_PLANAR 256
 int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y,
                      int nb, int h, int w_, int cin, int cout, int kh, int kw, int stride, int pad_t,
                      int pad_l, int ho, int wo, int mode, void* stream);
@@ -159,6 +163,11 @@ int mvae_pack_bf16(const float* x, void* y, long long n, void* stream);
  * out[n] = beta*out[n] + sum_rows dy (fp64 partials, fixed order; workspace mvae_bias_grad_workspace_bytes). */
 int mvae_pack_bf16_colsum(const float* x, void* y, long long rows, int n, float* out, float beta, void* workspace,
                           size_t workspace_bytes, void* stream);
+/* Planar 3xBF16 (MVAE_CONV_PLANAR) of n fp32 values (n % 4 == 0): y = [hi plane: n bf16][lo plane: n bf16]. */
+int mvae_split_planar(const float* x, void* y, long long n, void* stream);
+/* mvae_pack_bf16_colsum writing dy planar 3xBF16 instead of packed bf16. */
+int mvae_split_planar_colsum(const float* x, void* y, long long rows, int n, float* out, float beta, void* workspace,
+                             size_t workspace_bytes, void* stream);
 
 /* Weight re-layouts for the input gradient: KRSC -> [cin][kh][kw][cout]; and the 4x4 tap-summed
  * kernel [cin][4][4][cout] for Upsample's conv (encoder_decoder.py:205-209). */
@@ -192,7 +201,8 @@ int mvae_softmax_rows_bwd(const float* y, const float* dy, float* dx, long long 
  * gradient of x from the block's other branch (ResnetBlock / AttnBlock residual, encoder_decoder.py:
  * 107,170), summed into dx in the same pass (replaces autograd's separate gradient add).
  * y_split = 1: y is written in the pre-split 3xBF16 operand layout (mvae_split_bf16) for a following
- * convolution (MVAE_CONV_XSPLIT); the backward never reads y. */
+ * convolution (MVAE_CONV_XSPLIT); 2: packed bf16 (MVAE_CONV_BF16); 3: planar 3xBF16 (MVAE_CONV_PLANAR) -- the
+ * backward never reads y. */
 int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* beta, float* y, float* mean,
                              float* rstd, int nb, int hw, int c, int groups, float eps, int silu,
                              float drop_p, unsigned long long seed, int y_split, void* workspace,

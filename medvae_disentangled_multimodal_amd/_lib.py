@@ -43,6 +43,8 @@ SIGNATURES = {
     "mvae_split_bf16": (I, [P, P, L, P]),
     "mvae_pack_bf16": (I, [P, P, L, P]),
     "mvae_pack_bf16_colsum": (I, [P, P, L, I, P, F, P, Z, P]),
+    "mvae_split_planar": (I, [P, P, L, P]),
+    "mvae_split_planar_colsum": (I, [P, P, L, I, P, F, P, Z, P]),
     "mvae_conv2d_upsample_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, P]),
     "mvae_conv_weight_upsample_fwd": (I, [P, P, I, I, I, P]),
     "mvae_conv2d_wgrad_upsample_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, P, Z, P]),

@@ -132,11 +132,15 @@ static int conv2d_impl(const float* x, const float* w, const float* bias, const 
                        size_t ws_bytes) {
   const bool presplit = (mode & MVAE_CONV_WSPLIT) != 0;
   const bool xsplit = (mode & MVAE_CONV_XSPLIT) != 0;
-  const bool bf = (mode & MVAE_CONV_BF16) != 0;
-  mode &= ~(MVAE_CONV_WSPLIT | MVAE_CONV_XSPLIT | MVAE_CONV_BF16);
-  if (bf && (presplit || xsplit || mode == 1 || cin % 8 || !al16(x) || !al16(w) || kh * kw > 32 || math_mode() != MATH_BF16)) {
-    set_error("conv2d: bf16-packed operands need the bf16 math mode, mode 0 or 2, cin %% 8 == 0, <= 32 taps, 16-B "
-              "aligned x, w");
+  const bool pk = (mode & MVAE_CONV_BF16) != 0;      // packed bf16 x (dy) and w: PREC 4
+  const bool pln = (mode & MVAE_CONV_PLANAR) != 0;   // planar 3xBF16 x (dy) and w: PREC 5
+  const bool bf = pk || pln;                         // LDS-DMA staged operands (bf16 element offsets)
+  mode &= ~(MVAE_CONV_WSPLIT | MVAE_CONV_XSPLIT | MVAE_CONV_BF16 | MVAE_CONV_PLANAR);
+  if (bf && ((pk && pln) || presplit || xsplit || mode == 1 || cin % 8 || !al16(x) || !al16(w) || kh * kw > 32 ||
+             math_mode() != (pln ? MATH_3XBF16 : MATH_BF16) ||
+             (pln && (long long)nb * h * wd * cin * 2 >= (1LL << 32)))) {
+    set_error("conv2d: DMA-staged operands need the matching math mode (packed bf16: bf16, planar: 3xBF16), mode 0 "
+              "or 2, cin %% 8 == 0, <= 32 taps, 16-B aligned x, w, a hi plane < 4 GiB");
     return MVAE_EINVAL;
   }
   if (xsplit && mode == 1) { set_error("conv2d: a pre-split input needs mode 0 or 2"); return MVAE_EINVAL; }
@@ -176,6 +180,10 @@ static int conv2d_impl(const float* x, const float* w, const float* bias, const 
     a.res = residual ? residual + (long long)b0 * (out_img / 4) : nullptr; a.ldr = cout;
     a.alpha = 1.f; a.beta = 0.f;
     a.a_bytes = (unsigned)(in_img * n / (bf ? 2 : 1)); a.b_bytes = (unsigned)(wbytes / (bf ? 2 : 1));
+    if (pln) {  // lo planes: one whole hi plane after the hi plane
+      a.a_lo = (unsigned)(in_img / 2 * nb);
+      a.b_lo = (unsigned)(wbytes / 2);
+    }
     a.c_bytes = (unsigned)(out_img * n); a.r_bytes = a.c_bytes;
     a.H = h; a.W = wd; a.Cx = cin; a.Ho = ho; a.Wo = wo; a.R = kh; a.S = kw;
     a.perm_rs = (v && cin % (bf ? DBK : BK) == 0 && kh * kw > 1 && kperm_enabled()) ? kh * kw : 1;
@@ -205,9 +213,8 @@ static int conv2d_impl(const float* x, const float* w, const float* bias, const 
       set_error("conv2d_gnstats: needs the vector (16-B) operand path");
       return MVAE_EINVAL;
     }
-    if (bf) {  // packed bf16 x (dy) and weights: LDS-DMA main loop
-      if (mode == 0) conv_dma(A_CONV_FWD, a, st, cfg);
-      else conv_dma(A_CONV_DGRAD, a, st, cfg);
+    if (bf) {  // DMA-staged x (dy) and weights: LDS-DMA main loop
+      conv_dma(mode == 0 ? A_CONV_FWD : A_CONV_DGRAD, a, st, cfg, pln ? 5 : 4);
     } else if (xsplit && mode == 2) {  // dy (the gathered operand of the input gradient) holds split4_bf16 groups
       if (presplit) launch_big<A_CONV_DGRAD_SPLIT, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
       else launch_big<A_CONV_DGRAD_SPLIT, 4, B_ROWK, 4>(a, st, cfg);
@@ -261,12 +268,18 @@ int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, 
   const int chunk = (int)std::min<long long>(nb, MAX_DESC_BYTES / std::max(in_img, out_img));
   hipStream_t st = (hipStream_t)stream;
   const int hc = h / 2, wc = wd / 2;
-  // w_split 4: dy and wt are packed bf16 (bf16-mixed mode, LDS-DMA main loop)
-  const bool bf = (w_split & 4) != 0;
-  if (bf && (w_split != 4 || cout % 8 || !al16(dy) || !al16(wt) || math_mode() != MATH_BF16)) {
-    set_error("dgrad_stride2: bf16-packed operands need the bf16 math mode, cout %% 8 == 0, aligned dy / wt");
+  // w_split 4: dy and wt are packed bf16 (bf16-mixed mode); 8: planar 3xBF16 (LDS-DMA main loop)
+  const bool pln = w_split == 8;
+  const bool bf = w_split == 4 || pln;
+  if (bf && (cout % 8 || !al16(dy) || !al16(wt) || math_mode() != (pln ? MATH_3XBF16 : MATH_BF16))) {
+    set_error("dgrad_stride2: DMA-staged operands need the matching math mode, cout %% 8 == 0, aligned dy / wt");
     return MVAE_EINVAL;
   }
+  if (bf && workspace_bytes < (size_t)kh * kw * cin * cout * (pln ? 4 : 2)) {
+    set_error("dgrad_stride2: workspace too small");
+    return MVAE_EWORKSPACE;
+  }
+  const long long wt_plane = (long long)cin * kh * kw * cout;  // planar wt: lo plane this many elements later
   float* wcls = workspace;
   bool empty_class = false;  // a kernel too small to reach every parity: those dx pixels are 0
   for (int p = 0; p < 2; ++p) {
@@ -291,10 +304,12 @@ int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, 
       for (int b = 0; b < ns; ++b) tp[a * ns + b] = rl[a] * kw + sl[b];
     if (nt > 4) { set_error("dgrad_stride2: class with more than 4 taps"); return MVAE_EINVAL; }
     const long long tot = (long long)cin * nt * cout;
-    if (bf)
-      hipLaunchKernelGGL(tap_select_bf16_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 8192)), dim3(256),
-                         0, st, (const __bf16*)wt, (__bf16*)wcls, cin, kh * kw, cout, nt,
-                         make_int4(tp[0], tp[1], tp[2], tp[3]));
+    if (bf) {
+      for (int pl = 0; pl < (pln ? 2 : 1); ++pl)  // planar: the class's hi block, then its lo block
+        hipLaunchKernelGGL(tap_select_bf16_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 8192)),
+                           dim3(256), 0, st, (const __bf16*)wt + pl * wt_plane, (__bf16*)wcls + pl * tot, cin, kh * kw,
+                           cout, nt, make_int4(tp[0], tp[1], tp[2], tp[3]));
+    }
     else
       hipLaunchKernelGGL(tap_select_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 8192)), dim3(256), 0,
                          st, wt, wcls, cin, kh * kw, cout, nt, make_int4(tp[0], tp[1], tp[2], tp[3]));
@@ -312,6 +327,10 @@ int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, 
       a.C = dx + (long long)b0 * (out_img / 4); a.ldc = cin;
       a.alpha = 1.f; a.beta = 0.f;
       a.a_bytes = (unsigned)(in_img * n / (bf ? 2 : 1)); a.b_bytes = (unsigned)(tot * (bf ? 2 : 4));
+      if (pln) {
+        a.a_lo = (unsigned)(in_img / 2 * nb);
+        a.b_lo = (unsigned)(tot * 2);
+      }
       a.c_bytes = (unsigned)(out_img * n); a.r_bytes = 0;
       a.H = ho; a.W = wo; a.Cx = cout; a.Ho = hc; a.Wo = wc; a.R = nr; a.S = ns;
       a.perm_rs = (v && cout % (bf ? DBK : BK) == 0 && nt > 1 && kperm_enabled()) ? nt : 1;
@@ -319,7 +338,7 @@ int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, 
       a.stride = 1; a.stride_shift = 0; a.pad_t = pt; a.pad_l = pl;
       a.sub_w2 = wd; a.sub_par = cls; a.out_remap = 1;
       const int cfg = choose_tile(a, v, false);
-      if (bf) conv_dma(A_CONV_FWD, a, st, cfg);
+      if (bf) conv_dma(A_CONV_FWD, a, st, cfg, pln ? 5 : 4);
       else if ((w_split & 3) == 3) launch_big<A_CONV_FWD_SPLIT, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
       else if (w_split & 2) launch_big<A_CONV_FWD_SPLIT, 4, B_ROWK, 4>(a, st, cfg);
       else if (w_split) launch_big<A_CONV_FWD, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
@@ -328,7 +347,7 @@ int mvae_conv2d_dgrad_stride2_nhwc(const float* dy, const float* wt, float* dx, 
       const int rc = gemm_finish(a, st);
       if (rc) return rc;
     }
-    wcls = bf ? (float*)((__bf16*)wcls + tot) : wcls + tot;
+    wcls = bf ? (float*)((__bf16*)wcls + (pln ? 2 : 1) * tot) : wcls + tot;
   }
   return MVAE_OK;
 }
@@ -354,10 +373,11 @@ int mvae_conv2d_upsample_nhwc(const float* x, const float* w4, const float* bias
   const int chunk = (int)std::min<long long>(nb, MAX_DESC_BYTES / std::max(in_img, out_img));
   hipStream_t st = (hipStream_t)stream;
   const bool v = (cin % 4 == 0) && al16(x) && al16(w4);
-  // w_split 2: x and w4 are packed bf16 (bf16-mixed mode, LDS-DMA main loop)
-  const bool bf = w_split == 2;
-  if (bf && (cin % 8 || !v || math_mode() != MATH_BF16)) {
-    set_error("conv2d_upsample: bf16-packed operands need the bf16 math mode, cin %% 8 == 0, aligned x / w4");
+  // w_split 2: x and w4 are packed bf16 (bf16-mixed mode); 3: planar 3xBF16 (LDS-DMA main loop)
+  const bool pln = w_split == 3;
+  const bool bf = w_split == 2 || pln;
+  if (bf && (cin % 8 || !v || math_mode() != (pln ? MATH_3XBF16 : MATH_BF16))) {
+    set_error("conv2d_upsample: DMA-staged operands need the matching math mode, cin %% 8 == 0, aligned x / w4");
     return MVAE_EINVAL;
   }
   if (w_split && !v) { set_error("conv2d_upsample: pre-split weights need cin %% 4 == 0"); return MVAE_EINVAL; }
@@ -373,6 +393,10 @@ int mvae_conv2d_upsample_nhwc(const float* x, const float* w4, const float* bias
     a.res = residual ? residual + (long long)b0 * (out_img / 4) : nullptr; a.ldr = cout; a.sR = 0;
     a.alpha = 1.f; a.beta = 0.f;
     a.a_bytes = (unsigned)(in_img * n / (bf ? 2 : 1)); a.b_bytes = (unsigned)(wbytes / 4 / (bf ? 2 : 1));
+    if (pln) {
+      a.a_lo = (unsigned)(in_img / 2 * nb);
+      a.b_lo = (unsigned)(wbytes / 2);
+    }
     a.c_bytes = (unsigned)(out_img * n); a.r_bytes = a.c_bytes;
     a.H = h; a.W = wd; a.Cx = cin; a.Ho = h; a.Wo = wd; a.R = 2; a.S = 2;
     a.perm_rs = (v && cin % (bf ? DBK : BK) == 0 && kperm_enabled()) ? 4 : 1;
@@ -380,7 +404,7 @@ int mvae_conv2d_upsample_nhwc(const float* x, const float* w4, const float* bias
     a.stride = 1; a.stride_shift = 0; a.pad_t = 1; a.pad_l = 1;
     a.sub_w2 = 2 * wd; a.sub_par = 0; a.out_remap = 1;
     const int cfg = choose_tile(a, v, false);
-    if (bf) conv_dma(A_CONV_SUBPIX, a, st, cfg);
+    if (bf) conv_dma(A_CONV_SUBPIX, a, st, cfg, pln ? 5 : 4);
     else if (w_split) launch_big<A_CONV_SUBPIX, 4, B_ROWK_SPLIT, 4>(a, st, cfg);
     else if (v) launch_big<A_CONV_SUBPIX, 4, B_ROWK, 4>(a, st, cfg);
     else launch_small<A_CONV_SUBPIX, 1, B_ROWK, 1>(a, st, cfg);

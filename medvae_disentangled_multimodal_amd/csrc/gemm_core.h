@@ -69,6 +69,7 @@ constexpr int MVAE_CONV_WSPLIT = 16;  // conv mode flag: weights hold split4_bf1
 constexpr int MVAE_CONV_XSPLIT = 32;  // conv mode flag: the input activation x holds split4_bf16 groups
 constexpr int MVAE_CONV_DYSPLIT = 64;  // wgrad mode flag: the output gradient dy holds split4_bf16 groups
 constexpr int MVAE_CONV_BF16 = 128;    // conv mode flag: the gathered operand and the weights are packed bf16 (PREC 4)
+constexpr int MVAE_CONV_PLANAR = 256;  // conv mode flag: ... are planar 3xBF16 (bf16 hi plane, then lo plane; PREC 5)
 
 // Exact division by a runtime constant d for 0 <= n < 2^31 (Granlund-Montgomery, N = 31):
 // q = (n * m) >> (31 + l), l = ceil(log2 d), m = floor(2^(31+l) / d) + 1 (< 2^32).
@@ -97,6 +98,7 @@ struct GemmArgs {
   float* ws;  // split partials [batch][splits][M][N]
   float* bias_ws;  // wgrad only: per-split row sums of A = dY^T (the conv bias gradient) [splits][M]
   unsigned a_bytes, b_bytes, c_bytes, r_bytes;  // descriptor ranges (per batch entry)
+  unsigned a_lo = 0, b_lo = 0;  // PREC 5: byte offset of the operand's lo plane from its hi plane
   // gather geometry: source X is [nb][H][W][Cx]; output pixels are [nb][Ho][Wo]
   int H, W, Cx, Ho, Wo, R, S, stride, stride_shift, pad_t, pad_l;
   int tiles_m, tiles_n;
@@ -751,112 +753,115 @@ struct LoadWgradX {
 };
 
 // ------------------------------------------------------------------------------------------
-// PREC 4: bf16 operands STORED as bf16 in HBM (the bf16-mixed mode's conv inputs, weights and output gradients are
-// packed by their producers), staged by LDS-DMA (buffer_load_dwordx4 ... lds): no staging registers, no VALU split,
-// no ds_write. Stage depth DKT (32 in the 4-stage ring, 64 in the 2-stage loop); ROW images [ROWS][DKT] bf16,
-// filled lane-linearly (one DMA instruction = 1 KB = DPR rows, lane l -> row l / DCH, 16-B slot l % DCH) and
-// swizzled on the SOURCE side: physical slot p of row r holds the row's logical 8-element chunk p ^ dswz(r), and
-// fragment reads apply the same involution (ds_read_b128 lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...
-// then hit 16 distinct 16-B bank windows: 64-B rows use [0,3,2,1][(r >> 2) & 3], 128-B rows (r >> 1) & 7).
+// LDS-DMA operand staging (buffer_load_dwordx4 ... lds): no staging registers, no VALU split, no ds_write.
+//   PREC 4 (bf16-mixed): operands STORED as packed bf16 by their producers; 64-deep stages.
+//   PREC 5 (3xBF16): operands stored PLANAR -- a bf16 hi plane (hi = bf16(x)) followed, GemmArgs::a_lo / b_lo bytes
+//          later, by the lo plane (lo = bf16(x - hi)) -- each plane DMA'd into its own LDS image; 32-deep stages.
+// ROW images [ROWS][KT] bf16, filled lane-linearly (one DMA instruction = 1 KB = 1024 / (2 KT) rows, lane l -> row
+// l / (KT/8), 16-B slot l % (KT/8)) and swizzled on the SOURCE side: physical slot p of row r holds the row's logical
+// 8-element chunk p ^ dswz(r), and fragment reads apply the same involution (ds_read_b128 lane groups {0-3,12-15,
+// 20-27}, {4-11,16-19,28-31}, ... then hit 16 distinct 16-B bank windows: 128-B rows use (r >> 1) & 7, 64-B rows
+// [0,3,2,1][(r >> 2) & 3]).
 // ------------------------------------------------------------------------------------------
 constexpr int DBK = 64;  // split-K granularity (whole stages of either loop)
-#ifndef MVAE_DMA_EXP
-#define MVAE_DMA_EXP 0
-#endif
-#ifndef MVAE_DMA_RING
-#define MVAE_DMA_RING 0
-#endif
 #ifndef MVAE_DMA_SPREAD  // 1: COL (weight-gradient) loops spread their DMA issue over the k-steps; 2: every loop
 #define MVAE_DMA_SPREAD 1
 #endif
-constexpr int DKT = MVAE_DMA_RING ? 32 : 64;  // K depth of one DMA stage
-constexpr int DCH = DKT / 8;                  // 16-B chunks per ROW-image row
-constexpr int DPR = 64 / DCH;                 // rows per 1-KB DMA piece
-constexpr int DNST = MVAE_DMA_RING ? 4 : 2;   // LDS stages
-__device__ __forceinline__ int dswz(int r) { return DKT == 64 ? (r >> 1) & 7 : (4 - ((r >> 2) & 3)) & 3; }
+template <int KT>
+__device__ __forceinline__ int dswz(int r) { return KT == 64 ? (r >> 1) & 7 : (4 - ((r >> 2) & 3)) & 3; }
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// (permuted) stage starting at k (k % DKT == 0): channel chunk t / RS of tap t % RS, DKT channels wide
-__device__ __forceinline__ int kperm64(const GemmArgs& a, int k) {
-  const int t = k / DKT;
+// (permuted) stage starting at k (k % KT == 0): channel chunk t / RS of tap t % RS, KT channels wide
+template <int KT>
+__device__ __forceinline__ int kperm_dma(const GemmArgs& a, int k) {
+  const int t = k / KT;
   const int chunk = mdiv(t, a.mg_rs);
-  return (t - chunk * a.perm_rs) * a.Cx + chunk * DKT;
+  return (t - chunk * a.perm_rs) * a.Cx + chunk * KT;
 }
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, __bf16* dst, unsigned off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)dst, 16, off, 0, 0, 0);
 }
 
-// Piece q of a ROWS-row image (DPR rows, 1 KB) is filled by wave (q % (NT/64)) as its instruction q / (NT/64); with
-// an even wave count a lane's logical chunk (slot ^ dswz(row)) is the same for all its pieces.
-template <int ROWS, int NT>
+// Piece q of a ROWS-row image (1 KB) is filled by wave (q % (NT/64)) as its instruction q / (NT/64); with an even
+// wave count a lane's logical chunk (slot ^ dswz(row)) is the same for all its pieces.
+template <int ROWS, int NT, int KT>
 struct DmaShape {
   static constexpr int NW = NT / 64;
-  static constexpr int NI = ROWS * DKT / (NT * 8);  // DMA instructions per thread per stage
-  static_assert(NI >= 1 && NI * NT * 8 == ROWS * DKT && NW % 2 == 0, "DMA image shape");
+  static constexpr int CH = KT / 8;    // 16-B chunks per row
+  static constexpr int PR = 64 / CH;   // rows per piece
+  static constexpr int NI = ROWS * KT / (NT * 8);  // DMA instructions per thread per stage and plane
+  static_assert(NI >= 1 && NI * NT * 8 == ROWS * KT && NW % 2 == 0, "DMA image shape");
 };
+template <int KT>
 __device__ __forceinline__ int dma_chunk(int lane, int w) {
-  const int row = w * DPR + lane / DCH;  // any of the lane's rows: the swizzle is the same
-  return (lane % DCH) ^ dswz(row);
+  const int row = w * (512 / KT) + lane / (KT / 8);  // any of the lane's rows: the swizzle is the same
+  return (lane % (KT / 8)) ^ dswz<KT>(row);
+}
+// descriptors of the hi plane (or the packed bf16 operand) and of the lo plane lo_off bytes later
+__device__ __forceinline__ void plane_rsrc(__amdgpu_buffer_rsrc_t (&rs)[2], const __bf16* p, unsigned bytes,
+                                           unsigned lo_off) {
+  rs[0] = make_rsrc(p, bytes);
+  rs[1] = make_rsrc((const char*)p + lo_off, bytes);
 }
 
 // ROW image of a row-major bf16 matrix: element (row, k) at P[row*ld + kperm(k)]
-template <int ROWS, int NT, bool IS_A>
+template <int ROWS, int NT, bool IS_A, int KT>
 struct DmaRowK {
-  using S = DmaShape<ROWS, NT>;
-  __amdgpu_buffer_rsrc_t rs;
+  using S = DmaShape<ROWS, NT, KT>;
+  __amdgpu_buffer_rsrc_t rs[2];
   unsigned rowoff[S::NI];
   bool rv[S::NI];
   int cb, k, K, w;
   unsigned kb2;
   bool kv;
   __device__ void init(const GemmArgs& a, const __bf16* p, int row0, int kb, int tid, int) {
-    rs = make_rsrc(p, IS_A ? a.a_bytes : a.b_bytes);
+    plane_rsrc(rs, p, IS_A ? a.a_bytes : a.b_bytes, IS_A ? a.a_lo : a.b_lo);
     const int lane = tid & 63;
     w = tid >> 6;
-    cb = dma_chunk(lane, w);
+    cb = dma_chunk<KT>(lane, w);
     const unsigned ld = (unsigned)(IS_A ? a.lda : a.ldb);
     const int rows = IS_A ? a.M : a.N;
     K = a.K; k = kb;
 #pragma unroll
     for (int i = 0; i < S::NI; ++i) {
-      const int row = row0 + (i * S::NW + w) * DPR + lane / DCH;
+      const int row = row0 + (i * S::NW + w) * S::PR + lane / S::CH;
       rv[i] = row < rows;
       rowoff[i] = (unsigned)row * ld * 2u;
     }
   }
   __device__ void prep(const GemmArgs& a) {
-    const int kk = kperm64(a, k) + cb * 8;
+    const int kk = kperm_dma<KT>(a, k) + cb * 8;
     kv = kk < K;
     kb2 = (unsigned)kk * 2u;
   }
-  __device__ void issue(const GemmArgs&, __bf16* img, int i) {
-    dma16(rs, img + (i * S::NW + w) * 512, (rv[i] & kv) ? rowoff[i] + kb2 : OOB);
+  __device__ void issue(const GemmArgs&, __bf16* img, int i, int pl) {
+    dma16(rs[pl], img + (i * S::NW + w) * 512, (rv[i] & kv) ? rowoff[i] + kb2 : OOB);
   }
-  __device__ void advance() { k += DKT; }
+  __device__ void advance() { k += KT; }
 };
 
 // ROW image of the implicit im2col of a bf16 NHWC tensor (affine gather of LoadConvA's vector path, in bf16
 // bytes); needs Cx % 8 == 0 (a 16-B chunk never straddles two taps) and <= 32 taps
-template <int ROWS, int NT, int MODE>
+template <int ROWS, int NT, int MODE, int KT>
 struct DmaConvA {
-  using S = DmaShape<ROWS, NT>;
-  __amdgpu_buffer_rsrc_t rs;
+  using S = DmaShape<ROWS, NT, KT>;
+  __amdgpu_buffer_rsrc_t rs[2];
   unsigned rowbase[S::NI], vmask[S::NI];
   unsigned tbit;
   int delta;
   int cb, k, w, pt, pl;
   __device__ void init(const GemmArgs& a, const __bf16* x, int row0, int kb, int tid, int bidx) {
-    rs = make_rsrc(x, a.a_bytes);
+    plane_rsrc(rs, x, a.a_bytes, a.a_lo);
     const int lane = tid & 63;
     w = tid >> 6;
-    cb = dma_chunk(lane, w);
+    cb = dma_chunk<KT>(lane, w);
     k = kb;
     pt = a.pad_t - ((bidx + a.sub_par) >> 1);
     pl = a.pad_l - ((bidx + a.sub_par) & 1);
 #pragma unroll
     for (int i = 0; i < S::NI; ++i) {
-      const int m = row0 + (i * S::NW + w) * DPR + lane / DCH;
+      const int m = row0 + (i * S::NW + w) * S::PR + lane / S::CH;
       const bool valid = m < a.M;
       const int mm = valid ? m : 0;
       const int b = mdiv(mm, a.mg_hw);
@@ -885,7 +890,7 @@ struct DmaConvA {
     }
   }
   __device__ void prep(const GemmArgs& a) {
-    const int kk = kperm64(a, k) + cb * 8;
+    const int kk = kperm_dma<KT>(a, k) + cb * 8;
     const int tap = mdiv(kk, a.mg_cx);
     const int c = kk - tap * a.Cx;
     const int r = mdiv(tap, a.mg_s);
@@ -904,13 +909,13 @@ struct DmaConvA {
     delta = ((dh * a.W + dw) * a.Cx + c) * 2;
     tbit = kk < a.K ? 1u << tap : 0u;
   }
-  __device__ void issue(const GemmArgs&, __bf16* img, int i) {
-    dma16(rs, img + (i * S::NW + w) * 512, (vmask[i] & tbit) ? rowbase[i] + (unsigned)delta : OOB);
+  __device__ void issue(const GemmArgs&, __bf16* img, int i, int pl_) {
+    dma16(rs[pl_], img + (i * S::NW + w) * 512, (vmask[i] & tbit) ? rowbase[i] + (unsigned)delta : OOB);
   }
-  __device__ void advance() { k += DKT; }
+  __device__ void advance() { k += KT; }
 };
 
-// COL images (weight gradient: K = pixels, both operands contiguous along their rows): [64 k-rows][ROWS] bf16, k-row
+// COL images (weight gradient: K = pixels, both operands contiguous along their rows): [KT k-rows][ROWS] bf16, k-row
 // pitch ROWS, element (kr, col) at kr * ROWS + (col ^ dcswz(kr)). The 32x32x16 transpose reads (ds_read_b64_tr_b16)
 // of a lane group touch 4 consecutive k-rows x 32 columns: the XOR moves the 4 k-rows' 64-B runs into the 4 quarters
 // of a 256-B bank row (conflict-free for ROWS >= 128; 2-way at ROWS 64). One DMA instruction fills KPI k-rows; a
@@ -919,25 +924,25 @@ template <int ROWS>
 __device__ __forceinline__ int dcswz(int kr) {
   return ROWS >= 128 ? (kr & 3) << 5 : (kr & 1) << 5;
 }
-template <int ROWS, int NT>
+template <int ROWS, int NT, int KT>
 struct DmaColShape {
   static constexpr int CPR = ROWS / 8;  // 16-B chunks per k-row
   static constexpr int KPI = 64 / CPR;  // k-rows per DMA instruction
   static constexpr int NW = NT / 64;
-  static constexpr int NI = ROWS * DKT / (NT * 8);  // DMA instructions per thread per stage
-  static_assert(ROWS >= 64 && NI >= 1 && NI * NT * 8 == ROWS * DKT, "DMA COL image shape");
+  static constexpr int NI = ROWS * KT / (NT * 8);  // DMA instructions per thread per stage and plane
+  static_assert(ROWS >= 64 && NI >= 1 && NI * NT * 8 == ROWS * KT, "DMA COL image shape");
 };
 
 // A = dY^T: element (m, k) at P[k * lda + m]
-template <int ROWS, int NT>
+template <int ROWS, int NT, int KT>
 struct DmaColK {
-  using S = DmaColShape<ROWS, NT>;
-  __amdgpu_buffer_rsrc_t rs;
+  using S = DmaColShape<ROWS, NT, KT>;
+  __amdgpu_buffer_rsrc_t rs[2];
   unsigned colb, ld2;
   bool cv;
   int kr0, k, K, w;
   __device__ void init(const GemmArgs& a, const __bf16* p, int row0, int kb, int tid, int) {
-    rs = make_rsrc(p, a.a_bytes);
+    plane_rsrc(rs, p, a.a_bytes, a.a_lo);
     const int lane = tid & 63;
     w = tid >> 6;
     kr0 = w * S::KPI + lane / S::CPR;
@@ -949,24 +954,26 @@ struct DmaColK {
     k = kb; K = a.K;
   }
   __device__ void prep(const GemmArgs&) {}
-  __device__ void issue(const GemmArgs&, __bf16* img, int i) {
+  __device__ void issue(const GemmArgs&, __bf16* img, int i, int pl) {
     const int kk = k + kr0 + i * S::NW * S::KPI;
-    dma16(rs, img + (i * S::NW + w) * 512, (cv & (kk < K)) ? (unsigned)kk * ld2 + colb : OOB);
+    dma16(rs[pl], img + (i * S::NW + w) * 512, (cv & (kk < K)) ? (unsigned)kk * ld2 + colb : OOB);
   }
-  __device__ void advance() { k += DKT; }
+  __device__ void advance() { k += KT; }
 };
 
 // B = im2col of the bf16 NHWC input X: element (n = (r*S+s)*Cx + c, k = output pixel) = X[b][src(oh, ow, r, s)][c]
-template <int ROWS, int NT, int MODE>
+template <int ROWS, int NT, int MODE, int KT>
 struct DmaWgradX {
-  using S = DmaColShape<ROWS, NT>;
-  __amdgpu_buffer_rsrc_t rs;
+  using S = DmaColShape<ROWS, NT, KT>;
+  __amdgpu_buffer_rsrc_t rs[2];
   int kr0, k, K, w;
   int rr, ss, pt, pl;
   unsigned cb;
   bool nv;
+  unsigned off_[S::NI];
+  bool ok_[S::NI];
   __device__ void init(const GemmArgs& a, const __bf16* x, int row0, int kb, int tid, int bidx) {
-    rs = make_rsrc(x, a.b_bytes);
+    plane_rsrc(rs, x, a.b_bytes, a.b_lo);
     const int lane = tid & 63;
     w = tid >> 6;
     kr0 = w * S::KPI + lane / S::CPR;
@@ -982,33 +989,26 @@ struct DmaWgradX {
     pl = a.pad_l - ((bidx + a.sub_par) & 1);
     k = kb; K = a.K;
   }
-  __device__ void prep(const GemmArgs&) {}
-  __device__ void issue(const GemmArgs& a, __bf16* img, int i) {
-    const int kk = k + kr0 + i * S::NW * S::KPI;
-    const int p = min(kk, K - 1);
-    const int b = mdiv(p, a.mg_hw);
-    const int rem = p - b * (a.Ho * a.Wo);
-    const int oh = mdiv(rem, a.mg_wo);
-    const int ow = rem - oh * a.Wo;
-    int ih = 0, iw = 0;
-    const bool ok = nv & (kk < K) & tap_src<MODE>(a, pt, pl, oh, ow, rr, ss, ih, iw);
-    const unsigned off = (((unsigned)b * (unsigned)a.H + (unsigned)ih) * (unsigned)a.W + (unsigned)iw) * (unsigned)a.Cx * 2u + cb;
-    dma16(rs, img + (i * S::NW + w) * 512, ok ? off : OOB);
+  // the source pixel of instruction i's k-row (computed once per stage, shared by both planes)
+  __device__ void prep(const GemmArgs& a) {
+#pragma unroll
+    for (int i = 0; i < S::NI; ++i) {
+      const int kk = k + kr0 + i * S::NW * S::KPI;
+      const int p = min(kk, K - 1);
+      const int b = mdiv(p, a.mg_hw);
+      const int rem = p - b * (a.Ho * a.Wo);
+      const int oh = mdiv(rem, a.mg_wo);
+      const int ow = rem - oh * a.Wo;
+      int ih = 0, iw = 0;
+      ok_[i] = nv & (kk < K) & tap_src<MODE>(a, pt, pl, oh, ow, rr, ss, ih, iw);
+      off_[i] = (((unsigned)b * (unsigned)a.H + (unsigned)ih) * (unsigned)a.W + (unsigned)iw) * (unsigned)a.Cx * 2u + cb;
+    }
   }
-  __device__ void advance() { k += DKT; }
+  __device__ void issue(const GemmArgs&, __bf16* img, int i, int pl_) {
+    dma16(rs[pl_], img + (i * S::NW + w) * 512, ok_[i] ? off_[i] : OOB);
+  }
+  __device__ void advance() { k += KT; }
 };
-
-// 32x32x16 fragment (k-step ks of 16) from a DMA COL image: two transpose reads, k-rows kr and kr + 4
-template <int ROWS>
-__device__ __forceinline__ bf16x8 dcfrag(const __bf16* img, int row0, int ks, int lane) {
-  const int g = lane >> 4, li = lane & 15;
-  const int kr = ks * 16 + (g >> 1) * 8 + (li >> 2);
-  const int col = row0 + (g & 1) * 16 + 4 * (li & 3);
-  const __bf16* p = img + kr * ROWS + (col ^ dcswz<ROWS>(kr));
-  const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)p);
-  const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(p + 4 * ROWS));
-  return __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
-}
 
 // Fragment reads of the DMA main loop as inline asm: the compiler then neither sinks them to just ahead of their
 // MFMAs nor waits for the in-flight LDS-DMA before them (it cannot tell a transpose read of stage t from the DMA
@@ -1024,11 +1024,14 @@ __device__ __forceinline__ bf16x4 ads_tr(const __bf16* p) {
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(lds_addr(p)));
   return v;
 }
+// 16x16x32 fragment (8 consecutive k of one row) of k-step ks from a DMA ROW image
+template <int KT>
 __device__ __forceinline__ bf16x8 dfrag_asm(const __bf16* img, int row0, int ks, int lane) {
   const int r = row0 + (lane & 15);
   const int c = 4 * ks + (lane >> 4);
-  return ads_b128(img + r * DKT + ((c ^ dswz(r)) << 3));
+  return ads_b128(img + r * KT + ((c ^ dswz<KT>(r)) << 3));
 }
+// 32x32x16 fragment (k-step ks of 16) from a DMA COL image: two transpose reads, k-rows kr and kr + 4
 template <int ROWS>
 __device__ __forceinline__ bf16x8 dcfrag_asm(const __bf16* img, int row0, int ks, int lane) {
   const int g = lane >> 4, li = lane & 15;
@@ -1043,30 +1046,23 @@ __device__ __forceinline__ void wait_lgkm() {
   asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N > 15 ? 15 : N));
 }
 
-template <int KIND, int ROWS, int NT, bool IS_A>
+template <int KIND, int ROWS, int NT, bool IS_A, int KT>
 struct DmaLoader;
-template <int ROWS, int NT, bool IS_A>
-struct DmaLoader<0, ROWS, NT, IS_A> : DmaRowK<ROWS, NT, IS_A> {};
-template <int ROWS, int NT>
-struct DmaLoader<A_CONV_FWD, ROWS, NT, true> : DmaConvA<ROWS, NT, MODE_FWD> {};
-template <int ROWS, int NT>
-struct DmaLoader<A_CONV_DGRAD, ROWS, NT, true> : DmaConvA<ROWS, NT, MODE_DGRAD> {};
-template <int ROWS, int NT>
-struct DmaLoader<A_CONV_SUBPIX, ROWS, NT, true> : DmaConvA<ROWS, NT, MODE_SUBPIX> {};
-template <int ROWS, int NT>
-struct DmaLoader<A_COLM, ROWS, NT, true> : DmaColK<ROWS, NT> {};
+template <int ROWS, int NT, bool IS_A, int KT>
+struct DmaLoader<0, ROWS, NT, IS_A, KT> : DmaRowK<ROWS, NT, IS_A, KT> {};
+template <int ROWS, int NT, int KT>
+struct DmaLoader<A_CONV_FWD, ROWS, NT, true, KT> : DmaConvA<ROWS, NT, MODE_FWD, KT> {};
+template <int ROWS, int NT, int KT>
+struct DmaLoader<A_CONV_DGRAD, ROWS, NT, true, KT> : DmaConvA<ROWS, NT, MODE_DGRAD, KT> {};
+template <int ROWS, int NT, int KT>
+struct DmaLoader<A_CONV_SUBPIX, ROWS, NT, true, KT> : DmaConvA<ROWS, NT, MODE_SUBPIX, KT> {};
+template <int ROWS, int NT, int KT>
+struct DmaLoader<A_COLM, ROWS, NT, true, KT> : DmaColK<ROWS, NT, KT> {};
 // B operands (IS_A false): weights (ROW) and the weight gradient's im2col gathers (COL)
-template <int ROWS, int NT>
-struct DmaLoader<B_WGRAD_FWD, ROWS, NT, false> : DmaWgradX<ROWS, NT, MODE_FWD> {};
-template <int ROWS, int NT>
-struct DmaLoader<B_WGRAD_SUBPIX, ROWS, NT, false> : DmaWgradX<ROWS, NT, MODE_SUBPIX> {};
-
-// 16x16x32 fragment (8 consecutive k of one row) of k-step ks from a DMA ROW image
-__device__ __forceinline__ bf16x8 dfrag(const __bf16* img, int row0, int ks, int lane) {
-  const int r = row0 + (lane & 15);
-  const int c = 4 * ks + (lane >> 4);
-  return *(const bf16x8*)(img + r * DKT + ((c ^ dswz(r)) << 3));
-}
+template <int ROWS, int NT, int KT>
+struct DmaLoader<B_WGRAD_FWD, ROWS, NT, false, KT> : DmaWgradX<ROWS, NT, MODE_FWD, KT> {};
+template <int ROWS, int NT, int KT>
+struct DmaLoader<B_WGRAD_SUBPIX, ROWS, NT, false, KT> : DmaWgradX<ROWS, NT, MODE_SUBPIX, KT> {};
 
 // one MFMA product step: 3xBF16 (lo*hi + hi*lo + hi*hi, small terms first) or plain bf16
 __device__ __forceinline__ f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
@@ -1149,15 +1145,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int MF = mf_of(AK), KS = ks_of<MF>(), NR = nr_of<MF>();
   using acc_t = acc_of<MF>;
-  constexpr int LP = PREC == 4 ? 1 : PREC;  // arithmetic of the register-staged loaders
+  constexpr int LP = PREC == 4 ? 1 : PREC == 5 ? 3 : PREC;  // arithmetic of the register-staged loaders
   using LA = Loader<AK, BM, VA, NT, true, LP>;
   using LB = Loader<BKIND, BN, VB, NT, false, LP>;
   using IA = Img<BM, LA::COL>;
   using IB = Img<BN, LB::COL>;
   constexpr int BUF = IA::SIZE + IB::SIZE;
-  constexpr int DBUF = (BM + BN) * DKT;  // PREC 4: one stage of the A and B DMA images
+  constexpr int DBUF = (PREC == 5 ? 2 : 1) * (BM + BN) * (PREC == 5 ? 32 : 64);  // PREC 4/5: one DMA stage
   constexpr int TM = BM / WGM / MF, TN = BN / WGN / MF;  // MFMA tiles per wave
-  __shared__ __attribute__((aligned(16))) __bf16 lds[(PREC == 4 && DNST * DBUF > 2 * BUF) ? DNST * DBUF : 2 * BUF];
+  __shared__ __attribute__((aligned(16))) __bf16 lds[(PREC >= 4 && 2 * DBUF > 2 * BUF) ? 2 * DBUF : 2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WGN, wn = wid - wm * WGN;
@@ -1190,122 +1186,66 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
       for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
   const int arow = wm * (BM / WGM), brow = wn * (BN / WGN);
 
-  if constexpr (PREC == 4) {
-    // LDS-DMA main loops. Only LDS-DMA loads are in flight in the loop (no VGPR-destination load the compiler would
-    // drain with them); fragment reads are inline asm with counted lgkmcnt waits (dfrag_asm). ROW images (fwd /
-    // dgrad) feed 16x16x32 MFMAs, COL images (weight gradient) 32x32x16 MFMAs.
+  if constexpr (PREC >= 4) {
+    // LDS-DMA main loop, two stages: at the top of iteration t each wave waits for its own DMA of stage t (vmcnt 0),
+    // the barrier makes every wave's DMA of stage t visible and guarantees that every wave has finished reading stage
+    // t-1, then the DMA of stage t+1 is issued into that slot and stage t is multiplied: the DMA has one phase to
+    // land. Only LDS-DMA loads are in flight in the loop (no VGPR-destination load the compiler would drain with
+    // them); fragment reads are inline asm with counted lgkmcnt waits. ROW images (fwd / dgrad) feed 16x16x32 MFMAs,
+    // COL images (weight gradient) 32x32x16 MFMAs. PREC 4: bf16 operands, 64-deep stages, the fragments of k-step
+    // ks+1 read during k-step ks. PREC 5: planar 3xBF16 operands (hi and lo images), 32-deep stages, per k-step the
+    // B fragments then the A fragments streamed one MF-row ahead of their 3 x TN MFMAs.
+    // (Measured and removed: a 4-stage ring of 32-deep bf16 stages with fragment reads one stage ahead, 5-10 %
+    // slower -- twice the barriers; with no DMA in the loop at all the bf16 loop runs 40-50 % faster, at a higher
+    // clock, which no issue order recovers.)
+    constexpr int KT = PREC == 5 ? 32 : 64;
+    constexpr int NPL = PREC == 5 ? 2 : 1;  // LDS images per operand (hi, lo)
     constexpr bool ACOL = AK == A_COLM, BCOL = BKIND == B_WGRAD_FWD || BKIND == B_WGRAD_SUBPIX;
     static_assert(ACOL == BCOL && MF == (ACOL ? 32 : 16), "DMA main loop: ROW x ROW (MF 16) or COL x COL (MF 32)");
-    using DA = DmaLoader<AK == A_ROWK ? 0 : AK, BM, NT, true>;
-    using DB = DmaLoader<BKIND == B_ROWK ? 0 : BKIND, BN, NT, false>;
+    using DA = DmaLoader<AK == A_ROWK ? 0 : AK, BM, NT, true, KT>;
+    using DB = DmaLoader<BKIND == B_ROWK ? 0 : BKIND, BN, NT, false, KT>;
+    constexpr int PA = BM * KT, PB = BN * KT;  // plane sizes (elements)
+    constexpr int SBUF = NPL * (PA + PB);      // one stage
+    static_assert(2 * SBUF * 2 <= 163840, "DMA stages exceed the LDS");
     DA da;
     DB db;
     da.init(a, (const __bf16*)a.A + bidx * a.sA, m0, kb, tid, bidx);
     db.init(a, (const __bf16*)a.B + bidx * a.sB, n0, kb, tid, bidx);
-    const int nt = ke > kb ? (ke - kb + DKT - 1) / DKT : 0;
-    constexpr int NID = DA::S::NI + DB::S::NI;  // DMA instructions per thread per stage
-    auto issue = [&](__bf16* stage) {  // DMA of the loaders' current stage, then advance them
+    const int nt = ke > kb ? (ke - kb + KT - 1) / KT : 0;
+    constexpr int NID = NPL * (DA::S::NI + DB::S::NI);  // DMA instructions per thread per stage
+    auto issue_q = [&](__bf16* stage, int q) {  // DMA instruction q of the stage (A planes first, then B planes)
+      constexpr int QA = NPL * DA::S::NI;
+      if (q < QA) da.issue(a, stage + (q / DA::S::NI) * PA, q % DA::S::NI, q / DA::S::NI);
+      else db.issue(a, stage + NPL * PA + ((q - QA) / DB::S::NI) * PB, (q - QA) % DB::S::NI, (q - QA) / DB::S::NI);
+    };
+    auto issue = [&](__bf16* stage) {
       da.prep(a);
       db.prep(a);
 #pragma unroll
-      for (int i = 0; i < DA::S::NI; ++i) da.issue(a, stage, i);
-#pragma unroll
-      for (int i = 0; i < DB::S::NI; ++i) db.issue(a, stage + BM * DKT, i);
+      for (int q = 0; q < NID; ++q) issue_q(stage, q);
       da.advance();
       db.advance();
     };
     auto frag_a = [&](const __bf16* img, int row0, int ks) {
       if constexpr (ACOL) return dcfrag_asm<BM>(img, row0, ks, lane);
-      else return dfrag_asm(img, row0, ks, lane);
+      else return dfrag_asm<KT>(img, row0, ks, lane);
     };
     auto frag_b = [&](const __bf16* img, int row0, int ks) {
       if constexpr (BCOL) return dcfrag_asm<BN>(img, row0, ks, lane);
-      else return dfrag_asm(img, row0, ks, lane);
+      else return dfrag_asm<KT>(img, row0, ks, lane);
     };
-    constexpr int DKS = DKT / (MF == 32 ? 16 : 32);    // MFMA k-steps per stage
-    constexpr int RPS = (ACOL ? 2 : 1) * (TM + TN);  // LDS read instructions per k-step
-    auto barrier = [&]() {
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    };
-#if MVAE_DMA_RING
-    // 4-stage ring, 32-deep stages, fragments read one stage ahead. Phase t: wait for this wave's DMA of stage t+1
-    // (stage t+2's stays in flight), barrier (every wave's stage t+1 has landed; every wave has finished reading
-    // stage t-1, whose fragments it read during phase t-2), DMA stage t+3 into ring slot (t+3)&3 = (t-1)&3, read
-    // stage t+1's fragments, multiply stage t (fragments read during phase t-1). The DMA has two phases to land;
-    // the LDS reads run under the previous stage's MFMAs.
-    static_assert(DKT == 32 && DNST == 4, "ring geometry");
-    bf16x8 fa[2][DKS][TM], fb[2][DKS][TN];
-    auto read_stage = [&](int slot, int f, int ks) {
-      const __bf16* Ai = lds + slot * DBUF;
-      const __bf16* Bi = Ai + BM * DKT;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) fb[f][ks][j] = frag_b(Bi, brow + j * MF, ks);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) fa[f][ks][i] = frag_a(Ai, arow + i * MF, ks);
-    };
-    auto mma_stage = [&](int f, int ks) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(fa[f][ks][i], fb[f][ks][j], acc[i][j]);
-    };
-    // prologue: stages 0..2 in flight, stage 0 landed and read
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-      if (q < nt) issue(lds + q * DBUF);
-    if (nt > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NID) : "memory");
-    else if (nt > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NID) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    barrier();
-    if (nt > 0) {
-#pragma unroll
-      for (int ks = 0; ks < DKS; ++ks) read_stage(0, 0, ks);
-    }
-    // t even / odd as two unrolled halves: the fragment register sets alternate without runtime indexing
-    auto phase = [&](int t, auto fcur) {
-      constexpr int F = decltype(fcur)::value;
-      if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NID) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      barrier();
-      if (t + 3 < nt) issue(lds + ((t + 3) & 3) * DBUF);
-      const bool more = t + 1 < nt;
-      if (more) read_stage((t + 1) & 3, F ^ 1, 0);
-      if (more) wait_lgkm<RPS>();
-      else wait_lgkm<0>();
-      __builtin_amdgcn_sched_barrier(0);
-      mma_stage(F, 0);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ks = 1; ks < DKS; ++ks) {
-        if (more) read_stage((t + 1) & 3, F ^ 1, ks);
-        __builtin_amdgcn_sched_barrier(0);
-        mma_stage(F, ks);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    int t = 0;
-    for (; t + 1 < nt; t += 2) {
-      phase(t, std::integral_constant<int, 0>{});
-      phase(t + 1, std::integral_constant<int, 1>{});
-    }
-    if (t < nt) phase(t, std::integral_constant<int, 0>{});
-#else
-    // 2 stages of 64: at the top of iteration t each wave waits for its own DMA of stage t (vmcnt 0), the barrier
-    // makes every wave's DMA of stage t visible and guarantees that every wave has finished reading stage t-1, then
-    // the DMA of stage t+1 is issued into that slot and stage t is multiplied: the DMA has one phase to land.
+    constexpr int DKS = KT / (MF == 32 ? 16 : 32);   // MFMA k-steps per stage
+    constexpr int RPF = ACOL ? 2 : 1;                // LDS read instructions per fragment
+    // (measured, c5 shapes: the spread issue gains 3-6 % on the weight-gradient loops and loses 0-3 % on fwd / dgrad)
+    constexpr bool SPREAD = MVAE_DMA_SPREAD == 2 || (MVAE_DMA_SPREAD == 1 && ACOL);
     if (nt > 0) issue(lds);
     for (int t = 0; t < nt; ++t) {
-      __bf16* cur = lds + (t & 1) * DBUF;
-#if MVAE_DMA_EXP != 1  // (experiment 1: no wait for the DMA -- timing only, wrong results)
+      __bf16* cur = lds + (t & 1) * SBUF;
+      __bf16* nxt = lds + ((t + 1) & 1) * SBUF;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-      barrier();
-      __bf16* nxt = lds + ((t + 1) & 1) * DBUF;
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
       const bool more = t + 1 < nt;
-      // (measured, c5 shapes: the spread issue gains 3-6 % on the weight-gradient loops and loses 0-3 % on fwd / dgrad)
-      constexpr bool SPREAD = MVAE_DMA_SPREAD == 2 || (MVAE_DMA_SPREAD == 1 && ACOL);
-#if MVAE_DMA_EXP != 2  // (experiment 2: no DMA in the loop -- timing only, wrong results)
       // SPREAD: the stage's DMA instructions are issued in DKS slices, one ahead of each k-step's MFMAs, instead of
       // in one burst after the barrier
       if (SPREAD && more) {
@@ -1313,50 +1253,76 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
         db.prep(a);
       }
       if (!SPREAD && more) issue(nxt);
-#endif
-      const __bf16* Ai = cur;
-      const __bf16* Bi = cur + BM * DKT;
-      // fragments double-buffered over the k-steps: the reads of k-step ks+1 are issued ahead of k-step ks's MFMAs
-      bf16x8 fa[2][TM], fb[2][TN];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) fb[0][j] = frag_b(Bi, brow + j * MF, 0);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) fa[0][i] = frag_a(Ai, arow + i * MF, 0);
-#pragma unroll
-      for (int ks = 0; ks < DKS; ++ks) {
-        const int c = ks & 1;
-        if (ks + 1 < DKS) {
-#pragma unroll
-          for (int j = 0; j < TN; ++j) fb[c ^ 1][j] = frag_b(Bi, brow + j * MF, ks + 1);
-#pragma unroll
-          for (int i = 0; i < TM; ++i) fa[c ^ 1][i] = frag_a(Ai, arow + i * MF, ks + 1);
-        }
-        if (ks + 1 < DKS) wait_lgkm<RPS>();  // k-step ks's reads are done; ks+1's stay in flight
-        else wait_lgkm<0>();
-        __builtin_amdgcn_sched_barrier(0);
-#if MVAE_DMA_EXP != 2
+      auto dma_slice = [&](int ks) {
         if (SPREAD && more) {
 #pragma unroll
-          for (int q = ks * NID / DKS; q < (ks + 1) * NID / DKS; ++q) {
-            if (q < DA::S::NI) da.issue(a, nxt, q);
-            else db.issue(a, nxt + BM * DKT, q - DA::S::NI);
+          for (int q = ks * NID / DKS; q < (ks + 1) * NID / DKS; ++q) issue_q(nxt, q);
+        }
+      };
+      const __bf16* Ah = cur;
+      const __bf16* Bh = cur + NPL * PA;
+      if constexpr (PREC == 4) {
+        constexpr int RPS = RPF * (TM + TN);  // LDS read instructions per k-step
+        bf16x8 fa[2][TM], fb[2][TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[0][j] = frag_b(Bh, brow + j * MF, 0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[0][i] = frag_a(Ah, arow + i * MF, 0);
+#pragma unroll
+        for (int ks = 0; ks < DKS; ++ks) {
+          const int c = ks & 1;
+          if (ks + 1 < DKS) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) fb[c ^ 1][j] = frag_b(Bh, brow + j * MF, ks + 1);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) fa[c ^ 1][i] = frag_a(Ah, arow + i * MF, ks + 1);
+          }
+          if (ks + 1 < DKS) wait_lgkm<RPS>();  // k-step ks's reads are done; ks+1's stay in flight
+          else wait_lgkm<0>();
+          __builtin_amdgcn_sched_barrier(0);
+          dma_slice(ks);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(fa[c][i], fb[c][j], acc[i][j]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+        const __bf16* Al = Ah + PA;
+        const __bf16* Bl = Bh + PB;
+        constexpr int RA = 2 * RPF;  // reads per A fragment pair (hi, lo)
+#pragma unroll
+        for (int ks = 0; ks < DKS; ++ks) {
+          bf16x8 bh[TN], bl[TN], ah[2], al[2];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            bh[j] = frag_b(Bh, brow + j * MF, ks);
+            bl[j] = frag_b(Bl, brow + j * MF, ks);
+          }
+          ah[0] = frag_a(Ah, arow, ks);
+          al[0] = frag_a(Al, arow, ks);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            if (i + 1 < TM) {
+              ah[(i + 1) & 1] = frag_a(Ah, arow + (i + 1) * MF, ks);
+              al[(i + 1) & 1] = frag_a(Al, arow + (i + 1) * MF, ks);
+              wait_lgkm<RA>();  // everything but the pair just issued
+            } else {
+              wait_lgkm<0>();
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (i == 0) dma_slice(ks);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) mma<3>(acc[i][j], ah[i & 1], al[i & 1], bh[j], bl[j]);
+            __builtin_amdgcn_sched_barrier(0);
           }
         }
-#endif
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_bf16(fa[c][i], fb[c][j], acc[i][j]);
-        __builtin_amdgcn_sched_barrier(0);
       }
-#if MVAE_DMA_EXP != 2
       if (SPREAD && more) {
         da.advance();
         db.advance();
       }
-#endif
     }
-#endif
   } else {
   LA la;
   LB lb;
@@ -1868,22 +1834,23 @@ void launch_big(GemmArgs& a, hipStream_t st, int cfg) {
   }
 }
 
-// bf16-stored operands (MVAE_CONV_BF16): every tile config on the LDS-DMA main loop
-template <int AK>
+// DMA-staged operands (MVAE_CONV_BF16: PREC 4, MVAE_CONV_PLANAR: PREC 5): every tile config on the LDS-DMA main loop
+template <int AK, int P>
 void launch_dma(GemmArgs& a, hipStream_t st, int cfg) {
   switch (cfg) {
-    case T256x256: launch_cfg<T256x256, AK, 4, B_ROWK, 4, 4>(a, st); break;
-    case T256x128: launch_cfg<T256x128, AK, 4, B_ROWK, 4, 4>(a, st); break;
-    case T128x256: launch_cfg<T128x256, AK, 4, B_ROWK, 4, 4>(a, st); break;
-    case T128x128: launch_cfg<T128x128, AK, 4, B_ROWK, 4, 4>(a, st); break;
-    default: launch_cfg<T64x64, AK, 4, B_ROWK, 4, 4>(a, st); break;  // (and the skinny-N 128x16 choice)
+    case T256x256: launch_cfg<T256x256, AK, 4, B_ROWK, 4, P>(a, st); break;
+    case T256x128: launch_cfg<T256x128, AK, 4, B_ROWK, 4, P>(a, st); break;
+    case T128x256: launch_cfg<T128x256, AK, 4, B_ROWK, 4, P>(a, st); break;
+    case T128x128: launch_cfg<T128x128, AK, 4, B_ROWK, 4, P>(a, st); break;
+    default: launch_cfg<T64x64, AK, 4, B_ROWK, 4, P>(a, st); break;  // (and the skinny-N 128x16 choice)
   }
 }
 
 // gemm_dma.hip: launch_dma for AK in {A_ROWK, A_CONV_FWD, A_CONV_DGRAD, A_CONV_SUBPIX} (own translation unit)
-void conv_dma(int ak, GemmArgs& a, hipStream_t st, int cfg);
-// weight gradient on packed bf16 dY^T (COL) x im2col of bf16 X (B_WGRAD_FWD / B_WGRAD_SUBPIX)
-void wgrad_dma(int bkind, GemmArgs& a, hipStream_t st, int cfg);
+// prec 4: packed bf16 operands; prec 5: planar 3xBF16 operands (hi plane, lo plane a_lo / b_lo bytes later)
+void conv_dma(int ak, GemmArgs& a, hipStream_t st, int cfg, int prec);
+// weight gradient on DMA-staged dY^T (COL) x im2col of X (B_WGRAD_FWD / B_WGRAD_SUBPIX)
+void wgrad_dma(int bkind, GemmArgs& a, hipStream_t st, int cfg, int prec);
 
 template <int AK, int VA, int BKIND, int VB>
 void launch_small(GemmArgs& a, hipStream_t st, int cfg) {

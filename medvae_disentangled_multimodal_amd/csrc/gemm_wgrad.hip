@@ -66,12 +66,13 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
                            size_t workspace_bytes, void* stream) {
   const bool xsplit = (mode & MVAE_CONV_XSPLIT) != 0;   // x holds split4_bf16 groups
   const bool dysplit = (mode & MVAE_CONV_DYSPLIT) != 0;  // dy holds split4_bf16 groups
-  const bool bf = (mode & MVAE_CONV_BF16) != 0;          // dy and x packed bf16 (LDS-DMA main loop)
-  mode &= ~(MVAE_CONV_XSPLIT | MVAE_CONV_DYSPLIT | MVAE_CONV_BF16);
+  const bool pln = (mode & MVAE_CONV_PLANAR) != 0;      // dy and x planar 3xBF16 (PREC 5)
+  const bool bf = (mode & MVAE_CONV_BF16) != 0 || pln;  // dy and x DMA-staged (LDS-DMA main loop)
+  mode &= ~(MVAE_CONV_XSPLIT | MVAE_CONV_DYSPLIT | MVAE_CONV_BF16 | MVAE_CONV_PLANAR);
   if (bf && (xsplit || dysplit || mode != 0 || dbias || cin % 8 || cout % 8 || !al16(dy) || !al16(x) ||
-             math_mode() != MATH_BF16)) {
-    set_error("wgrad: bf16-packed operands need the bf16 math mode, mode 0, cin %% 8 == 0, cout %% 8 == 0, aligned "
-              "dy / x, no fused bias");
+             math_mode() != (pln ? MATH_3XBF16 : MATH_BF16))) {
+    set_error("wgrad: DMA-staged operands need the matching math mode, mode 0, cin %% 8 == 0, cout %% 8 == 0, "
+              "aligned dy / x, no fused bias");
     return MVAE_EINVAL;
   }
   if (dysplit && (cout % 4 != 0 || !al16(dy))) {
@@ -106,6 +107,10 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
     a.B = bf ? (const float*)((const __bf16*)x + (long long)b0 * (in_img / 4)) : x + (long long)b0 * (in_img / 4);
     a.C = dw; a.ldc = a.N; a.alpha = 1.f; a.beta = b0 == 0 ? beta : 1.f;
     a.a_bytes = (unsigned)(out_img * n / (bf ? 2 : 1)); a.b_bytes = (unsigned)(in_img * n / (bf ? 2 : 1));
+    if (pln) {
+      a.a_lo = (unsigned)(out_img / 2 * nb);
+      a.b_lo = (unsigned)(in_img / 2 * nb);
+    }
     a.c_bytes = (unsigned)((long long)a.M * a.N * 4);
     a.H = h; a.W = wd; a.Cx = cin; a.Ho = ho; a.Wo = wo; a.R = kh; a.S = kw;
     set_gather_magic(a);
@@ -117,7 +122,7 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
     // bias partials live after the split-K partials
     a.bias_ws = dbias ? (float*)((char*)workspace + ((splitk_ws_bytes(a) + 255) & ~(size_t)255)) : nullptr;
     if (bf) {
-      wgrad_dma(B_WGRAD_FWD, a, st, cfg);
+      wgrad_dma(B_WGRAD_FWD, a, st, cfg, pln ? 5 : 4);
     } else if (dysplit) {
       if (xsplit) launch_big<A_COLM_SPLIT, 4, B_WGRAD_FWD_SPLIT, 4>(a, st, cfg);
       else if (mode == 0 && vb) launch_big<A_COLM_SPLIT, 4, B_WGRAD_FWD, 4>(a, st, cfg);

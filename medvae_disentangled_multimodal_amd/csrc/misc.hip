@@ -17,7 +17,22 @@ namespace mvae {
 // bf16-mixed mode's GEMM operand, 2 B per element at the same element offsets)
 __device__ __forceinline__ void write_transposed(const float (*tile)[65], float* __restrict__ wt, int c0, int o0, int t,
                                                  int rs, int cin, int cout, int split) {
-  if (split == 2) {
+  if (split == 3) {  // planar 3xBF16: hi plane [cin*rs*cout] bf16, then the lo plane
+    const int g = threadIdx.x & 31, cr = threadIdx.x >> 5;
+    __bf16* wb = (__bf16*)wt;
+    const long long plane = (long long)cin * rs * cout;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int cl = cr + 8 * i, c = c0 + cl, o = o0 + 2 * g;
+      if (c < cin && o < cout) {  // cout % 4 == 0: o + 1 < cout
+        const long long e = ((long long)c * rs + t) * cout + o;
+        const float v0 = tile[2 * g][cl], v1 = tile[2 * g + 1][cl];
+        const unsigned h = pk_bf16x2(v0, v1);
+        *(unsigned*)(wb + e) = h;
+        *(unsigned*)(wb + plane + e) = pk_bf16x2(v0 - __uint_as_float(h << 16), v1 - __uint_as_float(h & 0xFFFF0000u));
+      }
+    }
+  } else if (split == 2) {
     const int g = threadIdx.x & 31, cr = threadIdx.x >> 5;
     __bf16* wb = (__bf16*)wt;
 #pragma unroll
@@ -132,9 +147,14 @@ __global__ void __launch_bounds__(256) w_ups_fwd_kernel(const float* __restrict_
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] += t[r][s][e];
         float* o = w4 + ((((long long)cls * cout + co) * 2 + a) * 2 + b) * cin + ci;
-        if (split == 2) {
+        if (split >= 2) {  // packed bf16 (2) or planar 3xBF16 (3: lo plane 16*cout*cin elements later)
           __bf16* ob = (__bf16*)w4 + (o - w4);
-          *(uint2*)ob = uint2{pk_bf16x2(v[0], v[1]), pk_bf16x2(v[2], v[3])};
+          const unsigned h01 = pk_bf16x2(v[0], v[1]), h23 = pk_bf16x2(v[2], v[3]);
+          *(uint2*)ob = uint2{h01, h23};
+          if (split == 3)
+            *(uint2*)(ob + 16LL * cout * cin) =
+                uint2{pk_bf16x2(v[0] - __uint_as_float(h01 << 16), v[1] - __uint_as_float(h01 & 0xFFFF0000u)),
+                      pk_bf16x2(v[2] - __uint_as_float(h23 << 16), v[3] - __uint_as_float(h23 & 0xFFFF0000u))};
         } else if (split) {
           *(uint4*)o = split4_bf16(float4{v[0], v[1], v[2], v[3]});
         } else {
@@ -156,9 +176,27 @@ __global__ void __launch_bounds__(256) pack_bf16_kernel(const float4* __restrict
   }
 }
 
+// planar 3xBF16 of 4 fp32 values: hi (returned in .x) and lo (.y) bf16 pairs x 2
+__device__ __forceinline__ void planar4(float4 v, uint2& hi, uint2& lo) {
+  const unsigned h01 = pk_bf16x2(v.x, v.y), h23 = pk_bf16x2(v.z, v.w);
+  hi = uint2{h01, h23};
+  lo = uint2{pk_bf16x2(v.x - __uint_as_float(h01 << 16), v.y - __uint_as_float(h01 & 0xFFFF0000u)),
+             pk_bf16x2(v.z - __uint_as_float(h23 << 16), v.w - __uint_as_float(h23 & 0xFFFF0000u))};
+}
+// planar 3xBF16 of n values: y[0, n) hi plane, y[n, 2n) lo plane (bf16)
+__global__ void __launch_bounds__(256) split_planar_kernel(const float4* __restrict__ x, uint2* __restrict__ y, long long n4) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    uint2 h, l;
+    planar4(x[i], h, l);
+    y[i] = h;
+    y[n4 + i] = l;
+  }
+}
+
 // packed bf16 of x [rows][n] (n % 4 == 0, row stride n) plus the fp64 column sums of the fp32 values per chunk of
 // rows: part[chunk][n] (the conv bias gradient of a dy that the bf16-mixed GEMMs read packed: one pass over dy for
 // both). 256 threads = 64 column groups of 4 x 4 row phases; fixed summation order.
+template <bool PLANAR>
 __global__ void __launch_bounds__(256) pack_colsum_kernel(const float* __restrict__ x, uint2* __restrict__ y,
                                                           long long rows, int n, int rows_per_chunk,
                                                           double* __restrict__ part) {
@@ -172,7 +210,14 @@ __global__ void __launch_bounds__(256) pack_colsum_kernel(const float* __restric
   if (c < n) {
     for (long long r = r0 + rg; r < r1; r += 4) {
       const float4 v = *(const float4*)(x + r * n + c);
-      y[(r * n + c) >> 2] = uint2{pk_bf16x2(v.x, v.y), pk_bf16x2(v.z, v.w)};
+      if constexpr (PLANAR) {  // hi plane, then the lo plane rows * n elements later
+        uint2 h, l;
+        planar4(v, h, l);
+        y[(r * n + c) >> 2] = h;
+        y[((rows * n) >> 2) + ((r * n + c) >> 2)] = l;
+      } else {
+        y[(r * n + c) >> 2] = uint2{pk_bf16x2(v.x, v.y), pk_bf16x2(v.z, v.w)};
+      }
       a0 += v.x; a1 += v.y; a2 += v.z; a3 += v.w;
     }
   }
@@ -231,7 +276,7 @@ using namespace mvae;
 extern "C" {
 
 int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int kw, int cin, int split, void* stream) {
-  if (cout <= 0 || kh <= 0 || kw <= 0 || cin <= 0 || split < 0 || split > 2 || (split && (cout & 3))) {
+  if (cout <= 0 || kh <= 0 || kw <= 0 || cin <= 0 || split < 0 || split > 3 || (split && (cout & 3))) {
     set_error("w_transpose: bad sizes");
     return MVAE_EINVAL;
   }
@@ -242,7 +287,7 @@ int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int 
 
 // wt [cin][4][4][cout] for the dgrad of "nearest-x2 upsample then 3x3 conv"
 int mvae_conv_weight_upsample_dgrad(const float* w, float* wt, int cout, int cin, int split, void* stream) {
-  if (cout <= 0 || cin <= 0 || split < 0 || split > 2 || (split && (cout & 3))) { set_error("w_ups: bad sizes"); return MVAE_EINVAL; }
+  if (cout <= 0 || cin <= 0 || split < 0 || split > 3 || (split && (cout & 3))) { set_error("w_ups: bad sizes"); return MVAE_EINVAL; }
   hipLaunchKernelGGL(w_ups_dgrad_kernel, dim3((cin + 63) / 64, (cout + 63) / 64, 16), dim3(256), 0,
                      (hipStream_t)stream, w, wt, cout, cin, split);
   return launch_status();
@@ -250,7 +295,7 @@ int mvae_conv_weight_upsample_dgrad(const float* w, float* wt, int cout, int cin
 
 // w4 [4][cout][2][2][cin] for the sub-pixel forward of "nearest-x2 upsample then 3x3 conv"
 int mvae_conv_weight_upsample_fwd(const float* w, float* w4, int cout, int cin, int split, void* stream) {
-  if (cout <= 0 || cin <= 0 || split < 0 || split > 2 || (split && (cin & 3))) { set_error("w_ups_fwd: bad sizes"); return MVAE_EINVAL; }
+  if (cout <= 0 || cin <= 0 || split < 0 || split > 3 || (split && (cin & 3))) { set_error("w_ups_fwd: bad sizes"); return MVAE_EINVAL; }
   const long long tot = (long long)cout * (split ? cin / 4 : cin);
   hipLaunchKernelGGL(w_ups_fwd_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, w, w4,
                      cout, cin, split);
@@ -278,8 +323,29 @@ int mvae_pack_bf16(const float* x, void* y, long long n, void* stream) {
 // y = packed bf16 of x [rows][n] (fp32, row stride n) and out[n] = beta*out[n] + sum_rows x (the conv bias gradient,
 // fp64 partials in a fixed order): the bf16-mixed mode's output-gradient pack (MVAE_CONV_BF16) and bias gradient in
 // one pass over dy. Workspace: mvae_bias_grad_workspace_bytes(rows, n).
+static int pack_colsum(bool planar, const float* x, void* y, long long rows, int n, float* out, float beta,
+                       void* workspace, size_t workspace_bytes, void* stream);
 int mvae_pack_bf16_colsum(const float* x, void* y, long long rows, int n, float* out, float beta, void* workspace,
                           size_t workspace_bytes, void* stream) {
+  return pack_colsum(false, x, y, rows, n, out, beta, workspace, workspace_bytes, stream);
+}
+// the same pass writing dy as planar 3xBF16 (hi plane, then lo plane rows * n elements later; MVAE_CONV_PLANAR)
+int mvae_split_planar_colsum(const float* x, void* y, long long rows, int n, float* out, float beta, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+  return pack_colsum(true, x, y, rows, n, out, beta, workspace, workspace_bytes, stream);
+}
+// planar 3xBF16 of n fp32 values (n % 4 == 0): y = [hi plane n bf16][lo plane n bf16]
+int mvae_split_planar(const float* x, void* y, long long n, void* stream) {
+  if (n <= 0 || (n & 3) || ((uintptr_t)x & 15) || ((uintptr_t)y & 7)) {
+    set_error("split_planar: n must be a positive multiple of 4, x 16-B / y 8-B aligned");
+    return MVAE_EINVAL;
+  }
+  hipLaunchKernelGGL(split_planar_kernel, dim3(egrid(n / 4)), dim3(256), 0, (hipStream_t)stream, (const float4*)x,
+                     (uint2*)y, n / 4);
+  return launch_status();
+}
+static int pack_colsum(bool planar, const float* x, void* y, long long rows, int n, float* out, float beta,
+                       void* workspace, size_t workspace_bytes, void* stream) {
   if (rows <= 0 || n <= 0 || (n & 3) || ((uintptr_t)x & 15) || ((uintptr_t)y & 7)) {
     set_error("pack_bf16_colsum: n %% 4 == 0, 16-B aligned x, 8-B aligned y");
     return MVAE_EINVAL;
@@ -288,8 +354,12 @@ int mvae_pack_bf16_colsum(const float* x, void* y, long long rows, int n, float*
   if (workspace_bytes < (size_t)chunks * n * sizeof(double)) { set_error("pack_bf16_colsum: workspace"); return MVAE_EWORKSPACE; }
   const int rpc = (int)((rows + chunks - 1) / chunks);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(pack_colsum_kernel, dim3((n / 4 + 63) / 64, chunks), dim3(256), 0, st, x, (uint2*)y, rows, n, rpc,
-                     (double*)workspace);
+  if (planar)
+    hipLaunchKernelGGL(pack_colsum_kernel<true>, dim3((n / 4 + 63) / 64, chunks), dim3(256), 0, st, x, (uint2*)y, rows, n,
+                       rpc, (double*)workspace);
+  else
+    hipLaunchKernelGGL(pack_colsum_kernel<false>, dim3((n / 4 + 63) / 64, chunks), dim3(256), 0, st, x, (uint2*)y, rows,
+                       n, rpc, (double*)workspace);
   hipLaunchKernelGGL(colsum_final_kernel, dim3((n + 255) / 256), dim3(256), 0, st, (const double*)workspace, chunks, n,
                      out, beta);
   return launch_status();

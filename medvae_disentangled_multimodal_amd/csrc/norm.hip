@@ -53,7 +53,8 @@ struct GnArgs {
   float drop_p;
   unsigned long long seed;
   double* ws;  // [nb][chunks][C][2]
-  int y_split;  // forward apply: write y as split4_bf16 groups (1, the 3xBF16 GEMM operand format) or packed bf16 (2)
+  int y_split;  // forward apply: write y as split4_bf16 groups (1), packed bf16 (2) or planar 3xBF16 (3: bf16 hi plane
+                // of nb*hw*C elements, then the lo plane) -- the GEMM operand formats
   const float* dx_add;  // backward: optional gradient of the same tensor from another branch, summed into dx
   // process-wide dropout salt in device memory (mvae_set_dropout_salt): mixed into the seed, so a replayed HIP
   // graph -- whose kernel arguments, seeds included, are frozen -- still draws a fresh mask once the salt advances
@@ -281,9 +282,14 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(GnArgs a, const float* __
             }
           }
           const float4 ov{o[0], o[1], o[2], o[3]};
-          if (a.y_split == 2)  // packed bf16 (bf16-mixed GEMM operand): element offset * 2 B
-            *(uint2*)((__bf16*)y + off) = uint2{pk_bf16x2(ov.x, ov.y), pk_bf16x2(ov.z, ov.w)};
-          else if (a.y_split)
+          if (a.y_split >= 2) {  // packed bf16 / planar 3xBF16 hi plane: element offset * 2 B
+            const unsigned h01 = pk_bf16x2(ov.x, ov.y), h23 = pk_bf16x2(ov.z, ov.w);
+            *(uint2*)((__bf16*)y + off) = uint2{h01, h23};
+            if (a.y_split == 3)
+              *(uint2*)((__bf16*)y + (long long)a.nb * a.hw * a.C + off) =
+                  uint2{pk_bf16x2(ov.x - __uint_as_float(h01 << 16), ov.y - __uint_as_float(h01 & 0xFFFF0000u)),
+                        pk_bf16x2(ov.z - __uint_as_float(h23 << 16), ov.w - __uint_as_float(h23 & 0xFFFF0000u))};
+          } else if (a.y_split)
             *(uint4*)(yp + (long long)r * a.C) = split4_bf16(ov);
           else
             *(float4*)(yp + (long long)r * a.C) = ov;
@@ -581,6 +587,8 @@ __device__ __forceinline__ void gn_fwd_unit(const GnArgs& a, int SC, int u, cons
   const __amdgpu_buffer_rsrc_t yr = un.rsrc(y);
   const __amdgpu_buffer_rsrc_t ybr =
       __builtin_amdgcn_make_buffer_rsrc((void*)((__bf16*)y + un.ubase), (short)0, (int)(un.bytes >> 1), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ylr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((__bf16*)y + (long long)a.nb * a.hw * a.C + un.ubase), (short)0, (int)(un.bytes >> 1), 0x00020000);
   const unsigned vo = (unsigned)(rph * a.C + c4 * 4) * 4u;
   const int rstep = rpar * a.C * 4;
 #pragma unroll
@@ -596,10 +604,16 @@ __device__ __forceinline__ void gn_fwd_unit(const GnArgs& a, int SC, int u, cons
       }
     }
     const float4 ov{o[0], o[1], o[2], o[3]};
-    if (a.y_split == 2) {  // packed bf16: half the byte offsets, 8-B stores (rows past hw: dropped)
+    if (a.y_split >= 2) {  // packed bf16 / planar hi plane: half the byte offsets, 8-B stores (rows past hw: dropped)
       typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{pk_bf16x2(ov.x, ov.y), pk_bf16x2(ov.z, ov.w)}, ybr,
-                                            (vo >> 1) + (unsigned)(i * (rstep >> 1)), 0, 0);
+      const unsigned h01 = pk_bf16x2(ov.x, ov.y), h23 = pk_bf16x2(ov.z, ov.w);
+      const unsigned o2 = (vo >> 1) + (unsigned)(i * (rstep >> 1));
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{h01, h23}, ybr, o2, 0, 0);
+      if (a.y_split == 3)  // lo plane
+        __builtin_amdgcn_raw_buffer_store_b64(
+            u32x2{pk_bf16x2(ov.x - __uint_as_float(h01 << 16), ov.y - __uint_as_float(h01 & 0xFFFF0000u)),
+                  pk_bf16x2(ov.z - __uint_as_float(h23 << 16), ov.w - __uint_as_float(h23 & 0xFFFF0000u))},
+            ylr, o2, 0, 0);
       continue;
     }
     const uint4 sp = a.y_split ? split4_bf16(ov) : uint4{0u, 0u, 0u, 0u};

@@ -203,22 +203,58 @@ def _al16(*ts) -> bool:
     return all(t.data_ptr() % 16 == 0 for t in ts)
 
 
-# bf16-mixed convolutions on packed bf16 operands (MVAE_CONV_BF16: the GEMM stages them into LDS by DMA in 64-deep
-# K-tiles, no staging registers or conversion). MVAE_NO_BF16_DMA=1 keeps the register-staged bf16 loop on fp32
-# operands.
+# Convolutions on DMA-staged operands: the GEMM stages them into LDS by DMA (no staging registers, conversion or
+# split). bf16-mixed: packed bf16 (MVAE_CONV_BF16, 64-deep K-tiles; default, MVAE_NO_BF16_DMA=1 keeps the
+# register-staged bf16 loop on fp32 operands). fp32-class 3xBF16: planar hi / lo bf16 planes (MVAE_CONV_PLANAR,
+# 32-deep K-tiles) -- opt-in (MVAE_PLANAR_DMA=1): measured on c4 (same box) the planar weight gradient runs 10 % faster
+# (384 -> 421 TF/s) but fwd / dgrad 5-7 % slower than the hand-pipelined register loop, and the planar dy / x passes
+# (8 B per element) cost more than the rest gains: 453 -> 427 img/s.
 BF16_DMA = os.environ.get("MVAE_NO_BF16_DMA") is None
+PLANAR_DMA = os.environ.get("MVAE_PLANAR_DMA") is not None
 MVAE_CONV_BF16 = 128
+MVAE_CONV_PLANAR = 256
+
+
+def _dma_fmt() -> int:
+    """operand format of the DMA-staged conv path in the current math mode: 2 = packed bf16, 3 = planar 3xBF16
+    (the GroupNorm y_split / weight-prep split codes), 0 = none."""
+    if _MATH[0] == 1 and BF16_DMA:
+        return 2
+    if _MATH[0] == 0 and PLANAR_DMA:
+        return 3
+    return 0
 
 
 def _bf16_dma() -> bool:
-    return BF16_DMA and _MATH[0] == 1
+    return _dma_fmt() != 0
+
+
+# 3xBF16 mode: the planar DMA path for convolutions of at least this many MACs (the c4 layers; the small layers of the
+# 28x28 models keep their tuned register-staged / direct kernels). One rule for the GroupNorm that writes a conv's
+# input and for the conv's three GEMMs, so their operand formats agree.
+PLANAR_MIN_MACS = 1e11
+
+
+def _dma_ok(macs: float) -> bool:
+    f = _dma_fmt()
+    return f == 2 or (f == 3 and macs >= PLANAR_MIN_MACS)
+
+
+def _dma_flag() -> int:
+    return MVAE_CONV_PLANAR if _dma_fmt() == 3 else MVAE_CONV_BF16
+
+
+def _dma_bytes(numel: int) -> int:
+    """bytes of a DMA-staged operand of numel elements (packed bf16: 2 per element; planar: two bf16 planes)"""
+    return numel * (4 if _dma_fmt() == 3 else 2)
 
 
 def pack_bf16(t: torch.Tensor, key: str) -> torch.Tensor:
-    """Packed bf16 (round to nearest even) copy of an fp32 tensor in arena scratch `key` (2 B per element, same
-    element order)."""
-    out = ARENA.get(key, t.numel() * 2, t.device)
-    _lib.call("mvae_pack_bf16", t.data_ptr(), out.data_ptr(), t.numel(), _stream(t))
+    """DMA-staged operand copy of an fp32 tensor in arena scratch `key`: packed bf16 (round to nearest even, 2 B per
+    element) in the bf16-mixed mode, planar 3xBF16 (hi plane then lo plane) in the 3xBF16 mode."""
+    out = ARENA.get(key, _dma_bytes(t.numel()), t.device)
+    fn = "mvae_split_planar" if _dma_fmt() == 3 else "mvae_pack_bf16"
+    _lib.call(fn, t.data_ptr(), out.data_ptr(), t.numel(), _stream(t))
     return out
 
 
@@ -293,7 +329,7 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
     split = WEIGHT_SPLIT and _splits_ok() and c % 4 == 0 and _al16(x) and not g.pointwise and g.kh * g.kw <= 32
     if x_split and (g.pointwise or g.upsample or c % 4 or not _al16(x)):
         raise RuntimeError("conv2d: a pre-split input needs a non-pointwise, non-upsample conv with cin % 4 == 0")
-    if _bf16_dma() and c % 8 == 0 and not x_split and _al16(x) and not g.pointwise and g.kh * g.kw <= 32 and \
+    if _dma_ok(ref / 2) and c % 8 == 0 and not x_split and _al16(x) and not g.pointwise and g.kh * g.kw <= 32 and \
             (sub or not g.upsample):
         return _conv_fwd_bf16(x, w, b, res, g, y, n, c, h, wd, co, ho, wo, sub, alg, ref, gn_part, st, x_bf16)
     if x_bf16:
@@ -326,41 +362,42 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
 
 def _conv_fwd_bf16(x, w, b, res, g, y, n, c, h, wd, co, ho, wo, sub, alg, ref, gn_part, st, x_bf16=False):
     """bf16-mixed forward on packed bf16 x and weights (MVAE_CONV_BF16)."""
+    fmt, flag = _dma_fmt(), _dma_flag()
     xb = x if x_bf16 else pack_bf16(x, "xbf")
     if sub:
-        wg = ARENA.get("w4", 16 * co * c * 2, x.device)
-        _lib.call("mvae_conv_weight_upsample_fwd", w.data_ptr(), wg.data_ptr(), co, c, 2, st)
+        wg = ARENA.get("w4", _dma_bytes(16 * co * c), x.device)
+        _lib.call("mvae_conv_weight_upsample_fwd", w.data_ptr(), wg.data_ptr(), co, c, fmt, st)
     else:
         wg = pack_bf16(w, "wsplit")
     with _timed("conv_fwd", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
         if sub:
             _lib.call("mvae_conv2d_upsample_nhwc", xb.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n,
-                      h, wd, c, co, 2, st)
+                      h, wd, c, co, fmt, st)
         elif gn_part is not None:
             _lib.call("mvae_conv2d_gnstats_nhwc", xb.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(),
-                      n, h, wd, c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, MVAE_CONV_BF16,
-                      gn_part.data_ptr(), st)
+                      n, h, wd, c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, flag, gn_part.data_ptr(), st)
         else:
             _conv_call(xb.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y, n, h, wd, c, co, g.kh, g.kw, g.stride,
-                       g.pad_t, g.pad_l, ho, wo, MVAE_CONV_BF16, st)
+                       g.pad_t, g.pad_l, ho, wo, flag, st)
     return y
 
 
-def pack_dy(dy: torch.Tensor, g: ConvGeom, bias_out=None, beta: float = 1.0):
+def pack_dy(dy: torch.Tensor, g: ConvGeom, cin: int, bias_out=None, beta: float = 1.0):
     """dy as packed bf16 for the backward GEMMs of the bf16-mixed mode, or None when that path does not apply.
     bias_out: also accumulate the conv bias gradient (beta * bias_out + column sums of the fp32 dy) from the same pass
     (mvae_pack_bf16_colsum). Returns (packed dy or None, whether the bias gradient was produced)."""
     if not _bf16_dma() or g.pointwise or dy.dim() != 4 or dy.shape[1] % 8 or g.kh * g.kw > 32 or not _al16(dy) or \
-            not dy.is_contiguous(memory_format=CL):
+            not dy.is_contiguous(memory_format=CL) or not _dma_ok(float(dy.numel()) * cin * g.kh * g.kw):
         return None, False
     if bias_out is None:
         return pack_bf16(dy, "dybf"), False
     n, co, ho, wo = dy.shape
     rows = n * ho * wo
-    out = ARENA.get("dybf", dy.numel() * 2, dy.device)
+    out = ARENA.get("dybf", _dma_bytes(dy.numel()), dy.device)
     ws = ARENA.get("bias", _lib.query("mvae_bias_grad_workspace_bytes", rows, co), dy.device)
-    _lib.call("mvae_pack_bf16_colsum", dy.data_ptr(), out.data_ptr(), rows, co, bias_out.data_ptr(), float(beta),
-              ws.data_ptr(), ws.numel(), _stream(dy))
+    fn = "mvae_split_planar_colsum" if _dma_fmt() == 3 else "mvae_pack_bf16_colsum"
+    _lib.call(fn, dy.data_ptr(), out.data_ptr(), rows, co, bias_out.data_ptr(), float(beta), ws.data_ptr(), ws.numel(),
+              _stream(dy))
     return out, True
 
 
@@ -442,25 +479,26 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
 def _conv_dgrad_bf16(dyb, w, dx, g, n, c, h, wd, co, ho, wo, flops, shp, st):
     """bf16-mixed input gradient on packed bf16 dy and weights (MVAE_CONV_BF16)."""
     dev = dx.device
+    fmt, flag = _dma_fmt(), _dma_flag()
     if g.upsample:
-        wt = ARENA.get("wt", c * 16 * co * 2, dev)
-        _lib.call("mvae_conv_weight_upsample_dgrad", w.data_ptr(), wt.data_ptr(), co, c, 2, st)
+        wt = ARENA.get("wt", _dma_bytes(c * 16 * co), dev)
+        _lib.call("mvae_conv_weight_upsample_dgrad", w.data_ptr(), wt.data_ptr(), co, c, fmt, st)
         with _timed("conv_dgrad", flops * 4 / 9, shp, flops):
             # dX = stride-2, pad-1 4x4 (forward-gather) conv of dY with the tap-summed kernel
             _lib.call("mvae_conv2d_nhwc", dyb.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
-                      4, 4, 2, 1, 1, h, wd, MVAE_CONV_BF16, st)
+                      4, 4, 2, 1, 1, h, wd, flag, st)
         return dx
-    wt = ARENA.get("wt", c * g.kh * g.kw * co * 2, dev)
-    _lib.call("mvae_conv_weight_transpose", w.data_ptr(), wt.data_ptr(), co, g.kh, g.kw, c, 2, st)
+    wt = ARENA.get("wt", _dma_bytes(c * g.kh * g.kw * co), dev)
+    _lib.call("mvae_conv_weight_transpose", w.data_ptr(), wt.data_ptr(), co, g.kh, g.kw, c, fmt, st)
     if g.stride == 2 and h % 2 == 0 and wd % 2 == 0 and g.kh <= 4 and g.kw <= 4 and STRIDE2_CLASSES:
         wc = ARENA.get("wcls", c * g.kh * g.kw * co * 4, dev)
         with _timed("conv_dgrad", flops, shp):
             _lib.call("mvae_conv2d_dgrad_stride2_nhwc", dyb.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, h, wd, c, co,
-                      g.kh, g.kw, g.pad_t, g.pad_l, ho, wo, 4, wc.data_ptr(), wc.numel(), st)
+                      g.kh, g.kw, g.pad_t, g.pad_l, ho, wo, 8 if fmt == 3 else 4, wc.data_ptr(), wc.numel(), st)
         return dx
     with _timed("conv_dgrad", flops, shp):
         _conv_call(dyb.data_ptr(), wt.data_ptr(), None, None, dx, n, ho, wo, co, c, g.kh, g.kw, g.stride, g.pad_t,
-                   g.pad_l, h, wd, 2 | MVAE_CONV_BF16, st)
+                   g.pad_l, h, wd, 2 | flag, st)
     return dx
 
 
@@ -483,7 +521,7 @@ def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool
         ws = ARENA.get("ws", nbytes, dy.device)
         with _timed("conv_wgrad", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
             _lib.call("mvae_conv2d_wgrad_nhwc", dyb.data_ptr(), xb.data_ptr(), dw.data_ptr(), None, float(beta), n, h,
-                      wd, c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, MVAE_CONV_BF16, ws.data_ptr(),
+                      wd, c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, _dma_flag(), ws.data_ptr(),
                       ws.numel(), st)
         return False
     if x_bf16:
@@ -622,7 +660,7 @@ class Conv2dFn(torch.autograd.Function):
             bt = _main_grad(ctx.bias_ref) if want_b else None
             if want_b and bt is None:
                 db_ret = torch.empty(dy.shape[1], device=dy.device, dtype=torch.float32)
-            dyb, bias_done = pack_dy(dy, g, bt if bt is not None else db_ret, 1.0 if bt is not None else 0.0)
+            dyb, bias_done = pack_dy(dy, g, w.shape[1], bt if bt is not None else db_ret, 1.0 if bt is not None else 0.0)
             if not bias_done:
                 db_ret = None
         dys = split_dy(dy) if not g.pointwise and not _subpixel_upsample(g) and dyb is None else None
@@ -816,9 +854,9 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
     the ResnetBlock / norm_out pattern, encoder_decoder.py:141-163, :318-328); in the bf16-mixed mode, with a known
     output channel count that is a multiple of 8, packed bf16 for the LDS-DMA GEMM."""
     packed = bool(for_conv and not isinstance(for_conv, bool) and int(for_conv) % 8 == 0 and _bf16_dma() and
-                  x.shape[1] % 8 == 0 and _al16(x))
-    split = 2 if packed else int(bool(for_conv and ACT_SPLIT and _splits_ok() and not _bf16_dma() and
-                                      x.shape[1] % 4 == 0))
+                  x.shape[1] % 8 == 0 and _al16(x) and _dma_ok(9.0 * x.numel() * int(for_conv)))
+    split = _dma_fmt() if packed else int(bool(for_conv and ACT_SPLIT and _splits_ok() and not _bf16_dma() and
+                                                x.shape[1] % 4 == 0))
     part = getattr(x, GN_PART_ATTR, None)
     if part is not None:
         delattr(x, GN_PART_ATTR)  # consumed once; frees the statistics with the next allocation cycle
@@ -828,7 +866,7 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
         part = part[0] if ok else None
     link = GnBwdLink(groups, silu) if (for_conv and GN_BWD_FUSED and drop_p == 0.0 and x.requires_grad) else None
     y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink, part, link)
-    if split == 2:
+    if split >= 2:
         setattr(y, BF16_ATTR, True)
     elif split:
         setattr(y, XSPLIT_ATTR, True)

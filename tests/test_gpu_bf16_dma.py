@@ -1,10 +1,14 @@
-"""bf16-mixed convolutions on packed bf16 operands (MVAE_CONV_BF16: LDS-DMA main loop of the implicit GEMM, 64-deep
-K-tiles, source-swizzled ROW images). The edge cases of that loader: channel counts that are multiples of 8 but not
+"""Convolutions on DMA-staged operands: bf16-mixed on packed bf16 operands (MVAE_CONV_BF16: LDS-DMA main loop of the
+implicit GEMM, 64-deep K-tiles, source-swizzled ROW images) and the fp32-class 3xBF16 mode on planar hi / lo bf16
+operands (MVAE_CONV_PLANAR, 32-deep K-tiles; the size rule ops.PLANAR_MIN_MACS is lowered to 0 here so the small
+edge cases take that path). The edge cases of that loader: channel counts that are multiples of 8 but not
 of 64 (K-tiles straddle filter taps, no K permutation), ragged pixel tails (M not a multiple of any tile), the
 stride-2 Downsample forward and its input gradient by parity class, the sub-pixel Upsample forward and its 4x4
 stride-2 input gradient, and a 1x1-tap conv. Reference: float64 on the bf16-rounded GEMM operands (forward: x, w;
 input gradient: dy, w), so only fp32 accumulation differs -- tolerance 2e-5 (tests/test_gpu_c5.py). The same
-launches through the register-staged bf16 loop (ops.BF16_DMA off) agree to the same tolerance."""
+launches through the register-staged bf16 loop (ops.BF16_DMA off) agree to the same tolerance. 3xBF16: float64 on the
+fp32 operands at the fp32-class conv tolerance 2e-4 (tests/test_gpu_kernels.py CONV_TOL), and the planar path against
+the register-staged 3xBF16 loop (same K order, same split) at 2e-6."""
 import math
 
 import pytest
@@ -43,7 +47,7 @@ CASES = [
 ]
 
 
-def _run(dev, case, dma):
+def _run(dev, case, dma, prec="bf16-mixed"):
     from medvae_disentangled_multimodal_amd import ops
     n, ci, co, h, w, k, s, pads, ups = case
     g = torch.Generator().manual_seed(ci * 13 + co + h)
@@ -54,9 +58,10 @@ def _run(dev, case, dma):
     xd = x.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_()
     wd = wt.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_()
     bd = b.to(dev).requires_grad_()
-    prev_dma = ops.BF16_DMA
-    ops.BF16_DMA = dma
-    prev = ops.set_precision("bf16-mixed")
+    saved = (ops.BF16_DMA, ops.PLANAR_DMA, ops.PLANAR_MIN_MACS)
+    ops.BF16_DMA = ops.PLANAR_DMA = dma
+    ops.PLANAR_MIN_MACS = 0
+    prev = ops.set_precision(prec)
     try:
         y = ops.conv2d(xd, wd, bd, geom)
         dy = torch.randn(y.shape, generator=g)
@@ -64,8 +69,8 @@ def _run(dev, case, dma):
         torch.cuda.synchronize()
     finally:
         ops.restore_math_mode(prev)
-        ops.BF16_DMA = prev_dma
-    return x, wt, b, dy, y.detach(), xd.grad, geom
+        ops.BF16_DMA, ops.PLANAR_DMA, ops.PLANAR_MIN_MACS = saved
+    return x, wt, b, dy, y.detach(), xd.grad, geom, wd.grad, bd.grad
 
 
 def _subpixel_kernels(w):
@@ -84,7 +89,7 @@ def _subpixel_kernels(w):
 
 @pytest.mark.parametrize("case", CASES)
 def test_bf16_dma_conv_fwd_dgrad(dev, case):
-    x, wt, b, dy, y, dx, geom = _run(dev, case, True)
+    x, wt, b, dy, y, dx, geom, _, _ = _run(dev, case, True)
     n, ci, co, h, w, k, s, pads, ups = case
     xr = bf(x).requires_grad_()
     if ups:
@@ -105,7 +110,28 @@ def test_bf16_dma_conv_fwd_dgrad(dev, case):
 
 @pytest.mark.parametrize("case", CASES[:4])
 def test_bf16_dma_matches_register_staged_loop(dev, case):
-    _, _, _, _, y1, dx1, _ = _run(dev, case, True)
-    _, _, _, _, y0, dx0, _ = _run(dev, case, False)
+    _, _, _, _, y1, dx1, _, _, _ = _run(dev, case, True)
+    _, _, _, _, y0, dx0, _, _, _ = _run(dev, case, False)
     assert rel(y1, y0) < TOL
     assert rel(dx1, dx0) < TOL
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_planar_3xbf16_conv_fwd_dgrad_wgrad(dev, case):
+    x, wt, b, dy, y, dx, geom, dw, db = _run(dev, case, True, "32")
+    n, ci, co, h, w, k, s, pads, ups = case
+    xr = x.double().requires_grad_()
+    wr = wt.double().requires_grad_()
+    xin = F.interpolate(xr, scale_factor=2.0, mode="nearest") if ups else xr
+    pt, pl, pb, pr = pads
+    yr = F.conv2d(F.pad(xin, (pl, pr, pt, pb)), wr, b.double(), stride=s)
+    yr.backward(dy.double())
+    assert rel(y, yr) < 2e-4
+    assert rel(dx, xr.grad) < 2e-4
+    assert rel(dw, wr.grad) < 2e-4
+    assert rel(db, dy.double().sum((0, 2, 3))) < 1e-5
+    # the register-staged 3xBF16 loop: same operand split, same K order
+    _, _, _, _, y0, dx0, _, dw0, _ = _run(dev, case, False, "32")
+    assert rel(y, y0) < 2e-6
+    assert rel(dx, dx0) < 2e-6
+    assert rel(dw, dw0) < 2e-6
