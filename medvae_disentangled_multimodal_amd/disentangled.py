@@ -31,7 +31,7 @@ ROUTING_KERNELS = os.environ.get("MVAE_NO_ROUTING") is None
 
 
 def _nan_to_zero(t):
-    return torch.where(torch.isnan(t), torch.zeros_like(t), t)
+    return torch.where(torch.isnan(t), 0.0, t)
 
 
 class DisentangledConditionalVAE(BaseVAE):

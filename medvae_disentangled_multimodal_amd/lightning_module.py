@@ -150,7 +150,7 @@ class VAELightningModule(_Base):
             loss_dict = self.criterion(inputs=x, reconstructions=outputs["reconstruction"],
                                        posteriors=outputs["posterior"], priors=outputs["prior"])
         loss = loss_dict["loss"]
-        loss = torch.where(torch.isfinite(loss), loss, torch.full_like(loss, 1e6))
+        loss = torch.where(torch.isfinite(loss), loss, 1e6)
         for k, v in loss_dict.items():
             self.log(f"train/{k}", v, prog_bar=True, logger=True, on_step=True, on_epoch=True)
         self._last_outputs = outputs
@@ -198,7 +198,7 @@ class VAELightningModule(_Base):
         else:
             loss = self.criterion(inputs=x, reconstructions=rec, posteriors=outputs["posterior"],
                                   priors=outputs["prior"])["loss"]
-        loss = torch.where(torch.isfinite(loss), loss, torch.full_like(loss, 1e6))
+        loss = torch.where(torch.isfinite(loss), loss, 1e6)
         self.log(f"{split}/loss", loss, prog_bar=True, logger=True, on_epoch=True)
         return outputs
 
@@ -370,14 +370,17 @@ class VAELightningModule(_Base):
         prev = ops.set_precision(self.precision)
         try:
             self.optimizer.zero_grad()
+            ops.prep_flat_weights(self.flat.data)  # every conv weight in the GEMM format, one launch
             loss = self.training_step(batch, batch_idx, eps=eps)
             if self.process_group is not None:
                 self.process_group.begin_backward()
             loss.backward()
             if self.process_group is not None:
                 self.process_group.allreduce_gradients(self.flat)
+            ops.flat_weights_stale()
             self.optimizer.step(used=self._used_mask())
         finally:
+            ops.flat_weights_stale()
             ops.restore_math_mode(prev)
         self.global_step_count += 1
         # hand back values, not the step's autograd graph: a graph kept alive past the step pins its AccumulateGrad

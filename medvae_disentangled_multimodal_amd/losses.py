@@ -47,7 +47,7 @@ class VAELoss(nn.Module):
 def _finite_or_zero(v: torch.Tensor) -> torch.Tensor:
     # device-side replacement of the reference's `if isnan(v).any(): v = 0` (no host sync); the term's own
     # gradient is gated by ops.finite_gated where it is computed, so a non-finite term contributes nothing
-    return torch.where(torch.isfinite(v), v, torch.zeros_like(v))
+    return torch.where(torch.isfinite(v), v, 0.0)
 
 
 class DisentangledVAELoss(nn.Module):
@@ -71,7 +71,7 @@ class DisentangledVAELoss(nn.Module):
         con = _finite_or_zero(outputs["contrastive_loss"])
         total = (self.recon_weight * recon + self.kl_weight * kl + self.separation_weight * sep +
                  self.contrastive_weight * con)
-        total = torch.where(torch.isfinite(total), total, torch.full_like(total, 1e6))
+        total = torch.where(torch.isfinite(total), total, 1e6)
         return {"loss": total, "recon_loss": recon, "kl_loss": kl, "separation_loss": sep,
                 "contrastive_loss": con}
 

@@ -249,6 +249,53 @@ def _dma_bytes(numel: int) -> int:
     return numel * (4 if _dma_fmt() == 3 else 2)
 
 
+class _FlatWeights:
+    """The conv weights of a step prepared in one launch: fit_step converts the whole flat parameter buffer
+    (optim.FlatParameters: every tensor 16-B aligned) into the forward GEMM's weight format -- split4_bf16 in the
+    3xBF16 mode, packed bf16 in the bf16-mixed mode -- before the forward, and every conv forward then reads its
+    weight's slice instead of converting it (one launch per conv, ~30 per c3 step). Valid until the optimizer step."""
+    __slots__ = ("base", "end", "buf", "fmt", "fresh")
+
+    def __init__(self):
+        self.base = self.end = 0
+        self.buf = None
+        self.fmt = 0
+        self.fresh = False
+
+
+_FLATW = _FlatWeights()
+
+
+def prep_flat_weights(flat_data: torch.Tensor):
+    """Convert the flat parameter buffer into the forward weight format of the current math mode (see
+    _FlatWeights); a no-op in modes without a converted weight format."""
+    fmt = 2 if _dma_fmt() == 2 else (1 if _MATH[0] == 0 and WEIGHT_SPLIT and _dma_fmt() == 0 else 0)
+    _FLATW.fresh = False
+    n = flat_data.numel()
+    if fmt == 0 or n % 8 or not _al16(flat_data):
+        return
+    nbytes = n * (4 if fmt == 1 else 2)
+    if _FLATW.buf is None or _FLATW.buf.numel() < nbytes or _FLATW.buf.device != flat_data.device:
+        _FLATW.buf = torch.empty(nbytes, dtype=torch.uint8, device=flat_data.device)
+    fn = "mvae_split_bf16" if fmt == 1 else "mvae_pack_bf16"
+    _lib.call(fn, flat_data.data_ptr(), _FLATW.buf.data_ptr(), n, _stream(flat_data))
+    _FLATW.base, _FLATW.end, _FLATW.fmt, _FLATW.fresh = flat_data.data_ptr(), flat_data.data_ptr() + 4 * n, fmt, True
+
+
+def flat_weights_stale():
+    _FLATW.fresh = False
+
+
+def _flat_weight_ptr(w: torch.Tensor, fmt: int) -> Optional[int]:
+    """Device pointer of w's prepared copy (fmt 1: split4_bf16, 2: packed bf16), or None."""
+    p = w.data_ptr()
+    if not (_FLATW.fresh and _FLATW.fmt == fmt and _FLATW.base <= p < _FLATW.end and
+            w.is_contiguous(memory_format=CL)):
+        return None
+    off = p - _FLATW.base
+    return _FLATW.buf.data_ptr() + (off if fmt == 1 else off // 2)
+
+
 def pack_bf16(t: torch.Tensor, key: str) -> torch.Tensor:
     """DMA-staged operand copy of an fp32 tensor in arena scratch `key`: packed bf16 (round to nearest even, 2 B per
     element) in the bf16-mixed mode, planar 3xBF16 (hi plane then lo plane) in the 3xBF16 mode."""
@@ -339,8 +386,12 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
         wg = ARENA.get("w4", 16 * co * c * 4, x.device)
         _lib.call("mvae_conv_weight_upsample_fwd", w.data_ptr(), wg.data_ptr(), co, c, int(split), st)
     elif split:
-        wg = ARENA.get("wsplit", w.numel() * 4, x.device)
-        _lib.call("mvae_split_bf16", w.data_ptr(), wg.data_ptr(), w.numel(), st)
+        wp = _flat_weight_ptr(w, 1)
+        if wp is None:
+            wg = ARENA.get("wsplit", w.numel() * 4, x.device)
+            _lib.call("mvae_split_bf16", w.data_ptr(), wg.data_ptr(), w.numel(), st)
+            wp = wg.data_ptr()
+    wptr = wg.data_ptr() if not split or sub else wp
     with _timed("conv_fwd", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
         if g.pointwise:
             # 1x1 conv = GEMM [pixels][cin] x [cout][cin]^T
@@ -352,10 +403,10 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
         else:
             mode = (1 if g.upsample else 0) | (MVAE_CONV_WSPLIT if split else 0) | (MVAE_CONV_XSPLIT if x_split else 0)
             if gn_part is not None:
-                _lib.call("mvae_conv2d_gnstats_nhwc", x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(),
+                _lib.call("mvae_conv2d_gnstats_nhwc", x.data_ptr(), wptr, _ptr(b), _ptr(res), y.data_ptr(),
                           n, h, wd, c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, mode, gn_part.data_ptr(), st)
             else:
-                _conv_call(x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y, n, h, wd, c, co, g.kh, g.kw, g.stride,
+                _conv_call(x.data_ptr(), wptr, _ptr(b), _ptr(res), y, n, h, wd, c, co, g.kh, g.kw, g.stride,
                            g.pad_t, g.pad_l, ho, wo, mode, st)
     return y
 
@@ -368,16 +419,18 @@ def _conv_fwd_bf16(x, w, b, res, g, y, n, c, h, wd, co, ho, wo, sub, alg, ref, g
         wg = ARENA.get("w4", _dma_bytes(16 * co * c), x.device)
         _lib.call("mvae_conv_weight_upsample_fwd", w.data_ptr(), wg.data_ptr(), co, c, fmt, st)
     else:
-        wg = pack_bf16(w, "wsplit")
+        wp = _flat_weight_ptr(w, 2) if fmt == 2 else None
+        wg = pack_bf16(w, "wsplit") if wp is None else None
+    wptr = wg.data_ptr() if wg is not None else wp
     with _timed("conv_fwd", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
         if sub:
-            _lib.call("mvae_conv2d_upsample_nhwc", xb.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n,
+            _lib.call("mvae_conv2d_upsample_nhwc", xb.data_ptr(), wptr, _ptr(b), _ptr(res), y.data_ptr(), n,
                       h, wd, c, co, fmt, st)
         elif gn_part is not None:
-            _lib.call("mvae_conv2d_gnstats_nhwc", xb.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(),
+            _lib.call("mvae_conv2d_gnstats_nhwc", xb.data_ptr(), wptr, _ptr(b), _ptr(res), y.data_ptr(),
                       n, h, wd, c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, flag, gn_part.data_ptr(), st)
         else:
-            _conv_call(xb.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y, n, h, wd, c, co, g.kh, g.kw, g.stride,
+            _conv_call(xb.data_ptr(), wptr, _ptr(b), _ptr(res), y, n, h, wd, c, co, g.kh, g.kw, g.stride,
                        g.pad_t, g.pad_l, ho, wo, flag, st)
     return y
 
@@ -1092,7 +1145,7 @@ class _FiniteGateFn(torch.autograd.Function):
         for r in req:
             gr = got.pop(0) if torch.is_tensor(r) and r.requires_grad else None
             if gr is not None:
-                gr = torch.where(ctx.ok, gr, torch.zeros((), device=gr.device, dtype=gr.dtype))
+                gr = torch.where(ctx.ok, gr, 0.0)  # (scalar other: no fill launch)
             out.append(gr)
         return (None, *out)
 

@@ -26,8 +26,18 @@ def _posterior(mean, logvar, std=None):
     return post
 
 
+_UNIT = {}
+
+
 def _prior(mean, logvar):
-    prior = Normal(torch.zeros_like(mean), torch.ones_like(logvar), validate_args=False)
+    # N(0, I) of the latent's shape as expanded views of cached per-device 0-d constants: the same distribution as
+    # the reference's Normal(zeros_like(mu), ones_like(logvar)) without two fill launches per step
+    key = (mean.device, mean.dtype)
+    if key not in _UNIT:
+        _UNIT[key] = (torch.zeros((), device=mean.device, dtype=mean.dtype),
+                      torch.ones((), device=mean.device, dtype=mean.dtype))
+    zero, one = _UNIT[key]
+    prior = Normal(zero.expand(mean.shape), one.expand(logvar.shape), validate_args=False)
     prior._mvae_standard = True
     return prior
 
