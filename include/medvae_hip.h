@@ -250,6 +250,25 @@ int mvae_kl_bwd(const float* mu, const float* logvar, long long ld, const float*
                 float* dmu, float* dlogvar, long long npix, int zc, void* stream);
 int mvae_recon_bwd(int kind, const float* a, const float* b, const float* gscale, double mult, float* da,
                    long long n, void* stream);
+/* DisentangledConditionalVAE.forward's latent side in one pass (src/models/disentangled_conditional_vae.py:
+ * 388-398 after encode's NaN scrub, :255-301; reparameterize base_vae.py:83-87): mu = clamp(nan0(h_mu), -10, 10),
+ * logvar likewise, s = exp(logvar/2), z = mu + eps*s, std = clamp(s, 1e-6, 10); outputs dense [npix][zc].
+ * The backward writes the gradients of h_mu / h_logvar at row stride ld_out (the encoder output's gradient);
+ * null incoming gradients count as zero. */
+int mvae_latent_prep_fwd(const float* h_mu, const float* h_logvar, long long ld, const float* eps, float* mu,
+                         float* logvar, float* std_out, float* z, long long npix, int zc, void* stream);
+int mvae_latent_prep_bwd(const float* h_mu, const float* h_logvar, long long ld, const float* eps, const float* g_mu,
+                         const float* g_logvar, const float* g_std, const float* g_z, float* d_mu, float* d_logvar,
+                         long long ld_out, long long npix, int zc, void* stream);
+/* DisentangledVAELoss's total (src/models/disentangled_conditional_vae.py:528-570): nt <= 4 device scalars v_i,
+ * o_i = v_i if finite else 0, total = sum w_i o_i (fp32, in order) or nonfinite_total when not finite;
+ * flags[0..nt] record finiteness for the backward: g_terms[i] = [v_i finite](g_i + w_i [total finite] g_total). */
+int mvae_loss_combine4_fwd(const float* v0, const float* v1, const float* v2, const float* v3, float w0, float w1,
+                           float w2, float w3, int nt, float nonfinite_total, float* total, float* o0, float* o1,
+                           float* o2, float* o3, float* flags, void* stream);
+int mvae_loss_combine4_bwd(const float* flags, float w0, float w1, float w2, float w3, int nt, const float* g_total,
+                           const float* g0, const float* g1, const float* g2, const float* g3, float* g_terms,
+                           void* stream);
 
 /* ---- optimizer step over one flat buffer ----------------------------------------------------------
  * on_before_optimizer_step (lightning_module.py:468-477) + configure_gradient_clipping (:452-466) +

@@ -66,6 +66,10 @@ SIGNATURES = {
     "mvae_loss_reduce": (I, [I, P, P, L, L, I, D, P, P, Z, P]),
     "mvae_reduce_workspace_bytes": (Z, []),
     "mvae_kl_bwd": (I, [P, P, L, P, D, P, P, L, I, P]),
+    "mvae_latent_prep_fwd": (I, [P, P, L, P, P, P, P, P, L, I, P]),
+    "mvae_latent_prep_bwd": (I, [P, P, L, P, P, P, P, P, P, P, L, L, I, P]),
+    "mvae_loss_combine4_fwd": (I, [P, P, P, P, F, F, F, F, I, F, P, P, P, P, P, P, P]),
+    "mvae_loss_combine4_bwd": (I, [P, F, F, F, F, I, P, P, P, P, P, P, P]),
     "mvae_recon_bwd": (I, [I, P, P, P, D, P, L, P]),
     "mvae_multi_tensor_adam": (I, [P, P, P, P, P, P, P, I, P, I, P, P, F, F, I, F, F, F, F, F, I, P, Z, P, P]),
     "mvae_multi_tensor_adam_workspace_bytes": (Z, [I, I]),

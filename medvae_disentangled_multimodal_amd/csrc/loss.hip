@@ -128,6 +128,105 @@ __global__ void __launch_bounds__(256) recon_bwd_kernel(int kind, const float* _
   }
 }
 
+// Latent preparation of the disentangled model, one pass (disentangled_conditional_vae.py:388-398 on the
+// encode output of :255-301, base_vae.py:83-87): with the NaN scrub of encode,
+//   mu = clamp(nan0(h_mu), -10, 10), lv = clamp(nan0(h_lv), -10, 10), s = exp(0.5 lv),
+//   z = mu + eps * s, std = clamp(s, 1e-6, 10)
+// replacing the isnan / where / clamp / exp / mul / clamp chain and the reparameterization launch.
+__global__ void __launch_bounds__(256) latent_prep_fwd_kernel(const float* __restrict__ hm, const float* __restrict__ hl,
+                                                              long long ld, const float* __restrict__ eps,
+                                                              float* __restrict__ mu, float* __restrict__ lv,
+                                                              float* __restrict__ sd, float* __restrict__ z,
+                                                              long long npix, int zc) {
+  const long long n = npix * zc;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const long long p = e / zc;
+    const int c = (int)(e - p * zc);
+    float m = hm[p * ld + c], l = hl[p * ld + c];
+    m = fminf(fmaxf(m != m ? 0.f : m, -10.f), 10.f);
+    l = fminf(fmaxf(l != l ? 0.f : l, -10.f), 10.f);
+    const float s = expf(0.5f * l);
+    mu[e] = m;
+    lv[e] = l;
+    sd[e] = fminf(fmaxf(s, 1e-6f), 10.f);
+    z[e] = m + eps[e] * s;
+  }
+}
+
+// Backward of latent_prep_fwd as torch's autograd composes it: the incoming gradients of mu / lv / std / z (null = 0)
+// give d(h_mu) = [h_mu not NaN, -10 <= h_mu <= 10] (g_mu + g_z) and d(h_lv) = [same for h_lv] (g_lv + g_z eps s/2 +
+// [1e-6 <= s <= 10] g_std s/2), written at row stride ldo (straight into the gradient of the encoder's [pixels][2 zc]
+// output: no chunk / cat / accumulation launches).
+__global__ void __launch_bounds__(256) latent_prep_bwd_kernel(const float* __restrict__ hm, const float* __restrict__ hl,
+                                                              long long ld, const float* __restrict__ eps,
+                                                              const float* __restrict__ gmu,
+                                                              const float* __restrict__ glv,
+                                                              const float* __restrict__ gsd,
+                                                              const float* __restrict__ gz, float* __restrict__ dm,
+                                                              float* __restrict__ dl, long long ldo, long long npix,
+                                                              int zc) {
+  const long long n = npix * zc;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const long long p = e / zc;
+    const int c = (int)(e - p * zc);
+    const float m = hm[p * ld + c], l = hl[p * ld + c];
+    const float lc = fminf(fmaxf(l != l ? 0.f : l, -10.f), 10.f);
+    const float s = expf(0.5f * lc);
+    const float g_z = gz ? gz[e] : 0.f;
+    const float g_m = (gmu ? gmu[e] : 0.f) + g_z;
+    float g_l = glv ? glv[e] : 0.f;
+    g_l += g_z * eps[e] * 0.5f * s;
+    if (gsd && s >= 1e-6f && s <= 10.f) g_l += gsd[e] * s * 0.5f;
+    dm[p * ldo + c] = (m >= -10.f && m <= 10.f) ? g_m : 0.f;  // NaN compares false: scrubbed values get 0
+    dl[p * ldo + c] = (l >= -10.f && l <= 10.f) ? g_l : 0.f;
+  }
+}
+
+// The weighted total of up to 4 scalar loss terms with DisentangledVAELoss's non-finite handling
+// (disentangled_conditional_vae.py:528-565): out[1 + i] = v_i if finite else 0, out[0] = sum_i w_i out[1 + i] in
+// order (fp32, no contraction: torch's 0-d arithmetic), replaced by `nonfinite_total` when it is not finite.
+// flags[i] = v_i finite, flags[nt] = total finite (read by the backward). One thread, one launch.
+// a product rounded to fp32 before any following add (hipcc's default -ffp-contract=fast ignores the contract
+// pragma; the empty asm keeps the multiply and the add separate, as torch's 0-d arithmetic rounds them)
+__device__ __forceinline__ float mul_rounded(float a, float b) {
+  float p = a * b;
+  asm volatile("" : "+v"(p));
+  return p;
+}
+
+struct CombineArgs {
+  const float* v[4];
+  float w[4];
+  float* o[5];  // forward: total, then the finite-or-zero terms (separate 0-d tensors)
+};
+
+__global__ void __launch_bounds__(64) loss_combine_fwd_entry(CombineArgs a, int nt, float nonfinite_total,
+                                                             float* __restrict__ flags) {
+  if (threadIdx.x != 0) return;
+  float tot = 0.f;
+  for (int i = 0; i < nt; ++i) {
+    const float x = *a.v[i];
+    const bool ok = isfinite(x);
+    const float f = ok ? x : 0.f;
+    *a.o[1 + i] = f;
+    flags[i] = ok ? 1.f : 0.f;
+    tot = i == 0 ? mul_rounded(a.w[i], f) : tot + mul_rounded(a.w[i], f);
+  }
+  const bool okt = isfinite(tot);
+  *a.o[0] = okt ? tot : nonfinite_total;
+  flags[nt] = okt ? 1.f : 0.f;
+}
+
+__global__ void __launch_bounds__(64) loss_combine_bwd_entry(CombineArgs a, int nt, const float* __restrict__ flags,
+                                                             const float* __restrict__ gtot, float* __restrict__ g) {
+  if (threadIdx.x != 0) return;
+  const float gt = (gtot && flags[nt] != 0.f) ? *gtot : 0.f;
+  for (int i = 0; i < nt; ++i) {
+    const float go = a.v[i] ? *a.v[i] : 0.f;  // a.v holds the incoming gradients of the per-term outputs here
+    g[i] = flags[i] != 0.f ? go + mul_rounded(a.w[i], gt) : 0.f;  // [v_i finite](g_out_i + w_i g_total)
+  }
+}
+
 static int egrid(long long n) { return (int)std::max<long long>(1, std::min<long long>((n + 255) / 256, 8192)); }
 
 }  // namespace mvae
@@ -182,6 +281,50 @@ int mvae_recon_bwd(int kind, const float* a, const float* b, const float* gscale
   if ((kind != 1 && kind != 2) || n <= 0) { set_error("recon_bwd: bad args"); return MVAE_EINVAL; }
   hipLaunchKernelGGL(recon_bwd_kernel, dim3(egrid(n)), dim3(256), 0, (hipStream_t)stream, kind, a, b, gscale, mult, da,
                      n);
+  return launch_status();
+}
+
+int mvae_latent_prep_fwd(const float* h_mu, const float* h_logvar, long long ld, const float* eps, float* mu,
+                         float* logvar, float* std_out, float* z, long long npix, int zc, void* stream) {
+  if (npix <= 0 || zc <= 0 || ld < zc || !h_mu || !h_logvar || !eps || !mu || !logvar || !std_out || !z) {
+    set_error("latent_prep_fwd: bad args");
+    return MVAE_EINVAL;
+  }
+  hipLaunchKernelGGL(latent_prep_fwd_kernel, dim3(egrid(npix * zc)), dim3(256), 0, (hipStream_t)stream, h_mu, h_logvar,
+                     ld, eps, mu, logvar, std_out, z, npix, zc);
+  return launch_status();
+}
+
+int mvae_latent_prep_bwd(const float* h_mu, const float* h_logvar, long long ld, const float* eps, const float* g_mu,
+                         const float* g_logvar, const float* g_std, const float* g_z, float* d_mu, float* d_logvar,
+                         long long ld_out, long long npix, int zc, void* stream) {
+  if (npix <= 0 || zc <= 0 || ld < zc || ld_out < zc || !h_mu || !h_logvar || !eps || !d_mu || !d_logvar) {
+    set_error("latent_prep_bwd: bad args");
+    return MVAE_EINVAL;
+  }
+  hipLaunchKernelGGL(latent_prep_bwd_kernel, dim3(egrid(npix * zc)), dim3(256), 0, (hipStream_t)stream, h_mu, h_logvar,
+                     ld, eps, g_mu, g_logvar, g_std, g_z, d_mu, d_logvar, ld_out, npix, zc);
+  return launch_status();
+}
+
+int mvae_loss_combine4_fwd(const float* v0, const float* v1, const float* v2, const float* v3, float w0, float w1,
+                           float w2, float w3, int nt, float nonfinite_total, float* total, float* o0, float* o1,
+                           float* o2, float* o3, float* flags, void* stream) {
+  CombineArgs a{{v0, v1, v2, v3}, {w0, w1, w2, w3}, {total, o0, o1, o2, o3}};
+  if (nt < 1 || nt > 4 || !total || !flags) { set_error("loss_combine4_fwd: bad args"); return MVAE_EINVAL; }
+  for (int i = 0; i < nt; ++i)
+    if (!a.v[i] || !a.o[1 + i]) { set_error("loss_combine4_fwd: null term"); return MVAE_EINVAL; }
+  hipLaunchKernelGGL(loss_combine_fwd_entry, dim3(1), dim3(64), 0, (hipStream_t)stream, a, nt, nonfinite_total, flags);
+  return launch_status();
+}
+
+int mvae_loss_combine4_bwd(const float* flags, float w0, float w1, float w2, float w3, int nt, const float* g_total,
+                           const float* g0, const float* g1, const float* g2, const float* g3, float* g_terms,
+                           void* stream) {
+  CombineArgs a{{g0, g1, g2, g3}, {w0, w1, w2, w3}, {}};
+  if (nt < 1 || nt > 4 || !flags || !g_terms) { set_error("loss_combine4_bwd: bad args"); return MVAE_EINVAL; }
+  hipLaunchKernelGGL(loss_combine_bwd_entry, dim3(1), dim3(64), 0, (hipStream_t)stream, a, nt, flags, g_total,
+                     g_terms);
   return launch_status();
 }
 

@@ -28,6 +28,8 @@ from .vae import BaseVAE, _posterior, _prior
 
 # batched per-sample routing kernels (csrc/routing.hip); MVAE_NO_ROUTING=1 selects the grouped-conv form
 ROUTING_KERNELS = os.environ.get("MVAE_NO_ROUTING") is None
+# fused latent side of the forward (ops.latent_prep); MVAE_NO_LATENT_PREP=1 keeps the torch clamp / reparam chain
+LATENT_PREP = os.environ.get("MVAE_NO_LATENT_PREP") is None
 
 
 def _nan_to_zero(t):
@@ -110,11 +112,16 @@ class DisentangledConditionalVAE(BaseVAE):
                 all(c in (1, mx) for c in self.modality_channels.values()) and
                 ops.routing_fits(t.shape[2], t.shape[3], mx, len(self.modality_decoders)))
 
+    def _encode_routed_raw(self, x: torch.Tensor, modality_indices: torch.Tensor) -> torch.Tensor:
+        """The encoder output [B, 2 z, r, r] of the routed batch before the chunk / NaN scrub (routing-kernel path)."""
+        mx = max(self.modality_channels.values())
+        routed = ops.modality_route_in(x, modality_indices, mx, len(self.modality_channels), self._route_in_params())
+        return self.encoder(ops.nhwc(routed))
+
     def encode(self, x: torch.Tensor, modality_indices: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         mx = max(self.modality_channels.values())
         if self._routing_kernel_ok(x):  # one launch: each sample through its own input projector (csrc/routing.hip)
-            routed = ops.modality_route_in(x, modality_indices, mx, len(self.modality_channels), self._route_in_params())
-            mu, logvar = BaseVAE.encode(self, routed)
+            mu, logvar = torch.chunk(self._encode_routed_raw(x, modality_indices), 2, dim=1)
             return _nan_to_zero(mu), _nan_to_zero(logvar)
         x = _nan_to_zero(x)
         idx = self._clamp(modality_indices.to(x.device).long(), len(self.modality_channels))
@@ -224,10 +231,20 @@ class DisentangledConditionalVAE(BaseVAE):
         return torch.where(n > 0, loss, torch.zeros_like(loss))
 
     def forward(self, x: torch.Tensor, modality_indices: torch.Tensor, return_latents: bool = False, *, eps=None):
-        mu, logvar = self.encode(x, modality_indices)
-        logvar = torch.clamp(logvar, min=-10.0, max=10.0)
-        mu = torch.clamp(mu, min=-10.0, max=10.0)
-        z = self.reparameterize(mu, logvar, eps=eps)
+        std = None
+        if LATENT_PREP and self._routing_kernel_ok(x):
+            # NaN scrub + clamps + reparameterization + posterior std: one launch per direction (csrc/loss.hip)
+            h = self._encode_routed_raw(x, modality_indices)
+            zc = h.shape[1] // 2
+            if eps is None:
+                eps = torch.randn((h.shape[0], zc) + tuple(h.shape[2:]), device=h.device,
+                                  dtype=torch.float32).contiguous(memory_format=torch.channels_last)
+            mu, logvar, std, z = ops.latent_prep(h, zc, eps)
+        else:
+            mu, logvar = self.encode(x, modality_indices)
+            logvar = torch.clamp(logvar, min=-10.0, max=10.0)
+            mu = torch.clamp(mu, min=-10.0, max=10.0)
+            z = self.reparameterize(mu, logvar, eps=eps)
         hint = 1 if x.shape[1] == 1 else max(self.modality_channels.values())
         rec = self._decode_routed(z, modality_indices, hint)
         # gated terms: a NaN/Inf value drops the term's gradient (DisentangledVAELoss replaces it by 0, :540-550)
@@ -236,7 +253,8 @@ class DisentangledConditionalVAE(BaseVAE):
         else:
             sep = ops.finite_gated(lambda zz: self.modality_separation_loss(zz, modality_indices), z)
             con = ops.finite_gated(lambda zz: self.contrastive_loss(zz, modality_indices), z)
-        std = torch.clamp(torch.exp(0.5 * logvar), min=1e-6, max=10.0)
+        if std is None:
+            std = torch.clamp(torch.exp(0.5 * logvar), min=1e-6, max=10.0)
         out = {"reconstruction": rec, "mean": mu, "logvar": logvar, "mu": mu, "z": z,
                "prior": _prior(mu, std), "posterior": _posterior(mu, logvar, std),
                "separation_loss": sep, "contrastive_loss": con}

@@ -150,7 +150,8 @@ class VAELightningModule(_Base):
             loss_dict = self.criterion(inputs=x, reconstructions=outputs["reconstruction"],
                                        posteriors=outputs["posterior"], priors=outputs["prior"])
         loss = loss_dict["loss"]
-        loss = torch.where(torch.isfinite(loss), loss, 1e6)
+        if not isinstance(self.criterion, DisentangledVAELoss):  # (that total is already guarded by the criterion)
+            loss = torch.where(torch.isfinite(loss), loss, 1e6)
         for k, v in loss_dict.items():
             self.log(f"train/{k}", v, prog_bar=True, logger=True, on_step=True, on_epoch=True)
         self._last_outputs = outputs

@@ -7,6 +7,7 @@ torch.distributions (not on the hot path).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict
 
 import torch
@@ -15,6 +16,10 @@ import torch.nn.functional as F
 from torch.distributions import Normal, kl_divergence
 
 from . import ops
+
+# DisentangledVAELoss's term guards + weighted total as one fused launch (ops.loss_combine); MVAE_NO_FUSED_COMBINE=1
+# keeps the torch where / isfinite chain
+FUSED_COMBINE = os.environ.get("MVAE_NO_FUSED_COMBINE") is None
 
 
 def _recon(kind: str, rec: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
@@ -64,11 +69,17 @@ class DisentangledVAELoss(nn.Module):
 
     def forward(self, outputs: Dict[str, torch.Tensor], targets: torch.Tensor) -> Dict[str, torch.Tensor]:
         kind, n = self.recon_loss_type, targets.numel()
-        recon = _finite_or_zero(ops.finite_gated(lambda r, t: _recon(kind, r, t), outputs["reconstruction"], targets))
-        kl = _finite_or_zero(ops.finite_gated(lambda m, lv: ops.kl_closed_form_sum(m, lv, n), outputs["mu"],
-                                              outputs["logvar"]))
-        sep = _finite_or_zero(outputs["separation_loss"])
-        con = _finite_or_zero(outputs["contrastive_loss"])
+        recon = ops.finite_gated(lambda r, t: _recon(kind, r, t), outputs["reconstruction"], targets)
+        kl = ops.finite_gated(lambda m, lv: ops.kl_closed_form_sum(m, lv, n), outputs["mu"], outputs["logvar"])
+        sep, con = outputs["separation_loss"], outputs["contrastive_loss"]
+        if FUSED_COMBINE and recon.is_cuda:  # finite-or-zero terms + weighted total + its guard: one launch each way
+            total, recon, kl, sep, con = ops.loss_combine(
+                [recon, kl, sep, con],
+                [self.recon_weight, self.kl_weight, self.separation_weight, self.contrastive_weight])
+            return {"loss": total, "recon_loss": recon, "kl_loss": kl, "separation_loss": sep,
+                    "contrastive_loss": con}
+        recon, kl = _finite_or_zero(recon), _finite_or_zero(kl)
+        sep, con = _finite_or_zero(sep), _finite_or_zero(con)
         total = (self.recon_weight * recon + self.kl_weight * kl + self.separation_weight * sep +
                  self.contrastive_weight * con)
         total = torch.where(torch.isfinite(total), total, 1e6)

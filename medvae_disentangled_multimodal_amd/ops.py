@@ -1049,6 +1049,85 @@ def reparameterize(mean, logvar, eps):
     return ReparamFn.apply(mean, logvar, eps)
 
 
+class LatentPrepFn(torch.autograd.Function):
+    """The disentangled model's latent side in one launch per direction (mvae_latent_prep_fwd / _bwd): encode's NaN
+    scrub + forward's clamps of mu / logvar (disentangled_conditional_vae.py:388-398), the reparameterization
+    (base_vae.py:83-87) and the posterior's clamped std. h = the encoder output [n, 2 zc, hh, ww] (mean channels
+    first, torch.chunk); the backward writes h's gradient directly (no chunk / accumulation launches)."""
+
+    @staticmethod
+    def forward(ctx, h, eps, zc: int):
+        _check(h, "encoder output")
+        if h.dim() != 4 or h.shape[1] != 2 * zc:
+            raise RuntimeError(f"latent_prep: expected an encoder output [n, {2 * zc}, h, w], got {tuple(h.shape)}")
+        h, ld = _pix(h)
+        eps = nhwc(eps)
+        n, _, hh, ww = h.shape
+        outs = [torch.empty((n, zc, hh, ww), device=h.device, dtype=torch.float32, memory_format=CL) for _ in range(4)]
+        mu, lv, sd, z = outs
+        _lib.call("mvae_latent_prep_fwd", h.data_ptr(), h.data_ptr() + 4 * zc, ld, eps.data_ptr(), mu.data_ptr(),
+                  lv.data_ptr(), sd.data_ptr(), z.data_ptr(), n * hh * ww, zc, _stream(h))
+        ctx.save_for_backward(h, eps)
+        ctx.ld, ctx.zc = ld, zc
+        return mu, lv, sd, z
+
+    @staticmethod
+    def backward(ctx, gmu, glv, gsd, gz):
+        h, eps = ctx.saved_tensors
+        zc, ld = ctx.zc, ctx.ld
+        n, c2, hh, ww = h.shape
+        dh = torch.empty((n, c2, hh, ww), device=h.device, dtype=torch.float32, memory_format=CL)  # fully written
+        gs = [None if g is None else nhwc(g.float()) for g in (gmu, glv, gsd, gz)]
+        _lib.call("mvae_latent_prep_bwd", h.data_ptr(), h.data_ptr() + 4 * zc, ld, eps.data_ptr(),
+                  *[_ptr(g) for g in gs], dh.data_ptr(), dh.data_ptr() + 4 * zc, c2, n * hh * ww, zc, _stream(h))
+        return dh, None, None
+
+
+def latent_prep(h, zc: int, eps):
+    """(mu, logvar, std, z) of the disentangled forward from the encoder output h (see LatentPrepFn)."""
+    return LatentPrepFn.apply(h, eps, int(zc))
+
+
+class LossCombineFn(torch.autograd.Function):
+    """DisentangledVAELoss's combination of its scalar terms (disentangled_conditional_vae.py:528-570) in one launch
+    per direction: each term replaced by 0 when non-finite, the weighted sum in order, the total replaced by
+    `nonfinite_total` when non-finite (mvae_loss_combine4_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, weights, nonfinite_total, *terms):
+        nt = len(terms)
+        dev = terms[0].device
+        outs = [torch.empty((), device=dev, dtype=torch.float32) for _ in range(nt + 1)]  # total, terms
+        flags = torch.empty(nt + 1, device=dev, dtype=torch.float32)
+        tp = [t.detach().float().contiguous() for t in terms]
+        ptrs = [t.data_ptr() for t in tp] + [None] * (4 - nt)
+        optr = [o.data_ptr() for o in outs] + [None] * (4 - nt)
+        w = list(map(float, weights)) + [0.0] * (4 - nt)
+        _lib.call("mvae_loss_combine4_fwd", *ptrs, *w, nt, float(nonfinite_total), *optr, flags.data_ptr(),
+                  _stream(terms[0]))
+        ctx.w, ctx.nt, ctx.flags = w, nt, flags
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, gtot, *gterms):
+        nt = ctx.nt
+        dev = ctx.flags.device
+        gt = None if gtot is None else gtot.float().contiguous()
+        gs = [None if g is None else g.float().contiguous() for g in gterms] + [None] * (4 - nt)
+        out = torch.empty(nt, device=dev, dtype=torch.float32)
+        _lib.call("mvae_loss_combine4_bwd", ctx.flags.data_ptr(), *ctx.w, nt, _ptr(gt), *[_ptr(g) for g in gs],
+                  out.data_ptr(), _stream(out))
+        ctx.flags = None
+        return (None, None, *[out[i] for i in range(nt)])
+
+
+def loss_combine(terms, weights, nonfinite_total: float = 1e6):
+    """(total, *finite_or_zero(terms)) of DisentangledVAELoss (see LossCombineFn); up to 4 0-d device terms."""
+    if not 1 <= len(terms) <= 4 or len(weights) != len(terms):
+        raise ValueError("loss_combine: 1-4 terms with one weight each")
+    return LossCombineFn.apply(tuple(weights), float(nonfinite_total), *terms)
+
+
 class KLFn(torch.autograd.Function):
     """kind 0: mean over elements of KL(N(mu, e^{lv/2}) || N(0,1));
     kind 3: -0.5*sum(1+lv-mu^2-e^lv) / denom (DisentangledVAELoss)."""
@@ -1131,7 +1210,8 @@ class _FiniteGateFn(torch.autograd.Function):
             req = [t.detach().requires_grad_(bool(n)) if torch.is_tensor(t) else t for t, n in zip(inputs, need)]
             v = fn(*req)
         ctx.v, ctx.req = v, req
-        ctx.ok = torch.isfinite(v.detach()).all()
+        ok = torch.isfinite(v.detach())
+        ctx.ok = ok.all() if ok.dim() else ok  # (a 0-d term needs no reduction launch)
         return v.detach()
 
     @staticmethod
