@@ -172,6 +172,16 @@ int mvae_split_planar_colsum(const float* x, void* y, long long rows, int n, flo
 /* Weight re-layouts for the input gradient: KRSC -> [cin][kh][kw][cout]; and the 4x4 tap-summed
  * kernel [cin][4][4][cout] for Upsample's conv (encoder_decoder.py:205-209). */
 int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int kw, int cin, int split, void* stream);
+/* All of a step's dgrad weight re-layouts in one launch: `table` (device memory) holds n descriptors sorted by
+ * block0, each one mvae_conv_weight_transpose (w [cout][rs][cin] -> wt [cin][rs][cout] in format `split`) over
+ * ceil(cin/64) * ceil(cout/64) * rs workgroups starting at block0; total_blocks = the sum. */
+typedef struct {
+  const float* w;
+  float* wt;
+  int cout, rs, cin, split;
+  int block0, pad0;
+} mvae_wt_desc;
+int mvae_conv_weight_transpose_batched(const mvae_wt_desc* table, int n, int total_blocks, void* stream);
 int mvae_conv_weight_upsample_dgrad(const float* w, float* wt, int cout, int cin, int split, void* stream);
 
 /* Bias gradient: out[n] = beta*out[n] + sum_rows x[row*ld + n] (conv bias, encoder_decoder.py:123-146). */

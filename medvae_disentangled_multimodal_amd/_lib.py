@@ -38,6 +38,7 @@ SIGNATURES = {
     "mvae_conv2d_wgrad_direct_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, I, P, Z, P]),
     "mvae_conv2d_wgrad_direct_workspace_bytes": (Z, [I, I, I, I, I]),
     "mvae_conv_weight_transpose": (I, [P, P, I, I, I, I, I, P]),
+    "mvae_conv_weight_transpose_batched": (I, [P, I, I, P]),
     "mvae_conv_weight_upsample_dgrad": (I, [P, P, I, I, I, P]),
     "mvae_conv2d_dgrad_stride2_nhwc": (I, [P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),
     "mvae_split_bf16": (I, [P, P, L, P]),

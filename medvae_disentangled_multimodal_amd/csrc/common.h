@@ -11,6 +11,15 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 #define MVAE_WAVE 64
 
+// descriptor of mvae_conv_weight_transpose_batched (same layout as include/medvae_hip.h)
+typedef struct {
+  const float* w;
+  float* wt;
+  int cout, rs, cin, split;
+  int block0, pad0;
+} mvae_wt_desc;
+static_assert(sizeof(mvae_wt_desc) == 40, "mvae_wt_desc layout");
+
 namespace mvae {
 
 // Error reporting across the C ABI: every entry point returns 0 on success, a negative code for

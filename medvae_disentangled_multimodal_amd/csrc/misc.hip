@@ -82,6 +82,35 @@ __global__ void __launch_bounds__(256) w_transpose_kernel(const float* __restric
   write_transposed(tile, wt, c0, o0, t, rs, cin, cout, split);
 }
 
+// Every dgrad weight re-layout of a training step in one launch (mvae_conv_weight_transpose_batched): a 1-D grid over
+// the concatenated (cin/64, cout/64, tap) tiles of all descriptors; each workgroup finds its descriptor by binary
+// search over the block offsets (wave-uniform loads) and runs w_transpose_kernel's body.
+__global__ void __launch_bounds__(256) w_transpose_batched_kernel(const mvae_wt_desc* __restrict__ d, int nd) {
+  __shared__ float tile[64][65];
+  const int blk = blockIdx.x;
+  int lo = 0, hi = nd - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].block0 <= blk) lo = mid; else hi = mid - 1;
+  }
+  const float* __restrict__ w = d[lo].w;
+  float* __restrict__ wt = d[lo].wt;
+  const int cout = d[lo].cout, rs = d[lo].rs, cin = d[lo].cin, split = d[lo].split;
+  const int bx = (cin + 63) / 64, by = (cout + 63) / 64;
+  int b = blk - d[lo].block0;
+  const int cx = b % bx;
+  b /= bx;
+  const int c0 = cx * 64, o0 = (b % by) * 64, t = b / by;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int o = o0 + ty + 4 * i, c = c0 + tx;
+    tile[ty + 4 * i][tx] = (o < cout && c < cin) ? w[((long long)o * rs + t) * cin + c] : 0.f;
+  }
+  __syncthreads();
+  write_transposed(tile, wt, c0, o0, t, rs, cin, cout, split);
+}
+
 __device__ __forceinline__ int tap_mask(int t) {
   // bit r set when source tap r contributes to effective tap t
   return t == 0 ? 0b100 : t == 1 ? 0b110 : t == 2 ? 0b011 : 0b001;
@@ -282,6 +311,12 @@ int mvae_conv_weight_transpose(const float* w, float* wt, int cout, int kh, int 
   }
   hipLaunchKernelGGL(w_transpose_kernel, dim3((cin + 63) / 64, (cout + 63) / 64, kh * kw), dim3(256), 0,
                      (hipStream_t)stream, w, wt, cout, kh * kw, cin, split);
+  return launch_status();
+}
+
+int mvae_conv_weight_transpose_batched(const mvae_wt_desc* table, int n, int total_blocks, void* stream) {
+  if (n <= 0 || !table || total_blocks <= 0) { set_error("w_transpose_batched: bad args"); return MVAE_EINVAL; }
+  hipLaunchKernelGGL(w_transpose_batched_kernel, dim3(total_blocks), dim3(256), 0, (hipStream_t)stream, table, n);
   return launch_status();
 }
 

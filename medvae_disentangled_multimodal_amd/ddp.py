@@ -79,7 +79,7 @@ class DataParallel:
         members, lo, hi = [], None, None
         for i in reversed(range(len(flat.params))):
             p, off = flat.params[i], flat.offsets[i]
-            end = off + (p.numel() + 3) // 4 * 4
+            end = off + (p.numel() + 3) // 4 * 4 if i < len(flat.params) - 1 else flat.numel  # (+ the tail padding)
             members.append(i)
             lo = off
             hi = end if hi is None else hi

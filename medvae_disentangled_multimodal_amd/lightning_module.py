@@ -301,6 +301,7 @@ class VAELightningModule(_Base):
         static = [t.clone() for t in ins]
         salt = ops.dropout_salt(dev)
         self._last_outputs = None  # no autograd graph of an earlier step may outlive into the capture
+        ops.refresh_weight_tables(self.flat.data)  # (the batched weight re-layout table is uploaded outside the capture)
         torch.cuda.synchronize(dev)
         self._graph = None  # release an outdated graph (and the arena buffers it pinned) before recording
         graph = torch.cuda.CUDAGraph()

@@ -264,6 +264,98 @@ class _FlatWeights:
 
 
 _FLATW = _FlatWeights()
+_FLATW = _FlatWeights()
+
+
+class _TransposedWeights:
+    """Every dgrad weight re-layout of a step in one launch (mvae_conv_weight_transpose_batched). The (weight, shape,
+    format) triples the input-gradient GEMMs ask for are learned on a step that runs them one launch per conv; the
+    descriptor table is then uploaded once, and from the next step on fit_step's weight prep (prep_flat_weights)
+    re-lays out all of them before the forward, each dgrad reading its slot (~30 launches fewer per c3 step). Valid
+    until the optimizer step, like _FlatWeights. Only weights inside the flat parameter buffer are tabled (stable
+    addresses); the buffers of replaced tables stay alive (a captured step graph may have baked them in)."""
+    __slots__ = ("slots", "want", "table", "buf", "n", "blocks", "fresh", "keep", "base", "end", "tbase", "tend")
+
+    def __init__(self):
+        self.slots, self.want = {}, {}
+        self.table = self.buf = None
+        self.n = self.blocks = 0
+        self.fresh = False
+        self.keep = []
+        self.base = self.end = self.tbase = self.tend = 0
+
+
+_WT = _TransposedWeights()
+BATCHED_WT = os.environ.get("MVAE_NO_BATCHED_WT") is None
+
+
+def _wt_blocks(co, rs, c):
+    return ((c + 63) // 64) * ((co + 63) // 64) * rs
+
+
+def refresh_weight_tables(flat_data: torch.Tensor):
+    """Build / extend the batched dgrad re-layout table from what earlier steps asked for (host work + one upload);
+    called by prep_flat_weights and, before a step graph is captured, by the trainer (no upload inside a capture)."""
+    n = flat_data.numel()
+    _WT.base, _WT.end = flat_data.data_ptr(), flat_data.data_ptr() + 4 * n
+    if BATCHED_WT:
+        _wt_rebuild(flat_data.device)
+
+
+def _wt_rebuild(dev):
+    if (_WT.tbase, _WT.tend) != (_WT.base, _WT.end):  # a new flat buffer: the table's weight addresses are gone
+        if _WT.table is not None:
+            _WT.keep.append((_WT.table, _WT.buf))
+        _WT.slots, _WT.table, _WT.buf, _WT.n = {}, None, None, 0
+        _WT.want = {k: v for k, v in _WT.want.items() if _WT.base <= k[0] < _WT.end}
+        _WT.tbase, _WT.tend = _WT.base, _WT.end
+    if any(k not in _WT.slots for k in _WT.want):
+        import numpy as np
+        keys = list(_WT.slots) + [k for k in _WT.want if k not in _WT.slots]
+        info = {**{k: _WT.want.get(k) for k in _WT.slots}, **_WT.want}
+        offs, o = {}, 0
+        for k in keys:
+            offs[k] = o
+            o += (info[k][5] + 255) // 256 * 256
+        buf = torch.empty(o, dtype=torch.uint8, device=dev)
+        dt = np.dtype([("w", "<u8"), ("wt", "<u8"), ("cout", "<i4"), ("rs", "<i4"), ("cin", "<i4"), ("split", "<i4"),
+                       ("block0", "<i4"), ("pad0", "<i4")])
+        arr = np.zeros(len(keys), dtype=dt)
+        b0 = 0
+        for i, k in enumerate(keys):
+            wp, co, rs, c, split, _ = info[k]
+            arr[i] = (wp, buf.data_ptr() + offs[k], co, rs, c, split, b0, 0)
+            b0 += _wt_blocks(co, rs, c)
+        table = torch.from_numpy(arr.view(np.uint8).copy()).to(dev)
+        if _WT.table is not None:
+            _WT.keep.append((_WT.table, _WT.buf))
+        _WT.slots, _WT.table, _WT.buf, _WT.n, _WT.blocks = offs, table, buf, len(keys), b0
+        _WT.want = dict(info)
+
+
+def _prep_transposed(dev, st):
+    _WT.fresh = False
+    if not BATCHED_WT:
+        return
+    if not torch.cuda.is_current_stream_capturing():
+        _wt_rebuild(dev)
+    if _WT.n and (_WT.tbase, _WT.tend) == (_WT.base, _WT.end):
+        _lib.call("mvae_conv_weight_transpose_batched", _WT.table.data_ptr(), _WT.n, _WT.blocks, st)
+        _WT.fresh = True
+
+
+def _weight_t(w, co, kh, kw, c, split, nbytes, st) -> int:
+    """Device pointer of w re-laid out [cin][taps][cout] in format `split` (mvae_conv_weight_transpose): the slot the
+    step's batched prep wrote, or a per-conv launch into arena scratch (recorded for the next table)."""
+    p = w.data_ptr()
+    key = (p, co, kh, kw, c, int(split))
+    if _WT.fresh and key in _WT.slots:
+        return _WT.buf.data_ptr() + _WT.slots[key]
+    wt = ARENA.get("wt", nbytes, w.device)
+    _lib.call("mvae_conv_weight_transpose", p, wt.data_ptr(), co, kh, kw, c, int(split), st)
+    if BATCHED_WT and _WT.base <= p < _WT.end and w.is_contiguous(memory_format=CL):
+        _WT.want[key] = (p, co, kh * kw, c, int(split), nbytes)
+    return wt.data_ptr()
 
 
 def prep_flat_weights(flat_data: torch.Tensor):
@@ -272,6 +364,8 @@ def prep_flat_weights(flat_data: torch.Tensor):
     fmt = 2 if _dma_fmt() == 2 else (1 if _MATH[0] == 0 and WEIGHT_SPLIT and _dma_fmt() == 0 else 0)
     _FLATW.fresh = False
     n = flat_data.numel()
+    _WT.base, _WT.end = flat_data.data_ptr(), flat_data.data_ptr() + 4 * n
+    _prep_transposed(flat_data.device, _stream(flat_data))
     if fmt == 0 or n % 8 or not _al16(flat_data):
         return
     nbytes = n * (4 if fmt == 1 else 2)
@@ -284,6 +378,7 @@ def prep_flat_weights(flat_data: torch.Tensor):
 
 def flat_weights_stale():
     _FLATW.fresh = False
+    _WT.fresh = False
 
 
 def _flat_weight_ptr(w: torch.Tensor, fmt: int) -> Optional[int]:
@@ -484,13 +579,12 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
     if gn_link is not None and gn_link.usable(dx) and not g.pointwise and not g.upsample and g.stride == 1 and \
             co % 4 == 0 and _al16(dy, dx):
         split = WEIGHT_SPLIT and _splits_ok()
-        wt = ARENA.get("wt", c * g.kh * g.kw * co * 4, dy.device)
-        _lib.call("mvae_conv_weight_transpose", w.data_ptr(), wt.data_ptr(), co, g.kh, g.kw, c, int(split), st)
+        wtp = _weight_t(w, co, g.kh, g.kw, c, int(split), c * g.kh * g.kw * co * 4, st)
         part = torch.empty(n * h * wd // 32 * c * 2, device=dy.device, dtype=torch.float64)
         L = gn_link
         flags = int(split) | (2 if dys is not None else 0)
         with _timed("conv_dgrad", flops, shp):
-            _lib.call("mvae_conv2d_dgrad_gnbwd_nhwc", dya.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, ho, wo, co, c,
+            _lib.call("mvae_conv2d_dgrad_gnbwd_nhwc", dya.data_ptr(), wtp, dx.data_ptr(), n, ho, wo, co, c,
                       g.kh, g.kw, g.pad_t, g.pad_l, h, wd, flags, L.x.data_ptr(), L.mean.data_ptr(),
                       L.rstd.data_ptr(), L.gamma.data_ptr(), L.beta.data_ptr(), L.groups, L.silu, part.data_ptr(), st)
         L.part, L.dx = part, dx
@@ -513,18 +607,17 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
             _lib.call("mvae_conv2d_nhwc", dya.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
                       4, 4, 2, 1, 1, h, wd, wflag | xflag, st)
         return dx
-    wt = ARENA.get("wt", c * g.kh * g.kw * co * 4, dy.device)
-    _lib.call("mvae_conv_weight_transpose", w.data_ptr(), wt.data_ptr(), co, g.kh, g.kw, c, int(split), st)
+    wtp = _weight_t(w, co, g.kh, g.kw, c, int(split), c * g.kh * g.kw * co * 4, st)
     if g.stride == 2 and h % 2 == 0 and wd % 2 == 0 and g.kh <= 4 and g.kw <= 4 and STRIDE2_CLASSES:
         # Downsample's input gradient by dx parity class: only the useful taps (no stride holes)
         wc = ARENA.get("wcls", c * g.kh * g.kw * co * 4, dy.device)
         flags = int(split) | (2 if dys is not None else 0)
         with _timed("conv_dgrad", flops, shp):
-            _lib.call("mvae_conv2d_dgrad_stride2_nhwc", dya.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, h, wd, c, co,
+            _lib.call("mvae_conv2d_dgrad_stride2_nhwc", dya.data_ptr(), wtp, dx.data_ptr(), n, h, wd, c, co,
                       g.kh, g.kw, g.pad_t, g.pad_l, ho, wo, flags, wc.data_ptr(), wc.numel(), st)
         return dx
     with _timed("conv_dgrad", flops, shp):
-        _conv_call(dya.data_ptr(), wt.data_ptr(), None, None, dx, n, ho, wo, co, c, g.kh, g.kw, g.stride, g.pad_t,
+        _conv_call(dya.data_ptr(), wtp, None, None, dx, n, ho, wo, co, c, g.kh, g.kw, g.stride, g.pad_t,
                    g.pad_l, h, wd, 2 | wflag | xflag, st)
     return dx
 
@@ -541,16 +634,15 @@ def _conv_dgrad_bf16(dyb, w, dx, g, n, c, h, wd, co, ho, wo, flops, shp, st):
             _lib.call("mvae_conv2d_nhwc", dyb.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
                       4, 4, 2, 1, 1, h, wd, flag, st)
         return dx
-    wt = ARENA.get("wt", _dma_bytes(c * g.kh * g.kw * co), dev)
-    _lib.call("mvae_conv_weight_transpose", w.data_ptr(), wt.data_ptr(), co, g.kh, g.kw, c, fmt, st)
+    wtp = _weight_t(w, co, g.kh, g.kw, c, fmt, _dma_bytes(c * g.kh * g.kw * co), st)
     if g.stride == 2 and h % 2 == 0 and wd % 2 == 0 and g.kh <= 4 and g.kw <= 4 and STRIDE2_CLASSES:
         wc = ARENA.get("wcls", c * g.kh * g.kw * co * 4, dev)
         with _timed("conv_dgrad", flops, shp):
-            _lib.call("mvae_conv2d_dgrad_stride2_nhwc", dyb.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, h, wd, c, co,
+            _lib.call("mvae_conv2d_dgrad_stride2_nhwc", dyb.data_ptr(), wtp, dx.data_ptr(), n, h, wd, c, co,
                       g.kh, g.kw, g.pad_t, g.pad_l, ho, wo, 8 if fmt == 3 else 4, wc.data_ptr(), wc.numel(), st)
         return dx
     with _timed("conv_dgrad", flops, shp):
-        _conv_call(dyb.data_ptr(), wt.data_ptr(), None, None, dx, n, ho, wo, co, c, g.kh, g.kw, g.stride, g.pad_t,
+        _conv_call(dyb.data_ptr(), wtp, None, None, dx, n, ho, wo, co, c, g.kh, g.kw, g.stride, g.pad_t,
                    g.pad_l, h, wd, 2 | flag, st)
     return dx
 

@@ -45,6 +45,9 @@ class FlatParameters:
             offs.append(o)
             o += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
         self.offsets = offs
+        # whole 8-element groups: the one-launch weight conversions of a step (ops.prep_flat_weights: split4 / packed
+        # bf16) take the buffer in 16-B output groups of 8 fp32 elements; the padding stays zero
+        o = (o + 7) // 8 * 8
         self.numel = o
         self.data = torch.zeros(o, device=self.device, dtype=torch.float32)
         self.grad = torch.zeros(o, device=self.device, dtype=torch.float32)

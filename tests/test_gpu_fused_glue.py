@@ -150,3 +150,51 @@ def test_loss_combine_total_only_backward():
     tot = ops.loss_combine(ts, [1.0, 6.0, 0.1, 0.05])[0]
     tot.backward()
     assert [float(t.grad) for t in ts] == pytest.approx([1.0, 6.0, 0.1, 0.05], rel=1e-7)
+
+
+# ---- batched dgrad weight re-layouts (ops._TransposedWeights, mvae_conv_weight_transpose_batched) -------------------
+_CVAE = dict(input_channels=3, latent_dim=8, hidden_channels=32, ch_mult=(1, 2, 4), num_res_blocks=1,
+             attn_resolutions=[14], dropout=0.0, resolution=28, condition_method="concat")
+_DIS = dict(num_modalities=5, shared_latent_dim=8, modality_latent_dim=8, hidden_channels=32, ch_mult=(1, 2, 4),
+            num_res_blocks=1, attn_resolutions=[], dropout=0.0, resolution=28, modality_separation_weight=0.1,
+            contrastive_weight=0.05)
+
+
+@pytest.mark.parametrize("cls,kw,loss,prec", [
+    ("ConditionalVAE", _CVAE, dict(type="vae", recon_loss_type="mse", kl_weight=1.0, recon_weight=1.0), "32"),
+    ("ConditionalVAE", _CVAE, dict(type="vae", recon_loss_type="mse", kl_weight=1.0, recon_weight=1.0), "bf16-mixed"),
+    ("DisentangledConditionalVAE", _DIS, dict(type="disentangled_vae", recon_loss_type="mse", kl_weight=1.0,
+                                              recon_weight=1.0, separation_weight=0.1, contrastive_weight=0.05), "32")])
+def test_batched_weight_relayout_matches_per_conv(monkeypatch, cls, kw, loss, prec):
+    """Steps whose dgrads read the step's one-launch weight re-layouts = steps with one re-layout launch per conv,
+    bit for bit (same kernel body, same formats); the table covers the model's dgrad convs after the first step."""
+    import medvae_disentangled_multimodal_amd as M
+    from medvae_disentangled_multimodal_amd import ops
+    dev = _dev()
+    B = 16
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randint(0, 256, (B, 3, 28, 28), generator=g).float() / 255 * 2 - 1).to(dev)
+    labels = torch.zeros(B, 1, dtype=torch.long, device=dev)
+    idx = torch.tensor([0, 1, 2, 3, 4, 1, 2, 4, 0, 3, 1, 2, 4, 4, 1, 2], device=dev)
+    if cls == "DisentangledConditionalVAE":
+        batch = (x, labels, torch.nn.functional.one_hot(idx, 12).float(), idx)
+    else:
+        batch = (x, labels, torch.nn.functional.one_hot(idx, 12).float())
+    r = 28 // 4
+    eps = [torch.randn(B, 16 if cls == "DisentangledConditionalVAE" else 8, r, r, generator=g).to(dev)
+           for _ in range(3)]
+    res = {}
+    for batched in (False, True):
+        monkeypatch.setattr(ops, "BATCHED_WT", batched)
+        torch.manual_seed(11)
+        model = getattr(M, cls)(**kw).to(dev)
+        mod = M.VAELightningModule(model, dict(type="adam", lr=5e-4, weight_decay=0.0, betas=[0.9, 0.999]),
+                                   {"type": "none"}, loss, gradient_clip_val=0.5, precision=prec)
+        mod.configure_optimizers()
+        losses = [mod.fit_step(batch, i, eps=eps[i]) for i in range(3)]
+        torch.cuda.synchronize()
+        res[batched] = (torch.stack(losses).cpu(), mod.flat.data.detach().cpu().clone())
+        if batched:
+            assert ops._WT.n > 0 and ops._WT.tbase == mod.flat.data.data_ptr()
+    assert torch.equal(res[True][0], res[False][0])
+    assert torch.equal(res[True][1], res[False][1])
