@@ -91,12 +91,13 @@ STRUCT_CEIL_TF = {"conv_fwd": 598.0, "conv_dgrad": 598.0, "conv_wgrad": 559.0, "
 HBM_MEASURED_GBS = {"read_only": 6262.0, "copy": 5314.0}
 
 
-def _pmc_traffic(config):
-    """HBM bytes per gemm3x_kernel launch from the committed PMC passes (tools/pmc_traffic.sh:
-    FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc, separate passes) -- counters cannot be read inside
-    this timed run, so the profile of the same command is attached (newest round first)."""
+def _pmc_traffic(config, family="gemm"):
+    """HBM bytes per launch of a kernel family (gemm: gemm3x_kernel; gn: the gn_* GroupNorm chains) from the
+    committed PMC passes (tools/pmc_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc, separate passes) --
+    counters cannot be read inside this timed run, so the profile of the same command is attached (newest round
+    first)."""
     for tag in ("r03", "r02", "r01"):
-        path = os.path.join(ROOT, "profiles", f"{tag}_{config}_gemm_traffic.json")
+        path = os.path.join(ROOT, "profiles", f"{tag}_{config}_{family}_traffic.json")
         if os.path.exists(path):
             break
     else:
@@ -106,6 +107,7 @@ def _pmc_traffic(config):
     return {"bytes_per_launch": round(t["traffic_bytes_per_launch"]), "unit": "B",
             "fetch_bytes_per_launch": round(t["fetch_bytes_per_launch"]),
             "write_bytes_per_launch": round(t["write_bytes_per_launch"]), "launches": t["launches"],
+            "total_bytes_per_step": round(t.get("traffic_bytes_total", 0.0) / t.get("steps", 1)),
             "source": os.path.relpath(path, ROOT)}
 
 
@@ -302,6 +304,12 @@ def _roofline(rec_all, bf16, config, step_ms, detail, rank):
                           "norm1); chains include the statistics finalize and parameter-gradient kernels",
             "by_pass": {k: {"launches": v[0], "ms": round(v[2], 2),
                             "GB/s": round(v[1] / (v[2] * 1e-3) / 1e9, 1)} for k, v in hb.items()}}
+        gpmc = _pmc_traffic(config, "gn")
+        if gpmc:  # moved vs algorithmic bytes of the whole family over one step
+            moved = gpmc["total_bytes_per_step"]
+            roofline["hbm_kernels"].update({
+                "traffic_bytes_per_step": moved, "algorithmic_bytes_per_step": round(hby),
+                "traffic_over_algorithmic": round(moved / max(hby, 1.0), 3), "traffic_detail": gpmc})
     return roofline
 
 

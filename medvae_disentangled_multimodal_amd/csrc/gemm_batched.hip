@@ -22,55 +22,28 @@ __global__ void splitk_reduce_kernel(GemmArgs a) {
   }
 }
 
-// Same reduction, 4 columns per thread (N, ldc, ldr multiples of 4; 16-B aligned C / residual / bias):
-// 2-D grid (column groups x output rows), so the row / batch index is block-uniform (no per-element
-// 64-bit division); the split partials are loaded 4 at a time and summed in split order (deterministic).
+// Same reduction, 4 columns per thread (splitk_reduce4_rows): 2-D grid (column groups x output rows), so the row /
+// batch index is block-uniform (no per-element 64-bit division).
 __global__ void __launch_bounds__(256) splitk_reduce4_kernel(GemmArgs a) {
-  const int c4 = blockIdx.x * 256 + threadIdx.x;
-  if (c4 >= (a.N >> 2)) return;
-  const int col = c4 * 4;
-  const long long mn = (long long)a.M * a.N;
-  const float4 zero{0.f, 0.f, 0.f, 0.f};
-  const float4 bv = a.bias ? *(const float4*)(a.bias + col) : zero;
-  for (int rb = blockIdx.y; rb < a.M * a.batch; rb += gridDim.y) {
-    const int bidx = rb / a.M, row = rb - bidx * a.M;
-    const float* w = a.ws + (long long)bidx * a.splits * mn + (long long)row * a.N + col;
-    float4 s = zero;
-    int z = 0;
-    for (; z + 4 <= a.splits; z += 4) {
-      const float4 w0 = *(const float4*)(w + z * mn), w1 = *(const float4*)(w + (z + 1) * mn);
-      const float4 w2 = *(const float4*)(w + (z + 2) * mn), w3 = *(const float4*)(w + (z + 3) * mn);
-      s.x = (((s.x + w0.x) + w1.x) + w2.x) + w3.x;
-      s.y = (((s.y + w0.y) + w1.y) + w2.y) + w3.y;
-      s.z = (((s.z + w0.z) + w1.z) + w2.z) + w3.z;
-      s.w = (((s.w + w0.w) + w1.w) + w2.w) + w3.w;
-    }
-    for (; z < a.splits; ++z) {
-      const float4 w0 = *(const float4*)(w + z * mn);
-      s.x += w0.x; s.y += w0.y; s.z += w0.z; s.w += w0.w;
-    }
-    float4 v{a.alpha * s.x + bv.x, a.alpha * s.y + bv.y, a.alpha * s.z + bv.z, a.alpha * s.w + bv.w};
-    if (a.res) {
-      const float4 r = *(const float4*)(a.res + bidx * a.sR + (long long)row * a.ldr + col);
-      v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
-    }
-    float* cp = a.C + bidx * a.sC + (long long)row * a.ldc + col;
-    if (a.beta != 0.f) {
-      const float4 c = *(const float4*)cp;
-      v.x += a.beta * c.x; v.y += a.beta * c.y; v.z += a.beta * c.z; v.w += a.beta * c.w;
-    }
-    *(float4*)cp = v;
-  }
+  splitk_reduce4_rows(a, blockIdx.x, blockIdx.y, gridDim.y);
+}
+
+bool splitk_vec_ok(const GemmArgs& a) {
+  return (a.N & 3) == 0 && (a.ldc & 3) == 0 && (a.sC & 3) == 0 && al16(a.C) &&
+         (!a.res || ((a.ldr & 3) == 0 && (a.sR & 3) == 0 && al16(a.res))) && (!a.bias || al16(a.bias)) &&
+         (long long)a.M * a.batch < (1LL << 31);
+}
+
+void splitk_vec_grid(const GemmArgs& a, int& gx, int& gy) {
+  gx = cdiv(a.N >> 2, 256);
+  gy = (int)std::min<long long>((long long)a.M * a.batch, std::max(1, 8192 / gx));
 }
 
 int gemm_finish(GemmArgs& a, hipStream_t st) {
   if (a.splits > 1) {
-    const bool vec = (a.N & 3) == 0 && (a.ldc & 3) == 0 && (a.sC & 3) == 0 && al16(a.C) &&
-                     (!a.res || ((a.ldr & 3) == 0 && (a.sR & 3) == 0 && al16(a.res))) && (!a.bias || al16(a.bias)) &&
-                     (long long)a.M * a.batch < (1LL << 31);
-    if (vec) {
-      const int gx = cdiv(a.N >> 2, 256);
-      const int gy = (int)std::min<long long>((long long)a.M * a.batch, std::max(1, 8192 / gx));
+    if (splitk_vec_ok(a)) {
+      int gx, gy;
+      splitk_vec_grid(a, gx, gy);
       hipLaunchKernelGGL(splitk_reduce4_kernel, dim3(gx, gy), dim3(256), 0, st, a);
     } else {
       const long long total = (long long)a.M * a.N * a.batch;

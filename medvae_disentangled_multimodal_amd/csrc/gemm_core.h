@@ -1704,6 +1704,47 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 
 // Fixed-order reduction of split-K partials + the same epilogue.
 __global__ void splitk_reduce_kernel(GemmArgs a);
+// Split-K reduction, 4 columns per thread (N, ldc, ldr multiples of 4; 16-B aligned C / residual / bias): column
+// group bx * 256 + thread, output rows y0, y0 + ystep, ...; the split partials are loaded 4 at a time and summed in
+// split order (deterministic). Body of splitk_reduce4_kernel and of the weight-gradient finish kernel.
+__device__ __forceinline__ void splitk_reduce4_rows(const GemmArgs& a, int bx, int y0, int ystep) {
+  const int c4 = bx * 256 + threadIdx.x;
+  if (c4 >= (a.N >> 2)) return;
+  const int col = c4 * 4;
+  const long long mn = (long long)a.M * a.N;
+  const float4 zero{0.f, 0.f, 0.f, 0.f};
+  const float4 bv = a.bias ? *(const float4*)(a.bias + col) : zero;
+  for (int rb = y0; rb < a.M * a.batch; rb += ystep) {
+    const int bidx = rb / a.M, row = rb - bidx * a.M;
+    const float* w = a.ws + (long long)bidx * a.splits * mn + (long long)row * a.N + col;
+    float4 s = zero;
+    int z = 0;
+    for (; z + 4 <= a.splits; z += 4) {
+      const float4 w0 = *(const float4*)(w + z * mn), w1 = *(const float4*)(w + (z + 1) * mn);
+      const float4 w2 = *(const float4*)(w + (z + 2) * mn), w3 = *(const float4*)(w + (z + 3) * mn);
+      s.x = (((s.x + w0.x) + w1.x) + w2.x) + w3.x;
+      s.y = (((s.y + w0.y) + w1.y) + w2.y) + w3.y;
+      s.z = (((s.z + w0.z) + w1.z) + w2.z) + w3.z;
+      s.w = (((s.w + w0.w) + w1.w) + w2.w) + w3.w;
+    }
+    for (; z < a.splits; ++z) {
+      const float4 w0 = *(const float4*)(w + z * mn);
+      s.x += w0.x; s.y += w0.y; s.z += w0.z; s.w += w0.w;
+    }
+    float4 v{a.alpha * s.x + bv.x, a.alpha * s.y + bv.y, a.alpha * s.z + bv.z, a.alpha * s.w + bv.w};
+    if (a.res) {
+      const float4 r = *(const float4*)(a.res + bidx * a.sR + (long long)row * a.ldr + col);
+      v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+    }
+    float* cp = a.C + bidx * a.sC + (long long)row * a.ldc + col;
+    if (a.beta != 0.f) {
+      const float4 c = *(const float4*)cp;
+      v.x += a.beta * c.x; v.y += a.beta * c.y; v.z += a.beta * c.z; v.w += a.beta * c.w;
+    }
+    *(float4*)cp = v;
+  }
+}
+
 
 // ------------------------------------------------------------------------------------------
 // host-side dispatch
@@ -1961,6 +2002,8 @@ inline void plan_splits(GemmArgs& a, int cfg, float* ws, size_t ws_bytes) {
 }
 
 int gemm_finish(GemmArgs& a, hipStream_t st);
+bool splitk_vec_ok(const GemmArgs& a);                  // splitk_reduce4_rows applies
+void splitk_vec_grid(const GemmArgs& a, int& gx, int& gy);  // its (column groups, row blocks) grid
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 constexpr long long MAX_DESC_BYTES = 0xFFFFFF00LL;  // one buffer descriptor covers < 4 GiB

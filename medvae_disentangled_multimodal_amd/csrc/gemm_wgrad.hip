@@ -4,14 +4,30 @@
 namespace mvae {
 // dbias[m] = beta*dbias[m] + sum over splits of the per-split row sums: one wave per row, lanes over the
 // splits, then the fixed wave tree (deterministic; the splits' loads are all in flight at once)
-__global__ void __launch_bounds__(256) bias_reduce_kernel(const float* __restrict__ part, int splits, int m,
-                                                          float* dbias, float beta) {
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+__device__ __forceinline__ void bias_reduce_rows(const float* __restrict__ part, int splits, int m, float* dbias,
+                                                 float beta, int blk) {
+  const int i = blk * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= m) return;
   float s = 0.f;
   for (int z = lane; z < splits; z += 64) s += part[(long long)z * m + i];
   s = wave_sum_f(s);
   if (lane == 0) dbias[i] = (beta != 0.f ? beta * dbias[i] : 0.f) + s;
+}
+
+__global__ void __launch_bounds__(256) bias_reduce_kernel(const float* __restrict__ part, int splits, int m,
+                                                          float* dbias, float beta) {
+  bias_reduce_rows(part, splits, m, dbias, beta, blockIdx.x);
+}
+
+// The weight-gradient epilogue of a split-K launch in ONE launch: blocks x < gx reduce the dW partials
+// (splitk_reduce4_rows), blocks x >= gx of row 0 sum the conv bias gradient from the per-split row sums
+// (bias_reduce_rows); the two halves touch disjoint memory.
+__global__ void __launch_bounds__(256) wgrad_finish4_kernel(GemmArgs a, int gx, float* dbias, float bbeta) {
+  if ((int)blockIdx.x < gx) {
+    splitk_reduce4_rows(a, blockIdx.x, blockIdx.y, gridDim.y);
+    return;
+  }
+  if (blockIdx.y == 0) bias_reduce_rows(a.bias_ws, a.splits, a.M, dbias, bbeta, blockIdx.x - gx);
 }
 
 // Upsample-conv weight gradient from the per-class partials of the sub-pixel form, already summed over the
@@ -142,6 +158,15 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
       else if (va) launch_small<A_COLM, 4, B_WGRAD_UPS, 1>(a, st, cfg);
       else if (vb) launch_small<A_COLM, 1, B_WGRAD_UPS, 4>(a, st, cfg);
       else launch_small<A_COLM, 1, B_WGRAD_UPS, 1>(a, st, cfg);
+    }
+    if (dbias && a.splits > 1 && splitk_vec_ok(a)) {  // dW reduction + bias gradient: one launch
+      int gx, gy;
+      splitk_vec_grid(a, gx, gy);
+      hipLaunchKernelGGL(wgrad_finish4_kernel, dim3(gx + cdiv(a.M, 4), gy), dim3(256), 0, st, a, gx, dbias,
+                         b0 == 0 ? beta : 1.f);
+      const int rc = launch_status();
+      if (rc) return rc;
+      continue;
     }
     if (dbias)
       hipLaunchKernelGGL(bias_reduce_kernel, dim3(cdiv(a.M, 4)), dim3(256), 0, st, (const float*)a.bias_ws,
