@@ -1719,6 +1719,17 @@ __device__ __forceinline__ void splitk_reduce4_rows(const GemmArgs& a, int bx, i
     const float* w = a.ws + (long long)bidx * a.splits * mn + (long long)row * a.N + col;
     float4 s = zero;
     int z = 0;
+    // 16 partial loads in flight per thread (the split loop is a latency chain, not a bandwidth one: a few thousand
+    // threads each walk up to 256 splits), summed strictly in split order (the result does not depend on the depth)
+    for (; z + 16 <= a.splits; z += 16) {
+      float4 wv[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) wv[j] = *(const float4*)(w + (z + j) * mn);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        s.x += wv[j].x; s.y += wv[j].y; s.z += wv[j].z; s.w += wv[j].w;
+      }
+    }
     for (; z + 4 <= a.splits; z += 4) {
       const float4 w0 = *(const float4*)(w + z * mn), w1 = *(const float4*)(w + (z + 1) * mn);
       const float4 w2 = *(const float4*)(w + (z + 2) * mn), w3 = *(const float4*)(w + (z + 3) * mn);

@@ -273,15 +273,15 @@ class _TransposedWeights:
     descriptor table is then uploaded once, and from the next step on fit_step's weight prep (prep_flat_weights)
     re-lays out all of them before the forward, each dgrad reading its slot (~30 launches fewer per c3 step). Valid
     until the optimizer step, like _FlatWeights. Only weights inside the flat parameter buffer are tabled (stable
-    addresses); the buffers of replaced tables stay alive (a captured step graph may have baked them in)."""
-    __slots__ = ("slots", "want", "table", "buf", "n", "blocks", "fresh", "keep", "base", "end", "tbase", "tend")
+    addresses); a step graph that bakes in the table and its buffer pins both (ARENA.pinning), so a replaced table
+    is freed unless a live graph still uses it."""
+    __slots__ = ("slots", "want", "table", "buf", "n", "blocks", "fresh", "base", "end", "tbase", "tend")
 
     def __init__(self):
         self.slots, self.want = {}, {}
         self.table = self.buf = None
         self.n = self.blocks = 0
         self.fresh = False
-        self.keep = []
         self.base = self.end = self.tbase = self.tend = 0
 
 
@@ -304,8 +304,6 @@ def refresh_weight_tables(flat_data: torch.Tensor):
 
 def _wt_rebuild(dev):
     if (_WT.tbase, _WT.tend) != (_WT.base, _WT.end):  # a new flat buffer: the table's weight addresses are gone
-        if _WT.table is not None:
-            _WT.keep.append((_WT.table, _WT.buf))
         _WT.slots, _WT.table, _WT.buf, _WT.n = {}, None, None, 0
         _WT.want = {k: v for k, v in _WT.want.items() if _WT.base <= k[0] < _WT.end}
         _WT.tbase, _WT.tend = _WT.base, _WT.end
@@ -327,8 +325,6 @@ def _wt_rebuild(dev):
             arr[i] = (wp, buf.data_ptr() + offs[k], co, rs, c, split, b0, 0)
             b0 += _wt_blocks(co, rs, c)
         table = torch.from_numpy(arr.view(np.uint8).copy()).to(dev)
-        if _WT.table is not None:
-            _WT.keep.append((_WT.table, _WT.buf))
         _WT.slots, _WT.table, _WT.buf, _WT.n, _WT.blocks = offs, table, buf, len(keys), b0
         _WT.want = dict(info)
 
@@ -340,6 +336,10 @@ def _prep_transposed(dev, st):
     if not torch.cuda.is_current_stream_capturing():
         _wt_rebuild(dev)
     if _WT.n and (_WT.tbase, _WT.tend) == (_WT.base, _WT.end):
+        if ARENA.pinning is not None:  # a step graph being recorded bakes in the table and its buffer
+            for t in (_WT.table, _WT.buf):
+                if not any(p is t for p in ARENA.pinning):
+                    ARENA.pinning.append(t)
         _lib.call("mvae_conv_weight_transpose_batched", _WT.table.data_ptr(), _WT.n, _WT.blocks, st)
         _WT.fresh = True
 
@@ -372,6 +372,8 @@ def prep_flat_weights(flat_data: torch.Tensor):
     if _FLATW.buf is None or _FLATW.buf.numel() < nbytes or _FLATW.buf.device != flat_data.device:
         _FLATW.buf = torch.empty(nbytes, dtype=torch.uint8, device=flat_data.device)
     fn = "mvae_split_bf16" if fmt == 1 else "mvae_pack_bf16"
+    if ARENA.pinning is not None and not any(p is _FLATW.buf for p in ARENA.pinning):
+        ARENA.pinning.append(_FLATW.buf)  # (a step graph being recorded bakes it in)
     _lib.call(fn, flat_data.data_ptr(), _FLATW.buf.data_ptr(), n, _stream(flat_data))
     _FLATW.base, _FLATW.end, _FLATW.fmt, _FLATW.fresh = flat_data.data_ptr(), flat_data.data_ptr() + 4 * n, fmt, True
 
