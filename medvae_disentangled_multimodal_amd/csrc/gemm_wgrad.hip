@@ -19,15 +19,16 @@ __global__ void __launch_bounds__(256) bias_reduce_kernel(const float* __restric
   bias_reduce_rows(part, splits, m, dbias, beta, blockIdx.x);
 }
 
-// The weight-gradient epilogue of a split-K launch in ONE launch: blocks x < gx reduce the dW partials
-// (splitk_reduce4_rows), blocks x >= gx of row 0 sum the conv bias gradient from the per-split row sums
-// (bias_reduce_rows); the two halves touch disjoint memory.
-__global__ void __launch_bounds__(256) wgrad_finish4_kernel(GemmArgs a, int gx, float* dbias, float bbeta) {
-  if ((int)blockIdx.x < gx) {
-    splitk_reduce4_rows(a, blockIdx.x, blockIdx.y, gridDim.y);
+// The weight-gradient epilogue of a split-K launch in ONE launch: grid rows y < gy reduce the dW partials
+// (splitk_reduce4_rows over the reducer's own (gx, gy) grid), the rows after them sum the conv bias gradient from the
+// per-split row sums (bias_reduce_rows, block (x, gy + r) -> bias block r * gx + x); the two parts touch disjoint
+// memory and no block is idle.
+__global__ void __launch_bounds__(256) wgrad_finish4_kernel(GemmArgs a, int gy, float* dbias, float bbeta) {
+  if ((int)blockIdx.y < gy) {
+    splitk_reduce4_rows(a, blockIdx.x, blockIdx.y, gy);
     return;
   }
-  if (blockIdx.y == 0) bias_reduce_rows(a.bias_ws, a.splits, a.M, dbias, bbeta, blockIdx.x - gx);
+  bias_reduce_rows(a.bias_ws, a.splits, a.M, dbias, bbeta, (blockIdx.y - gy) * gridDim.x + blockIdx.x);
 }
 
 // Upsample-conv weight gradient from the per-class partials of the sub-pixel form, already summed over the
@@ -162,7 +163,7 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
     if (dbias && a.splits > 1 && splitk_vec_ok(a)) {  // dW reduction + bias gradient: one launch
       int gx, gy;
       splitk_vec_grid(a, gx, gy);
-      hipLaunchKernelGGL(wgrad_finish4_kernel, dim3(gx + cdiv(a.M, 4), gy), dim3(256), 0, st, a, gx, dbias,
+      hipLaunchKernelGGL(wgrad_finish4_kernel, dim3(gx, gy + cdiv(cdiv(a.M, 4), gx)), dim3(256), 0, st, a, gy, dbias,
                          b0 == 0 ? beta : 1.f);
       const int rc = launch_status();
       if (rc) return rc;
