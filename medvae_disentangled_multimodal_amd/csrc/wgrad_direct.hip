@@ -209,19 +209,10 @@ __global__ void __launch_bounds__(256) wgrad_direct_final_kernel(const float* __
   const int o = blockIdx.x * 64 + (threadIdx.x & 63), gl = threadIdx.x >> 6;
   const bool isw = o < nw, isb = !isw && dbias != nullptr && o < nw + co;
   float s = 0.f;
-  if (isw || isb) {  // 8 partial loads in flight per lane (a latency chain over up to 512 partials), summed in order
-    const float* src = isw ? part + o : bpart + (o - nw);
-    const size_t ld = isw ? (size_t)nw : (size_t)co;
-    int g = gl;
-    for (; g + 28 < G; g += 32) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = src[(size_t)(g + 4 * j) * ld];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += v[j];
-    }
-    for (; g < G; g += 4) s += src[(size_t)g * ld];
-  }
+  if (isw)
+    for (int g = gl; g < G; g += 4) s += part[(size_t)g * nw + o];
+  else if (isb)
+    for (int g = gl; g < G; g += 4) s += bpart[(size_t)g * co + (o - nw)];
   sh[gl][threadIdx.x & 63] = s;
   __syncthreads();
   if (gl == 0 && (isw || isb)) {
