@@ -93,7 +93,7 @@ HBM_MEASURED_GBS = {"read_only": 6262.0, "copy": 5314.0}
 
 def _pmc_traffic(config, family="gemm"):
     """HBM bytes per launch of a kernel family (gemm: gemm3x_kernel; gn: the gn_* GroupNorm chains) from the
-    committed PMC passes (tools/pmc_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc, separate passes) --
+    committed PMC passes (tools/gpu_evidence.sh traffic: FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc, separate passes) --
     counters cannot be read inside this timed run, so the profile of the same command is attached (newest round
     first)."""
     for tag in ("r03", "r02", "r01"):

@@ -224,8 +224,15 @@ class VAELightningModule(_Base):
         return {k: v for k, v in self.logged.items() if k.startswith(f"{split}/")}
 
     # ---------------------------------------------------------------------------------------
+    def teardown(self, stage: Optional[str] = None):
+        """Lightning's end-of-fit / test hook: drop the captured step and free the converted weight copies (~2 x the
+        conv weights' bytes, see ops.release_weight_buffers)."""
+        self._graph = None
+        ops.release_weight_buffers()
+
     def configure_optimizers(self):
         self._graph = None  # a captured step holds the previous optimizer's buffers and hyper-parameters
+        ops.release_weight_buffers()  # (rebuilt by the next prepared step, for this optimizer's flat buffer)
         if self.flat is None:
             self.flat = FlatParameters(self.model)
         oc = self.optimizer_config

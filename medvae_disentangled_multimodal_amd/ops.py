@@ -264,7 +264,6 @@ class _FlatWeights:
 
 
 _FLATW = _FlatWeights()
-_FLATW = _FlatWeights()
 
 
 class _TransposedWeights:
@@ -275,10 +274,13 @@ class _TransposedWeights:
     until the optimizer step, like _FlatWeights. Only weights inside the flat parameter buffer are tabled (stable
     addresses); a step graph that bakes in the table and its buffer pins both (ARENA.pinning), so a replaced table
     is freed unless a live graph still uses it."""
-    __slots__ = ("slots", "want", "table", "buf", "n", "blocks", "fresh", "base", "end", "tbase", "tend")
+    __slots__ = ("slots", "want", "table", "buf", "n", "blocks", "fresh", "base", "end", "tbase", "tend", "seen",
+                 "idle")
 
     def __init__(self):
         self.slots, self.want = {}, {}
+        self.seen = set()  # keys the dgrads of the current step asked for
+        self.idle = {}     # key -> consecutive prepared steps that did not ask for it
         self.table = self.buf = None
         self.n = self.blocks = 0
         self.fresh = False
@@ -287,6 +289,7 @@ class _TransposedWeights:
 
 _WT = _TransposedWeights()
 BATCHED_WT = os.environ.get("MVAE_NO_BATCHED_WT") is None
+WT_IDLE_STEPS = 2  # a table entry unused for this many prepared steps is dropped
 
 
 def _wt_blocks(co, rs, c):
@@ -304,13 +307,19 @@ def refresh_weight_tables(flat_data: torch.Tensor):
 
 def _wt_rebuild(dev):
     if (_WT.tbase, _WT.tend) != (_WT.base, _WT.end):  # a new flat buffer: the table's weight addresses are gone
-        _WT.slots, _WT.table, _WT.buf, _WT.n = {}, None, None, 0
+        _WT.slots, _WT.table, _WT.buf, _WT.n, _WT.idle = {}, None, None, 0, {}
         _WT.want = {k: v for k, v in _WT.want.items() if _WT.base <= k[0] < _WT.end}
         _WT.tbase, _WT.tend = _WT.base, _WT.end
-    if any(k not in _WT.slots for k in _WT.want):
+    # entries no step has asked for in the last WT_IDLE_STEPS prepared steps (e.g. the other arithmetic's formats after
+    # a precision switch) leave the table instead of being re-laid out every step
+    stale = [k for k, c in _WT.idle.items() if c >= WT_IDLE_STEPS]
+    for k in stale:
+        _WT.want.pop(k, None)
+        _WT.idle.pop(k, None)
+    if stale or any(k not in _WT.slots for k in _WT.want):
         import numpy as np
-        keys = list(_WT.slots) + [k for k in _WT.want if k not in _WT.slots]
-        info = {**{k: _WT.want.get(k) for k in _WT.slots}, **_WT.want}
+        keys = [k for k in _WT.slots if k in _WT.want] + [k for k in _WT.want if k not in _WT.slots]
+        info = dict(_WT.want)
         offs, o = {}, 0
         for k in keys:
             offs[k] = o
@@ -334,6 +343,10 @@ def _prep_transposed(dev, st):
     if not BATCHED_WT:
         return
     if not torch.cuda.is_current_stream_capturing():
+        if _WT.seen:  # the previous prepared step's requests: age the entries it did not use
+            for k in _WT.slots:
+                _WT.idle[k] = 0 if k in _WT.seen else _WT.idle.get(k, 0) + 1
+            _WT.seen = set()
         _wt_rebuild(dev)
     if _WT.n and (_WT.tbase, _WT.tend) == (_WT.base, _WT.end):
         if ARENA.pinning is not None:  # a step graph being recorded bakes in the table and its buffer
@@ -349,6 +362,7 @@ def _weight_t(w, co, kh, kw, c, split, nbytes, st) -> int:
     step's batched prep wrote, or a per-conv launch into arena scratch (recorded for the next table)."""
     p = w.data_ptr()
     key = (p, co, kh, kw, c, int(split))
+    _WT.seen.add(key)
     if _WT.fresh and key in _WT.slots:
         return _WT.buf.data_ptr() + _WT.slots[key]
     wt = ARENA.get("wt", nbytes, w.device)
@@ -376,6 +390,18 @@ def prep_flat_weights(flat_data: torch.Tensor):
         ARENA.pinning.append(_FLATW.buf)  # (a step graph being recorded bakes it in)
     _lib.call(fn, flat_data.data_ptr(), _FLATW.buf.data_ptr(), n, _stream(flat_data))
     _FLATW.base, _FLATW.end, _FLATW.fmt, _FLATW.fresh = flat_data.data_ptr(), flat_data.data_ptr() + 4 * n, fmt, True
+
+
+def release_weight_buffers():
+    """Free the step's converted weight copies (_FLATW.buf: the flat buffer in split4 / packed bf16, 4 / 2 B per
+    parameter; _WT: the dgrad re-layouts, about one more copy of the conv weights -- together ~7.4 GB for the 927 M
+    parameters of c4 in the 3xBF16 mode) and forget the re-layout table. The next prepared step rebuilds them."""
+    flat_weights_stale()
+    _FLATW.buf, _FLATW.base, _FLATW.end = None, 0, 0
+    _WT.slots, _WT.want, _WT.seen, _WT.idle = {}, {}, set(), {}
+    _WT.table = _WT.buf = None
+    _WT.n = _WT.blocks = 0
+    _WT.tbase = _WT.tend = 0
 
 
 def flat_weights_stale():
@@ -1199,19 +1225,20 @@ class LossCombineFn(torch.autograd.Function):
         w = list(map(float, weights)) + [0.0] * (4 - nt)
         _lib.call("mvae_loss_combine4_fwd", *ptrs, *w, nt, float(nonfinite_total), *optr, flags.data_ptr(),
                   _stream(terms[0]))
-        ctx.w, ctx.nt, ctx.flags = w, nt, flags
+        ctx.w, ctx.nt = w, nt
+        ctx.save_for_backward(flags)  # freed with the graph; a retained graph can run its backward again
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, gtot, *gterms):
         nt = ctx.nt
-        dev = ctx.flags.device
+        (flags,) = ctx.saved_tensors
+        dev = flags.device
         gt = None if gtot is None else gtot.float().contiguous()
         gs = [None if g is None else g.float().contiguous() for g in gterms] + [None] * (4 - nt)
         out = torch.empty(nt, device=dev, dtype=torch.float32)
-        _lib.call("mvae_loss_combine4_bwd", ctx.flags.data_ptr(), *ctx.w, nt, _ptr(gt), *[_ptr(g) for g in gs],
+        _lib.call("mvae_loss_combine4_bwd", flags.data_ptr(), *ctx.w, nt, _ptr(gt), *[_ptr(g) for g in gs],
                   out.data_ptr(), _stream(out))
-        ctx.flags = None
         return (None, None, *[out[i] for i in range(nt)])
 
 
@@ -1783,8 +1810,15 @@ class ConditionConcatFn(torch.autograd.Function):
         return (dx, None, *ret)
 
 
+COND_MAX_HW = 256  # csrc/condition.hip COND_MAX_HW: the bilinear backward's LDS row buffer
+
+
+def condition_concat_fits(x: torch.Tensor) -> bool:
+    return x.is_cuda and x.dim() == 4 and max(x.shape[2], x.shape[3]) <= COND_MAX_HW
+
+
 def condition_concat(x, cond, weight, bias):
-    """(x_cond [B, 2C, H, W] channels_last, relu(condition_proj) [B, C*64])."""
+    """(x_cond [B, 2C, H, W] channels_last, relu(condition_proj) [B, C*64]); H, W <= COND_MAX_HW."""
     return ConditionConcatFn.apply(x, cond, weight, bias)
 
 

@@ -155,7 +155,9 @@ class ConditionalVAE(BaseVAE):
         return F.interpolate(cmap, size=(height, width), mode="bilinear", align_corners=False)
 
     def encode(self, x, condition):
-        if self.condition_method == "concat" and x.is_cuda:  # one fused conditioning op (csrc/condition.hip)
+        # one fused conditioning op (csrc/condition.hip) up to 256 x 256 (every reference config: <= 224); larger
+        # images take the module path (Linear + ReLU + bilinear interpolate + cat, conditional_vae.py:107-127)
+        if self.condition_method == "concat" and ops.condition_concat_fits(x):
             lin = self.condition_proj[0]
             x_cond, _ = ops.condition_concat(x, condition, lin.weight, lin.bias)
             return super().encode(x_cond)

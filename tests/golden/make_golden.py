@@ -262,6 +262,40 @@ def disc_case():
     print(f"disc: g_loss={float(g_loss):.8f} d_weight={float(d_weight):.6f} d_loss={float(d_loss):.8f}")
 
 
+LATENT_B = 512  # the c3 bench batch (BASELINE config 3: bs 512, z [16, 7, 7])
+
+
+def latent_case():
+    """The batch-coupled latent losses at the c3 bench batch, on the reference's own
+    DisentangledConditionalVAE.modality_separation_loss / contrastive_loss (src/models/
+    disentangled_conditional_vae.py:305-386, partition_latent :195-206) -- a fixed z [512, 16, 7, 7] with ids uniform
+    over the 5 modalities plus a few out-of-range ids (each its own centroid: the losses take the raw ids). Values and
+    dL/dz of each term, in the reference's fp32 and with the same reference methods on float64 tensors. Only the
+    partition's 8 + 8 elements (flat NCHW 0..15) can carry gradient: the fixture stores that [B, 16] slice and the
+    largest magnitude elsewhere (0)."""
+    torch.manual_seed(0)
+    m = ref_models.DisentangledConditionalVAE(
+        num_modalities=5, shared_latent_dim=8, modality_latent_dim=8, input_channels=3, latent_dim=16,
+        hidden_channels=32, ch_mult=(1, 2, 4), num_res_blocks=1, attn_resolutions=[], dropout=0.0, resolution=28)
+    rng = np.random.Generator(np.random.PCG64(512))
+    z = rng.standard_normal(size=(LATENT_B, 16, 7, 7)).astype(np.float32)
+    ids = rng.integers(0, 5, size=(LATENT_B,)).astype(np.int64)
+    ids[[5, 77, 301]] = [7, 9, 17]
+    rec = {"in.z": z, "in.idx": ids}
+    for tag, dt in (("f32", torch.float32), ("f64", torch.float64)):
+        for term, fn in (("sep", m.modality_separation_loss), ("con", m.contrastive_loss)):
+            zt = torch.from_numpy(z).to(dt).requires_grad_()
+            v = fn(zt, torch.from_numpy(ids))
+            v.backward()
+            g = zt.grad.reshape(LATENT_B, -1)
+            rec[f"{term}.{tag}"] = np.array(float(v))
+            rec[f"grad_{term}.{tag}"] = g[:, :16].numpy().astype(np.float64 if tag == "f64" else np.float32).copy()
+            rec[f"grad_{term}_rest_max.{tag}"] = np.array(float(g[:, 16:].abs().max()))
+    np.savez(os.path.join(HERE, "latent_b512.npz"), **rec)
+    print(f"latent_b512: sep={float(rec['sep.f32']):.8f} ({float(rec['sep.f64']):.10f} f64) "
+          f"con={float(rec['con.f32']):.8f} ({float(rec['con.f64']):.10f} f64)")
+
+
 def known_answer_anchor():
     """SURVEY.md section 8(c) known-answer anchor, run on the reference itself."""
     torch.manual_seed(0)
@@ -282,10 +316,12 @@ def known_answer_anchor():
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    sel = sys.argv[1:] or list(CASES) + ["disc"]
+    sel = sys.argv[1:] or list(CASES) + ["disc", "latent"]
     for n in sel:
         if n == "disc":
             disc_case()
+        elif n == "latent":
+            latent_case()
         else:
             run_case(n, CASES[n])
     known_answer_anchor()

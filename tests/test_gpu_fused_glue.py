@@ -152,6 +152,18 @@ def test_loss_combine_total_only_backward():
     assert [float(t.grad) for t in ts] == pytest.approx([1.0, 6.0, 0.1, 0.05], rel=1e-7)
 
 
+def test_loss_combine_second_backward_through_retained_graph():
+    """autograd.grad with retain_graph, then backward through the same graph (the torch composition allows it)."""
+    from medvae_disentangled_multimodal_amd import ops
+    dev = _dev()
+    ts = [torch.tensor(v, device=dev, requires_grad=True) for v in (0.5, float("nan"), 0.125)]
+    tot = ops.loss_combine(ts, [1.0, 6.0, 0.1])[0]
+    g1 = torch.autograd.grad(tot, ts, retain_graph=True)
+    tot.backward()
+    assert [float(g) for g in g1] == pytest.approx([1.0, 0.0, 0.1], rel=1e-7)
+    assert [float(t.grad) for t in ts] == pytest.approx([1.0, 0.0, 0.1], rel=1e-7)
+
+
 # ---- batched dgrad weight re-layouts (ops._TransposedWeights, mvae_conv_weight_transpose_batched) -------------------
 _CVAE = dict(input_channels=3, latent_dim=8, hidden_channels=32, ch_mult=(1, 2, 4), num_res_blocks=1,
              attn_resolutions=[14], dropout=0.0, resolution=28, condition_method="concat")

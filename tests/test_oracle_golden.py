@@ -118,3 +118,24 @@ def test_oracle_discriminator_matches_reference():
         assert abs(float((g * g).sum()) - s[1]) <= 1e-4 * s[1] + 1e-12, k
     for k, v in running.items():
         assert rel_err(v, data[f"buf.{k}"]) < 1e-5, k
+
+
+@pytest.mark.parametrize("tag,dt", [("f32", torch.float32), ("f64", torch.float64)])
+def test_oracle_latent_losses_b512(tag, dt):
+    """The oracle's separation / contrastive terms against the reference's own methods at the c3 bench batch
+    (tests/golden/latent_b512.npz, make_golden.latent_case): B = 512, ids 0..4 plus out-of-range 7 / 9 / 17."""
+    data = dict(np.load(os.path.join(GOLDEN, "latent_b512.npz"), allow_pickle=False))
+    a = R.make_arch("DisentangledConditionalVAE", dict(num_modalities=5, shared_latent_dim=8, modality_latent_dim=8,
+                                                       hidden_channels=32, ch_mult=[1, 2, 4], num_res_blocks=1,
+                                                       attn_resolutions=[], dropout=0.0, resolution=28))
+    idx = torch.from_numpy(data["in.idx"])
+    tol = 1e-6 if tag == "f32" else 1e-12
+    for term, fn in (("sep", R.separation_loss), ("con", R.contrastive_loss)):
+        z = torch.from_numpy(data["in.z"]).to(dt).requires_grad_()
+        v = fn(a, z, idx)
+        v.backward()
+        ref = float(data[f"{term}.{tag}"])
+        assert abs(float(v) - ref) <= tol * abs(ref), (term, float(v), ref)
+        g = z.grad.reshape(z.shape[0], -1)
+        assert rel_err(g[:, :16], data[f"grad_{term}.{tag}"]) < (1e-5 if tag == "f32" else 1e-12), term
+        assert float(g[:, 16:].abs().max()) == float(data[f"grad_{term}_rest_max.{tag}"]) == 0.0
