@@ -80,10 +80,14 @@ CONFIGS = {
                loss=dict(type="disentangled_vae", recon_loss_type="mse", kl_weight=1.0, recon_weight=1.0,
                          separation_weight=0.1, contrastive_weight=0.05)),
 }
+# config 4 in EXACT fp32 (the reference's arithmetic: every conv / bmm on the f32-input MFMA, v_mfma_f32_*_f32, no
+# operand rounding) -- timed next to the default 3xBF16 line against the 157.3 TF/s fp32 MFMA peak
+CONFIGS["c4x"] = dict(CONFIGS["c4"], precision="32-exact")
 METRIC_C4 = "training images/sec (whole node) + ELBO parity, multimodal CVAE 64\u00d764 bs=256"
 
 BF16_DENSE_PEAK_TF = 2500.0
 PEAK_3XBF16_TF = BF16_DENSE_PEAK_TF / 3.0
+FP32_MFMA_PEAK_TF = 157.3  # dense f32-input MFMA (v_mfma_f32_32x32x2_f32 / 16x16x4_f32)
 HBM_PEAK_GBS = 8000.0
 # measured on MI355X (profiles/r02_ceilings.txt): the GEMM main-loop structure without global traffic, per MFMA
 # shape (fp32-equivalent TF/s), and plain HBM streams (read-only / copy)
@@ -96,7 +100,7 @@ def _pmc_traffic(config, family="gemm"):
     committed PMC passes (tools/gpu_evidence.sh traffic: FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc, separate passes) --
     counters cannot be read inside this timed run, so the profile of the same command is attached (newest round
     first)."""
-    for tag in ("r03", "r02", "r01"):
+    for tag in ("r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", f"{tag}_{config}_{family}_traffic.json")
         if os.path.exists(path):
             break
@@ -231,7 +235,7 @@ def cpu_baseline_for(cfg, seconds_budget=20.0):
     return out
 
 
-def _roofline(rec_all, bf16, config, step_ms, detail, rank):
+def _roofline(rec_all, bf16, config, step_ms, detail, rank, exact=False):
     """GEMM-family (MFMA) and GroupNorm-family (HBM) rooflines from the HIP-event records of one step."""
     rec = [r for r in rec_all if r[0] not in ops_hbm_tags()]
     hbm_rec = [r for r in rec_all if r[0] in ops_hbm_tags()]
@@ -256,7 +260,7 @@ def _roofline(rec_all, bf16, config, step_ms, detail, rank):
         d[2] += s_.elapsed_time(e)
     ach = tot_fl / (tot_ms * 1e-3) / 1e12
     alg_bytes = sum(gemm_algorithmic_bytes(r[0], r[4]) for r in rec) / max(len(rec), 1)
-    peak = BF16_DENSE_PEAK_TF if bf16 else PEAK_3XBF16_TF
+    peak = BF16_DENSE_PEAK_TF if bf16 else FP32_MFMA_PEAK_TF if exact else PEAK_3XBF16_TF
     pmc = _pmc_traffic(config)
     roofline = {"bound": "mfma", "kernel": "gemm3x_kernel (implicit-GEMM conv + attention bmm, all launches)",
                 "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
@@ -264,6 +268,7 @@ def _roofline(rec_all, bf16, config, step_ms, detail, rank):
                 "traffic_unit": "HBM bytes per launch (PMC)", "traffic_detail": pmc,
                 "algorithmic_bytes_per_launch": round(alg_bytes),
                 "peak_note": ("bf16 dense MFMA peak 2.5 PF/s (bf16 operands, fp32 accumulate)" if bf16 else
+                              "exact fp32: dense f32-input MFMA peak 157.3 TF/s" if exact else
                               "3xBF16 fp32-emulation ceiling = bf16 dense MFMA 2.5 PF/s / 3; "
                               "native fp32 MFMA peak is 157.3 TF/s"),
                 "achieved_note": ("algorithmic FLOPs of the algorithms run (Upsample convs in sub-pixel form "
@@ -274,7 +279,7 @@ def _roofline(rec_all, bf16, config, step_ms, detail, rank):
                 "gemm_share_of_step": round(tot_ms / step_ms, 3),
                 "by_pass": {k: {"launches": v[0], "ms": round(v[2], 2),
                                 "TFLOP/s": round(v[1] / (v[2] * 1e-3) / 1e12, 1)} for k, v in by.items()}}
-    if not bf16:  # measured ceiling of the main-loop structure (no global traffic): profiles/r02_ceilings.txt
+    if not bf16 and not exact:  # measured ceiling of the main-loop structure (no global traffic): r02_ceilings.txt
         for k, v in roofline["by_pass"].items():
             c = STRUCT_CEIL_TF.get(k)
             if c is None:
@@ -285,6 +290,34 @@ def _roofline(rec_all, bf16, config, step_ms, detail, rank):
             "measured on the box: the kernel's per-wave 3xBF16 LDS-fragment + MFMA loop with one barrier per "
             "K-tile and no global loads, random operands (tools/micro/mfma_shape.hip): 16x16x32 (fwd / dgrad) "
             "598 TF/s, 32x32x16 (wgrad / attention) 559 TF/s fp32-equivalent")
+    loss_rec = [r for r in hbm_rec if r[0].startswith("loss_")]
+    hbm_rec = [r for r in hbm_rec if r[0].startswith("gn_")]
+    if loss_rec:  # the loss side (reparameterization, KL, reconstruction; SURVEY 8(d) bytes) against the HBM roofline
+        lb = {}
+        for tag, nbytes, s_, e, shp, _ in loss_rec:
+            d = lb.setdefault(f"{shp[0]}_{tag[5:]}", [0, 0.0, 0.0])
+            d[0] += 1
+            d[1] += nbytes
+            d[2] += s_.elapsed_time(e)
+        lms = sum(v[2] for v in lb.values())
+        lby = sum(v[1] for v in lb.values())
+        roofline["hbm_loss_kernels"] = {
+            "bound": "hbm", "kernel": "reparam_fwd / reparam_bwd, KL reduce / kl_bwd, MSE reduce / recon_bwd (csrc/loss.hip)",
+            "achieved": round(lby / (lms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(lby / (lms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms_per_step": round(lms, 3),
+            "algorithmic_bytes_per_step": round(lby),
+            "bytes_note": "algorithmic bytes (SURVEY 8(d)): reparam fwd 16 B/latent (read mu, logvar, eps; write z), "
+                          "reparam bwd 16 B/latent (read dz, eps, logvar; write dlogvar), KL fwd 8 B/latent, KL bwd "
+                          "16 B/latent (write dmu, dlogvar), MSE fwd 8 B/pixel, MSE bwd 12 B/pixel; the reduce launches "
+                          "include their fixed-order final stage",
+            "by_pass": {k: {"launches": v[0], "ms": round(v[2], 4), "bytes": round(v[1]),
+                            "GB/s": round(v[1] / (v[2] * 1e-3) / 1e9, 1)} for k, v in lb.items()}}
+        lpmc = _pmc_traffic(config, "loss")
+        if lpmc:
+            moved = lpmc["total_bytes_per_step"]
+            roofline["hbm_loss_kernels"].update({"traffic_bytes_per_step": moved,
+                                                 "traffic_over_algorithmic": round(moved / max(lby, 1.0), 3),
+                                                 "traffic_detail": lpmc})
     if hbm_rec:  # the memory-bound GroupNorm(+SiLU) family against the HBM roofline
         hb = {}
         for tag, nbytes, s_, e, _, _ in hbm_rec:
@@ -318,7 +351,7 @@ def ops_hbm_tags():
     return ops.HBM_TAGS
 
 
-def run_config(name, args, rank, world, dev, want_cpu=True):
+def run_config(name, args, rank, world, dev, want_cpu=True, steps=None, warmup=None):
     """Build the config's model, warm up, time `args.steps` steps (barrier + synchronize on both sides, max over
     ranks), then one instrumented step for the rooflines. Returns the measured fields of the JSON line."""
     import medvae_disentangled_multimodal_amd as M
@@ -326,6 +359,8 @@ def run_config(name, args, rank, world, dev, want_cpu=True):
     cfg = dict(CONFIGS[name])
     if args.batch:
         cfg["batch"] = args.batch
+    n_steps = args.steps if steps is None else steps
+    n_warm = args.warmup if warmup is None else warmup
     torch.manual_seed(42)
     model = getattr(M, cfg["cls"])(**cfg["kwargs"]).to(dev)
     mod = M.VAELightningModule(model, cfg["opt"], {"type": "none"}, cfg["loss"], gradient_clip_val=cfg["clip"],
@@ -341,18 +376,18 @@ def run_config(name, args, rank, world, dev, want_cpu=True):
     # HIP graph -- same kernels and arithmetic, the host issues one launch per step; eager for c4 / c5 and N > 1
     graphed = cfg.get("graph", False) and world == 1 and not args.eager
     step = mod.fit_step_graphed if graphed else mod.fit_step
-    for i in range(args.warmup):
+    for i in range(n_warm):
         mod.fit_step(batches[i % 2], i)
     if graphed:  # graph set-up, untimed: one eager step (if no warm-up ran), the capture (records, executes
-        if args.warmup == 0:  # nothing), one replay
+        if n_warm == 0:  # nothing), one replay
             mod.fit_step(batches[0], 0)
-        step(batches[args.warmup % 2], args.warmup)
+        step(batches[n_warm % 2], n_warm)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(n_steps):
         loss = step(batches[i % 2], i)
     torch.cuda.synchronize()
     if world > 1:
@@ -367,6 +402,7 @@ def run_config(name, args, rank, world, dev, want_cpu=True):
 
     roofline = None
     bf16 = cfg.get("precision", "32") == "bf16-mixed"
+    exact = cfg.get("precision", "32") == "32-exact"
     if not args.no_kernel_timing:
         ops.PROFILE = []
         torch.cuda.synchronize()
@@ -376,7 +412,7 @@ def run_config(name, args, rank, world, dev, want_cpu=True):
         step_ms = (time.perf_counter() - t1) * 1e3
         rec_all = ops.PROFILE
         ops.PROFILE = None
-        roofline = _roofline(rec_all, bf16, name, step_ms, args.detail, rank)
+        roofline = _roofline(rec_all, bf16, name, step_ms, args.detail, rank, exact)
     del mod, model, batches, step
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -384,14 +420,16 @@ def run_config(name, args, rank, world, dev, want_cpu=True):
     cpu = None
     if rank == 0 and world == 1 and want_cpu and not args.no_cpu_baseline:
         cpu = cpu_baseline_for(cfg)
-    imgs = cfg["batch"] * world * args.steps
-    return {"value": round(imgs / dt, 3), "unit": "images/s", "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 3),
+    imgs = cfg["batch"] * world * n_steps
+    return {"value": round(imgs / dt, 3), "unit": "images/s", "steps": n_steps, "warmup": n_warm,
+            "ms_per_step": round(dt / n_steps * 1e3, 3),
             "dtype": ("bf16 (bf16-mixed: bf16 MFMA operands, fp32 accumulate/activations)" if bf16
+                      else "fp32 (exact: f32-input MFMA, no operand rounding)" if exact
                       else "fp32 (3xBF16 MFMA, fp32 accumulate)"),
             "config": {"workload": f"{cfg['cls']} {cfg['res']}x{cfg['res']}x{cfg['kwargs'].get('input_channels', 3)} "
                                    f"train step (fwd+loss+bwd+clip+{cfg['opt']['type']})"
-                                   + (" + LPIPS-VGG generator objective" if bf16 else ""),
+                                   + (" + LPIPS-VGG generator objective" if bf16 else "")
+                                   + (", exact fp32 arithmetic" if exact else ""),
                        "model": cfg["cls"], "params": nparams, "global_batch": cfg["batch"] * world,
                        "per_gpu_batch": cfg["batch"], "resolution": cfg["res"], "parallelism": f"dp{world}",
                        "rccl_world_size": world, "backend": dist.get_backend() if world > 1 else None,
@@ -464,7 +502,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
-                    help="one config alone (default: c4, plus the c2 / c3 / c5 block and the parity block at N=1)")
+                    help="one config alone (default: c4, plus the c2 / c3 / c5 / c4x block and the parity block at "
+                         "N=1; c4x = c4 in exact fp32)")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch override (default: config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -494,8 +533,15 @@ def main():
     extra, parity = None, None
     if full:  # the other BASELINE configs on the same box, same clock (their own images/s; not summed)
         extra = {}
-        for c in ("c2", "c3", "c5"):
-            r = run_config(c, args, rank, world, dev)
+        for c in ("c2", "c3", "c5", "c4x"):
+            # c4x (exact fp32, ~4x the 3xBF16 step time): a short timed region, and the c4 line's CPU baseline (same
+            # model and step on the CPU)
+            short = c == "c4x"
+            r = run_config(c, args, rank, world, dev, want_cpu=not short, steps=min(args.steps, 4) if short else None,
+                           warmup=min(args.warmup, 1) if short else None)
+            if short:
+                r["cpu_baseline"] = dict(line["cpu_baseline"] or {}, note="the c4 line's baseline (same model / step)") \
+                    if line["cpu_baseline"] else None
             extra[c] = {k: r[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config",
                                           "loss", "roofline", "cpu_baseline")}
             print(f"[bench] {c}: {r['value']} images/s ({r['ms_per_step']} ms/step)", file=sys.stderr, flush=True)

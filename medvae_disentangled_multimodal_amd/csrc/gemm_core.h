@@ -663,6 +663,9 @@ struct LoadWgradX {
     krw = (C4 % 64 == 0) ? __builtin_amdgcn_readfirstlane(kr) : kr;
   }
   __device__ void prep(const GemmArgs& a) {
+#ifdef MVAE_WGRAD_XFAKE  // timing-only build: no gather index math (wrong results)
+    return;
+#endif
     // slot 0's pixel by division; the others step from it (pixels NT / C4 apart: usually the same or the next image
     // row), so each K-tile costs one decomposition instead of NS -- the k-rows are wave-uniform, this is scalar work
     // on every wave of the workgroup, and the wgrad loop is short of scalar issue (PMC: 16 % of wave cycles in the
@@ -707,6 +710,12 @@ struct LoadWgradX {
     const unsigned img = (unsigned)(a.H * a.W);
     const int krow = kr + i * (NT / C4);
     const bool kv = (krow < BK) & (k + krow < a.K);
+#ifdef MVAE_WGRAD_XFAKE
+    if (VEC == 4) {
+      v[i] = bload4(rs, (kv & nv[0]) ? (unsigned)(((k + krow) * a.Cx + cc[0]) * 4) : OOB);
+      return;
+    }
+#endif
     if constexpr (FAST) {
       const bool ok = kv & nv[0] & ((unsigned)(sh[i] + rr[0]) < (unsigned)a.H) & ((unsigned)(sw[i] + ss[0]) < (unsigned)a.W);
       v[i] = bload4(rs, ok ? sbase[i] + ldelta : OOB);
@@ -995,6 +1004,11 @@ struct DmaWgradX {
     for (int i = 0; i < S::NI; ++i) {
       const int kk = k + kr0 + i * S::NW * S::KPI;
       const int p = min(kk, K - 1);
+#ifdef MVAE_WGRAD_XFAKE  // timing-only build: no gather index math (wrong results)
+      ok_[i] = nv & (kk < K);
+      off_[i] = (unsigned)p * (unsigned)a.Cx * 2u + cb;
+      continue;
+#endif
       const int b = mdiv(p, a.mg_hw);
       const int rem = p - b * (a.Ho * a.Wo);
       const int oh = mdiv(rem, a.mg_wo);

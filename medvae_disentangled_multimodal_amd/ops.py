@@ -78,9 +78,10 @@ ARENA = _Arena()
 # Optional live kernel timing (bench.py): when PROFILE is a list, every implicit-GEMM launch is
 # bracketed by HIP events on the current stream and recorded as
 # (tag, algorithmic_flops, start, end, shape) -- shape = the launch's problem tuple. The HBM-bound
-# GroupNorm launches are recorded the same way under HBM_TAGS with algorithmic BYTES in the work slot.
+# GroupNorm launches are recorded the same way under HBM_TAGS with algorithmic BYTES in the work slot, and so are the
+# loss-side launches (reparameterization, KL, reconstruction MSE / L1 and their backwards: "loss_fwd" / "loss_bwd").
 PROFILE = None
-HBM_TAGS = ("gn_fwd", "gn_bwd")
+HBM_TAGS = ("gn_fwd", "gn_bwd", "loss_fwd", "loss_bwd")
 
 
 class _timed:
@@ -1140,13 +1141,11 @@ class ReparamFn(torch.autograd.Function):
         eps = nhwc(eps)
         n, zc, h, w = mean.shape
         z = torch.empty((n, zc, h, w), device=mean.device, dtype=torch.float32, memory_format=CL)
-        if ldm == ldl:
-            _lib.call("mvae_reparam_fwd", mean.data_ptr(), logvar.data_ptr(), ldm, eps.data_ptr(), z.data_ptr(),
-                      n * h * w, zc, _stream(mean))
-        else:
+        if ldm != ldl:
             mean, logvar = nhwc(mean.contiguous()), nhwc(logvar.contiguous())
             ldm = ldl = zc
-            _lib.call("mvae_reparam_fwd", mean.data_ptr(), logvar.data_ptr(), zc, eps.data_ptr(), z.data_ptr(),
+        with _timed("loss_fwd", 16.0 * z.numel(), ("reparam", n * h * w, zc)):  # read mu, logvar, eps; write z
+            _lib.call("mvae_reparam_fwd", mean.data_ptr(), logvar.data_ptr(), ldm, eps.data_ptr(), z.data_ptr(),
                       n * h * w, zc, _stream(mean))
         ctx.save_for_backward(logvar, eps)
         ctx.ld = ldl
@@ -1160,8 +1159,9 @@ class ReparamFn(torch.autograd.Function):
         dlv = None
         if ctx.needs_input_grad[1]:
             dlv = torch.empty((n, zc, h, w), device=dz.device, dtype=torch.float32, memory_format=CL)
-            _lib.call("mvae_reparam_bwd", dz.data_ptr(), eps.data_ptr(), logvar.data_ptr(), ctx.ld, dlv.data_ptr(),
-                      n * h * w, zc, _stream(dz))
+            with _timed("loss_bwd", 16.0 * dz.numel(), ("reparam", n * h * w, zc)):  # read dz, eps, logvar; write dlv
+                _lib.call("mvae_reparam_bwd", dz.data_ptr(), eps.data_ptr(), logvar.data_ptr(), ctx.ld, dlv.data_ptr(),
+                          n * h * w, zc, _stream(dz))
         return (dz if ctx.needs_input_grad[0] else None), dlv, None
 
 
@@ -1264,8 +1264,9 @@ class KLFn(torch.autograd.Function):
         out = torch.empty((), device=mean.device, dtype=torch.float32)
         ws = ARENA.get("red", _lib.query("mvae_reduce_workspace_bytes"), mean.device)
         scale = (1.0 / denom) if kind == 0 else (-0.5 / denom)
-        _lib.call("mvae_loss_reduce", kind, mean.data_ptr(), logvar.data_ptr(), ldm, n * h * w, zc, scale,
-                  out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(mean))
+        with _timed("loss_fwd", 8.0 * n * h * w * zc, ("kl", n * h * w, zc)):  # read mu, logvar
+            _lib.call("mvae_loss_reduce", kind, mean.data_ptr(), logvar.data_ptr(), ldm, n * h * w, zc, scale,
+                      out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(mean))
         ctx.save_for_backward(mean, logvar)
         ctx.ld, ctx.denom = ldm, denom
         return out
@@ -1277,8 +1278,9 @@ class KLFn(torch.autograd.Function):
         n, zc, h, w = mean.shape
         dmu = torch.empty((n, zc, h, w), device=mean.device, dtype=torch.float32, memory_format=CL)
         dlv = torch.empty_like(dmu, memory_format=CL)
-        _lib.call("mvae_kl_bwd", mean.data_ptr(), logvar.data_ptr(), ctx.ld, g.data_ptr(), 1.0 / ctx.denom,
-                  dmu.data_ptr(), dlv.data_ptr(), n * h * w, zc, _stream(mean))
+        with _timed("loss_bwd", 16.0 * dmu.numel(), ("kl", n * h * w, zc)):  # read mu, logvar; write dmu, dlogvar
+            _lib.call("mvae_kl_bwd", mean.data_ptr(), logvar.data_ptr(), ctx.ld, g.data_ptr(), 1.0 / ctx.denom,
+                      dmu.data_ptr(), dlv.data_ptr(), n * h * w, zc, _stream(mean))
         return dmu, dlv, None, None
 
 
@@ -1301,8 +1303,9 @@ class ReconFn(torch.autograd.Function):
         out = torch.empty((), device=a.device, dtype=torch.float32)
         ws = ARENA.get("red", _lib.query("mvae_reduce_workspace_bytes"), a.device)
         n = a.numel()
-        _lib.call("mvae_loss_reduce", kind, a.data_ptr(), b.data_ptr(), 1, n, 1, 1.0 / n, out.data_ptr(),
-                  ws.data_ptr(), ws.numel(), _stream(a))
+        with _timed("loss_fwd", 8.0 * n, ("recon", n)):  # read reconstruction, target
+            _lib.call("mvae_loss_reduce", kind, a.data_ptr(), b.data_ptr(), 1, n, 1, 1.0 / n, out.data_ptr(),
+                      ws.data_ptr(), ws.numel(), _stream(a))
         ctx.save_for_backward(a, b)
         ctx.kind = kind
         return out
@@ -1312,8 +1315,9 @@ class ReconFn(torch.autograd.Function):
         a, b = ctx.saved_tensors
         g = g.contiguous().float()
         da = torch.empty_like(a, memory_format=CL) if a.dim() == 4 else torch.empty_like(a)
-        _lib.call("mvae_recon_bwd", ctx.kind, a.data_ptr(), b.data_ptr(), g.data_ptr(), 1.0 / a.numel(),
-                  da.data_ptr(), a.numel(), _stream(a))
+        with _timed("loss_bwd", 12.0 * a.numel(), ("recon", a.numel())):  # read reconstruction, target; write da
+            _lib.call("mvae_recon_bwd", ctx.kind, a.data_ptr(), b.data_ptr(), g.data_ptr(), 1.0 / a.numel(),
+                      da.data_ptr(), a.numel(), _stream(a))
         return da, None, None
 
 

@@ -163,3 +163,48 @@ def test_state_dict_roundtrip_and_names():
     assert list(sd) == [k for k, _ in meta["params"]]
     for k in sd:
         assert torch.equal(sd[k], ref[k]), k
+
+
+@pytest.mark.parametrize("name", ["cvae_c4_full", "beta_c2_full", "dis_c3_b16"])
+def test_training_step_exact_fp32_matches_reference(name):
+    """The trainer's "32-exact" precision (every conv / bmm on the f32-input MFMA, no operand rounding -- the
+    arithmetic of the bench's c4x line) against the reference at the exact BASELINE architectures: outputs, loss
+    terms, the global gradient norm and the selected full gradients, 1e-4 relative (only the summation order
+    differs from the reference's CPU fp32)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import medvae_disentangled_multimodal_amd as M
+    from medvae_disentangled_multimodal_amd import ops
+    dev = torch.device("cuda:0")
+    meta, data = load_case(name)
+    case = CASES[name]
+    model = getattr(M, case["cls"])(**case["kwargs"])
+    model.load_state_dict(golden_state(meta))
+    model = model.to(dev)
+    mod = M.VAELightningModule(model, case["optimizer"], {"type": "none"}, case["loss"],
+                               gradient_clip_val=case["clip"], precision="32-exact")
+    mod.configure_optimizers()
+    prev = ops.set_precision("32-exact")
+    try:
+        mod.optimizer.zero_grad()
+        loss = mod.training_step(_batch(case, data, dev), 0, eps=torch.from_numpy(data["in.eps"]).to(dev))
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        ops.restore_math_mode(prev)
+    tol = 1e-4
+    out = mod._last_outputs
+    for k in ("reconstruction", "mean", "logvar", "z"):
+        assert rel_err(out[k].detach().cpu(), data[f"out.{k}"]) < tol, (k, rel_err(out[k].detach().cpu(),
+                                                                                    data[f"out.{k}"]))
+    for k in ("recon_loss", "kl_loss"):
+        ref = float(data[f"loss.{k}"])
+        assert abs(float(mod.logged[f"train/{k}"]) - ref) <= tol * abs(ref), k
+    names = mod.flat.names
+    has = [k for k, v in meta["param_has_grad"].items() if v]
+    exact = math.sqrt(sum(float(data[f"gradsum.{k}"][1]) for k in has))
+    got = math.sqrt(sum(float((mod.flat.params[names.index(k)]._mvae_main_grad.double() ** 2).sum()) for k in has))
+    assert abs(got - exact) <= tol * exact, (got, exact)
+    for k in FULL_GRADS[name]:
+        g = mod.flat.params[names.index(k)]._mvae_main_grad.cpu()
+        assert rel_err(g, data[f"grad.{k}"]) < 10 * tol, (k, rel_err(g, data[f"grad.{k}"]))

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""bf16-mixed conv passes (LDS-DMA path) at c5 layer shapes, timed by the per-launch HIP events of ops._timed:
-TF/s per pass (fwd / dgrad / wgrad). Used to A/B main-loop variants (MVAE_HIP_LIB=variants/<v>/libmvae_hip.so)."""
+"""Conv passes at c4 / c5 layer shapes through the model's autograd path, timed by the per-launch HIP events of
+ops._timed: TF/s per pass (fwd / dgrad / wgrad). tools/dma_exp.py [precision: bf16-mixed (default, the LDS-DMA loop)
+| 32 (3xBF16)]. Used to A/B main-loop variants (MVAE_HIP_LIB=variants/<v>/libmvae_hip.so)."""
 import json, math, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -11,7 +12,8 @@ SHAPES = [(256, 2048, 2048, 8), (256, 1024, 1024, 16), (256, 256, 256, 64)]
 
 def main():
     dev = torch.device("cuda:0")
-    ops.set_precision("bf16-mixed")
+    prec = sys.argv[1] if len(sys.argv) > 1 else "bf16-mixed"
+    ops.set_precision(prec)
     out = {}
     for n, ci, co, h in SHAPES:
         g = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1)
@@ -32,7 +34,7 @@ def main():
         out[f"{ci}x{h}"] = res
         del x, w, dy, y
         torch.cuda.empty_cache()
-    print(os.environ.get("MVAE_HIP_LIB", "default"), json.dumps(out), flush=True)
+    print(os.environ.get("MVAE_HIP_LIB", "default"), prec, json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

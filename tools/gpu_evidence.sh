@@ -9,13 +9,17 @@
 #   tools/gpu_evidence.sh perstep  <tag> <config> [S1 S2]         per-step rocprofv3 kernel table: two --kernel-trace
 #                                                                 --stats runs differing in timed steps, differenced
 #                                                                 by tools/prof_diff.py (set-up / warmup cancel)
-#   tools/gpu_evidence.sh traffic  <tag> <config> [family]        HBM bytes of a kernel family (regex, default gemm3x)
+#   tools/gpu_evidence.sh traffic  <tag> <config> [family]        HBM bytes of a kernel family (gemm | gn | loss)
 #                                                                 over one step: FETCH_SIZE and WRITE_SIZE in separate
 #                                                                 --pmc passes, gfx950 correction in pmc_traffic.py
 #   tools/gpu_evidence.sh pmc      <tag> <shape> <pass> <prec>    conv counter sets (MFMA busy, waits, VALU / SALU /
 #                                                                 LDS issue) of one tools/conv_bench.py shape + pass
 #   tools/gpu_evidence.sh ab       <tag> <config> <variant...>    interleaved A/B of library builds variants/<v>/
 #                                                                 (tools/build_variant.sh) on one bench config
+#   tools/gpu_evidence.sh loops    <tag> <variant...>              interleaved A/B of library builds on the GEMM main
+#                                                                 loops: tools/loop_bench.py (plain 4k GEMM + c4 3x3
+#                                                                 layers) and tools/dma_exp.py (per-pass conv), both
+#                                                                 arithmetics ("default" = the in-tree library)
 #   tools/gpu_evidence.sh final    <tag>                          round-end set: suite + smoke, default bench line,
 #                                                                 per-step tables of c3 and c4
 set -o pipefail
@@ -64,9 +68,11 @@ perstep() {
 }
 
 traffic() {
-  local cfg=$1 fam=${2:-gemm3x}
+  local cfg=$1 fam=${2:-gemm} re
+  case $fam in gemm) re=gemm3x;; gn) re=gn_;; loss) re="reparam_|reduce_partial|reduce_final|kl_bwd|recon_bwd";;
+    *) echo "family: gemm | gn | loss"; return 2;; esac
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 400 rocprofv3 --pmc $c --kernel-include-regex "$fam" -d gpurun_out/traffic_${cfg}_${fam}_$c -o run \
+    timeout -s KILL 400 rocprofv3 --pmc $c --kernel-include-regex "$re" -d gpurun_out/traffic_${cfg}_${fam}_$c -o run \
       --output-format csv -- python3 bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline \
       --no-kernel-timing --no-parity > $OUT/traffic_${cfg}_${fam}_$c.log 2>&1 || return $?
   done
@@ -102,6 +108,20 @@ ab() {
   done
 }
 
+loops() {
+  for r in 1 2; do
+    for v in "$@"; do
+      local lib=variants/$v/libmvae_hip.so
+      [ "$v" = default ] && lib=medvae_disentangled_multimodal_amd/libmvae_hip.so
+      for p in bf16-mixed 32; do
+        MVAE_HIP_LIB=$lib timeout -k 10 200 python -u tools/loop_bench.py $p >> $OUT/loops.txt 2>> $OUT/loops.err || return $?
+        MVAE_HIP_LIB=$lib timeout -k 10 200 python -u tools/dma_exp.py $p >> $OUT/loops.txt 2>> $OUT/loops.err || return $?
+      done
+    done
+  done
+  cat $OUT/loops.txt
+}
+
 case $CMD in
   suite) suite "$@" ;;
   bench) bench "$@" ;;
@@ -109,6 +129,7 @@ case $CMD in
   traffic) traffic "$@" ;;
   pmc) pmc "$@" ;;
   ab) ab "$@" ;;
+  loops) loops "$@" ;;
   final) suite && bench && perstep c3 && perstep c4 ;;
   *) echo "unknown subcommand $CMD"; exit 2 ;;
 esac

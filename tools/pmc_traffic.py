@@ -1,22 +1,25 @@
 #!/usr/bin/env python3
-"""Per-launch HBM bytes of a kernel family (gemm3x_kernel, or the gn_* GroupNorm chains) from the FETCH_SIZE /
+"""Per-launch HBM bytes of a kernel family (gemm: gemm3x_kernel; gn: the gn_* GroupNorm chains; loss: the
+reparameterization / KL / reconstruction kernels) from the FETCH_SIZE /
 WRITE_SIZE passes of tools/gpu_evidence.sh traffic.
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts 64 B per 128-B request of
 wide streaming reads -> x2; WRITE_SIZE is exact for 16-B/lane stores. Both are reported in KB."""
-import csv, glob, json, os, sys
+import csv, glob, json, os, re, sys
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c4"
 tag = sys.argv[2] if len(sys.argv) > 2 else "r02"
-fam = sys.argv[3] if len(sys.argv) > 3 else "gemm3x"
+short = sys.argv[3] if len(sys.argv) > 3 else "gemm"  # family: gemm | gn | loss
+FAMILY_RE = {"gemm": "gemm3x", "gn": "gn_", "loss": "reparam_|reduce_partial|reduce_final|kl_bwd|recon_bwd"}
+fam = FAMILY_RE[short]
 root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 
 
 def per_dispatch(counter):
     vals = {}
-    for f in glob.glob(os.path.join(root, f"gpurun_out/traffic_{cfg}_{fam}_{counter}", "**", "*counter_collection.csv"),
+    for f in glob.glob(os.path.join(root, f"gpurun_out/traffic_{cfg}_{short}_{counter}", "**", "*counter_collection.csv"),
                        recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] == counter and fam in r["Kernel_Name"]:
+            if r["Counter_Name"] == counter and re.search(fam, r["Kernel_Name"]):
                 vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return vals
 
@@ -25,11 +28,12 @@ fetch, write = per_dispatch("FETCH_SIZE"), per_dispatch("WRITE_SIZE")
 n = len(fetch)
 fb = 2.0 * 1024 * sum(fetch.values()) / max(n, 1)
 wb = 1024 * sum(write.values()) / max(len(write), 1)
-out = {"config": cfg, "kernel": "gemm3x_kernel" if fam == "gemm3x" else fam + "* (GroupNorm chains)", "launches": n, "fetch_bytes_per_launch": fb,
+kname = {"gemm": "gemm3x_kernel", "gn": "gn_* (GroupNorm chains)"}.get(short, f"loss family ({fam})")
+out = {"config": cfg, "kernel": kname, "launches": n, "fetch_bytes_per_launch": fb,
        "write_bytes_per_launch": wb, "traffic_bytes_per_launch": fb + wb,
        "traffic_bytes_total": 2.0 * 1024 * sum(fetch.values()) + 1024 * sum(write.values()), "steps": 1,
        "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, kernel-trace only) over one "
                  "training step; FETCH_SIZE x2 (gfx950 wide-read correction), KB -> bytes"}
-dst = os.path.join(root, "profiles", f"{tag}_{cfg}_{'gemm' if fam == 'gemm3x' else 'gn'}_traffic.json")
+dst = os.path.join(root, "profiles", f"{tag}_{cfg}_{short}_traffic.json")
 json.dump(out, open(dst, "w"), indent=1)
 print(json.dumps(out))
