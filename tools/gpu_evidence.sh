@@ -111,11 +111,14 @@ ab() {
 loops() {
   for r in 1 2; do
     for v in "$@"; do
-      local lib=variants/$v/libmvae_hip.so
+      local lib=variants/$v/libmvae_hip.so envs=()
       [ "$v" = default ] && lib=medvae_disentangled_multimodal_amd/libmvae_hip.so
-      for p in bf16-mixed 32; do
-        MVAE_HIP_LIB=$lib timeout -k 10 200 python -u tools/loop_bench.py $p >> $OUT/loops.txt 2>> $OUT/loops.err || return $?
-        MVAE_HIP_LIB=$lib timeout -k 10 200 python -u tools/dma_exp.py $p >> $OUT/loops.txt 2>> $OUT/loops.err || return $?
+      # "env:VAR=VAL[,VAR=VAL]": the in-tree library under those environment settings
+      if [[ $v == env:* ]]; then lib=medvae_disentangled_multimodal_amd/libmvae_hip.so; IFS=, read -ra envs <<< "${v#env:}"; fi
+      for p in ${PRECS:-bf16-mixed 32}; do
+        echo "== $v $p" >> $OUT/loops.txt
+        env "${envs[@]}" MVAE_HIP_LIB=$lib timeout -k 10 200 python -u tools/loop_bench.py $p >> $OUT/loops.txt 2>> $OUT/loops.err || return $?
+        env "${envs[@]}" MVAE_HIP_LIB=$lib timeout -k 10 200 python -u tools/dma_exp.py $p >> $OUT/loops.txt 2>> $OUT/loops.err || return $?
       done
     done
   done
