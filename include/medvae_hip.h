@@ -41,10 +41,6 @@ int mvae_get_math_mode(void);
  * mask (ResnetBlock nn.Dropout, encoder_decoder.py:163). Lets a captured HIP graph of a training step draw fresh
  * masks per replay: the graph advances the salt on the device; the frozen per-launch seeds stay valid. */
 int mvae_set_dropout_salt(const void* salt_dev);
-/* bf16-mixed GEMMs with 256x256 tiles on the ping-pong LDS-DMA main loop (1: two wave groups one barrier apart over a
- * 4-stage ring of 32-deep stages) or the two-stage loop (0); -1 restores the default (environment MVAE_PINGPONG, then
- * the build default). Same products, same fp32 accumulation order per k-step. Returns the previous setting. */
-int mvae_set_dma_pingpong(int on);
 
 /* ---- convolutions (implicit GEMM on MFMA, 3xBF16 split arithmetic, fp32 accumulate) ------------
  * Replaces nn.Conv2d forward in ResnetBlock/AttnBlock/Encoder/Decoder

@@ -26,7 +26,6 @@ SIGNATURES = {
     "mvae_set_math_mode": (I, [I]),
     "mvae_get_math_mode": (I, []),
     "mvae_set_dropout_salt": (I, [P]),
-    "mvae_set_dma_pingpong": (I, [I]),
     "mvae_conv2d_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P]),
     "mvae_conv2d_ws_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),
     "mvae_conv2d_split_workspace_bytes": (Z, [I, I, I, I, I, I, I]),

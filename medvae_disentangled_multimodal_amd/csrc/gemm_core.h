@@ -772,10 +772,7 @@ struct LoadWgradX {
 // 20-27}, {4-11,16-19,28-31}, ... then hit 16 distinct 16-B bank windows: 128-B rows use (r >> 1) & 7, 64-B rows
 // [0,3,2,1][(r >> 2) & 3]).
 // ------------------------------------------------------------------------------------------
-constexpr int DBK = 64;  // split-K granularity (whole stages of every DMA loop)
-#ifndef MVAE_PINGPONG_DEFAULT
-#define MVAE_PINGPONG_DEFAULT 0
-#endif
+constexpr int DBK = 64;  // split-K granularity (whole stages of either loop)
 #ifndef MVAE_DMA_SPREAD  // 1: COL (weight-gradient) loops spread their DMA issue over the k-steps; 2: every loop
 #define MVAE_DMA_SPREAD 1
 #endif
@@ -792,9 +789,6 @@ __device__ __forceinline__ int kperm_dma(const GemmArgs& a, int k) {
 }
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, __bf16* dst, unsigned off) {
-#ifdef MVAE_DMA_L1  // (timing experiment: every DMA reads inside one 4 KB window -- cache-resident, wrong results)
-  off &= 0xFF0u;
-#endif
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)dst, 16, off, 0, 0, 0);
 }
 
@@ -1165,13 +1159,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int MF = mf_of(AK), KS = ks_of<MF>(), NR = nr_of<MF>();
   using acc_t = acc_of<MF>;
-  constexpr int LP = (PREC == 4 || PREC == 6) ? 1 : PREC == 5 ? 3 : PREC;  // arithmetic of the register-staged loaders
+  constexpr int LP = PREC == 4 ? 1 : PREC == 5 ? 3 : PREC;  // arithmetic of the register-staged loaders
   using LA = Loader<AK, BM, VA, NT, true, LP>;
   using LB = Loader<BKIND, BN, VB, NT, false, LP>;
   using IA = Img<BM, LA::COL>;
   using IB = Img<BN, LB::COL>;
   constexpr int BUF = IA::SIZE + IB::SIZE;
-  constexpr int DBUF = (PREC == 5 ? 2 : 1) * (BM + BN) * (PREC == 5 ? 32 : 64);  // PREC 4/5/6: one DMA stage
+  constexpr int DBUF = (PREC == 5 ? 2 : 1) * (BM + BN) * (PREC == 5 ? 32 : 64);  // PREC 4/5: one DMA stage
   constexpr int TM = BM / WGM / MF, TN = BN / WGN / MF;  // MFMA tiles per wave
   __shared__ __attribute__((aligned(16))) __bf16 lds[(PREC >= 4 && 2 * DBUF > 2 * BUF) ? 2 * DBUF : 2 * BUF];
 
@@ -1206,127 +1200,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
       for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
   const int arow = wm * (BM / WGM), brow = wn * (BN / WGN);
 
-  if constexpr (PREC == 6) {
-    // Ping-pong main loop on bf16 operands (256x256 tiles on 8 waves), register-staged. Waves 0-3 (group 0) and 4-7
-    // (group 1) share the four SIMDs pairwise and run ONE BARRIER APART: a 64-deep stage is four phases per wave --
-    // (k-group kg, half h of the wave tile) -- each an R section (the phase's fragment reads + a share of the staging)
-    // and an M section (its MFMA cluster, 256 cycles), barrier-separated; group 1 enters the loop one barrier late, so in
-    // every section one wave of each SIMD issues a dense MFMA cluster while its partner reads fragments and stages.
-    // Staging: the LDS images and per-lane source offsets of the LDS-DMA loaders (lane-linear 1-KB pieces, swizzled on
-    // the source side), but through registers -- buffer_load_dwordx4 into VGPRs, ds_write_b128 -- because an LDS-DMA
-    // piece costs its wave 60-185 cycles of issue (MI355X_MICROARCH.md constants), which no partner MFMA cluster
-    // hides at 8 pieces per 64-deep stage. Two LDS stages (2 x 64 KB, 128-B source rows): stage t+2 is loaded into the
-    // registers in phase 3 of stage t, written into the slot of stage t (free: every wave retired its reads of t before
-    // the barrier that ends group 1's last M section of t) in phases 1-2 of stage t+1, and read in stage t+2.
-    // (cdna_hip_programming.md section 5: the 8-phase template's ping-pong structure)
-    static_assert(BM == 256 && BN == 256 && WGM == 2 && WGN == 4, "ping-pong loop: 256x256 tiles on 8 waves");
-    constexpr int KT = 64, NSTG = 2;
-    constexpr bool ACOL = AK == A_COLM, BCOL = BKIND == B_WGRAD_FWD || BKIND == B_WGRAD_SUBPIX;
-    static_assert(ACOL == BCOL && MF == (ACOL ? 32 : 16), "ping-pong loop: ROW x ROW (MF 16) or COL x COL (MF 32)");
-    using DA = DmaLoader<AK == A_ROWK ? 0 : AK, BM, NT, true, KT>;
-    using DB = DmaLoader<BKIND == B_ROWK ? 0 : BKIND, BN, NT, false, KT>;
-    constexpr int PA = BM * KT, PB = BN * KT, SBUF = PA + PB;
-    static_assert(NSTG * SBUF * 2 <= 163840, "ping-pong stages exceed the LDS");
-    constexpr int NA = DA::S::NI, NID = DA::S::NI + DB::S::NI;  // 16-B pieces per thread per stage
-    static_assert(NID % 2 == 0, "staging writes split over two R sections");
-    DA da;
-    DB db;
-    da.init(a, (const __bf16*)a.A + bidx * a.sA, m0, kb, tid, bidx);
-    db.init(a, (const __bf16*)a.B + bidx * a.sB, n0, kb, tid, bidx);
-    const int nt = ke > kb ? (ke - kb + KT - 1) / KT : 0;
-    const bool g1 = __builtin_amdgcn_readfirstlane(wid) >= 4;  // wave-uniform: the late group
-    u32x4_t stg[NID];
-    auto load_stage = [&]() {  // the current loader k-range into the staging registers, then advance
-      da.prep(a);
-      db.prep(a);
-#pragma unroll
-      for (int q = 0; q < NID; ++q)
-        stg[q] = q < NA ? __builtin_amdgcn_raw_buffer_load_b128(da.rs[0], da.src(q), 0, 0)
-                        : __builtin_amdgcn_raw_buffer_load_b128(db.rs[0], db.src(q - NA), 0, 0);
-      da.advance();
-      db.advance();
-    };
-    auto write_q = [&](int stage, int q) {  // piece q of the staging registers -> its lane-linear LDS slot
-      __bf16* sp = lds + (stage % NSTG) * SBUF + (q < NA ? 0 : PA);
-      const int i = q < NA ? q : q - NA;
-      constexpr int NW = NT / 64;
-      *(u32x4_t*)(sp + (i * NW + wid) * 512 + lane * 8) = stg[q];
-    };
-    auto bar = [&]() {
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    // prologue: stage 0 in the LDS, stage 1 in the registers (in flight), group 1 one barrier behind
-    if (nt > 0) {
-      load_stage();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int q = 0; q < NID; ++q) write_q(0, q);
-    }
-    if (nt > 1) load_stage();
-    wait_lgkm<0>();
-    bar();
-#ifndef MVAE_PP_NOSTAG  // (timing experiment: both groups in step)
-    if (g1) bar();
-#endif
-    constexpr int TH = TM / 2;                      // A fragments per half of the wave tile
-    constexpr int KSS = KT / (MF == 32 ? 16 : 32);  // MFMA k-steps per stage
-    constexpr int KG = KSS / 2;                     // k-steps per phase
-    bf16x8 fb[TN][KG], fa[TH][KG];
-    for (int t = 0; t < nt; ++t) {
-      const __bf16* Ai = lds + (t % NSTG) * SBUF;
-      const __bf16* Bi = Ai + PA;
-      const bool wr = t + 1 < nt, ld = t + 2 < nt;
-#pragma unroll
-      for (int ph = 0; ph < 4; ++ph) {
-        const int kg = ph >> 1, h = ph & 1;
-        // ---- R section: this phase's fragment reads (B once per k-group) + its share of the staging
-#pragma unroll
-        for (int kk = 0; kk < KG; ++kk) {
-          const int ks = kg * KG + kk;
-          if (h == 0) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              if constexpr (BCOL) fb[j][kk] = dcfrag_asm<BN>(Bi, brow + j * MF, ks, lane);
-              else fb[j][kk] = dfrag_asm<KT>(Bi, brow + j * MF, ks, lane);
-            }
-          }
-#pragma unroll
-          for (int i = 0; i < TH; ++i) {
-            if constexpr (ACOL) fa[i][kk] = dcfrag_asm<BM>(Ai, arow + (h * TH + i) * MF, ks, lane);
-            else fa[i][kk] = dfrag_asm<KT>(Ai, arow + (h * TH + i) * MF, ks, lane);
-          }
-        }
-        if (wr && (ph == 1 || ph == 2)) {  // stage t+1 (registers) -> the slot of stage t-1
-          if (ph == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NID / 2) : "memory");
-          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-          for (int q = (ph - 1) * (NID / 2); q < ph * (NID / 2); ++q) write_q(t + 1, q);
-        }
-        if (ld && ph == 3) load_stage();  // stage t+2 -> registers
-        bar();
-        // ---- M section: the MFMA cluster of this phase
-        wait_lgkm<0>();
-#ifndef MVAE_PP_NOPRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
-#pragma unroll
-        for (int kk = 0; kk < KG; ++kk)
-#pragma unroll
-          for (int i = 0; i < TH; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[h * TH + i][j] = mfma_bf16(fa[i][kk], fb[j][kk], acc[h * TH + i][j]);
-#ifndef MVAE_PP_NOPRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
-        bar();
-      }
-    }
-#ifndef MVAE_PP_NOSTAG
-    if (!g1) bar();  // group 0 takes the barrier group 1 took up front: both leave the loop in step
-#endif
-  } else if constexpr (PREC >= 4) {
+  if constexpr (PREC >= 4) {
     // LDS-DMA main loop, two stages: at the top of iteration t each wave waits for its own DMA of stage t (vmcnt 0),
     // the barrier makes every wave's DMA of stage t visible and guarantees that every wave has finished reading stage
     // t-1, then the DMA of stage t+1 is issued into that slot and stage t is multiplied: the DMA has one phase to
@@ -2037,18 +1911,11 @@ void launch_big(GemmArgs& a, hipStream_t st, int cfg) {
   }
 }
 
-// bf16 256x256 tiles on the ping-pong LDS-DMA loop (PREC 6) instead of the two-stage loop (PREC 4): the build default,
-// MVAE_PINGPONG=0 / 1 in the environment, or mvae_set_dma_pingpong (gemm_dma.hip)
-bool dma_pingpong();
-
 // DMA-staged operands (MVAE_CONV_BF16: PREC 4, MVAE_CONV_PLANAR: PREC 5): every tile config on the LDS-DMA main loop
 template <int AK, int P>
 void launch_dma(GemmArgs& a, hipStream_t st, int cfg) {
   switch (cfg) {
-    case T256x256:
-      if (P == 4 && dma_pingpong()) launch_cfg<T256x256, AK, 4, B_ROWK, 4, 6>(a, st);
-      else launch_cfg<T256x256, AK, 4, B_ROWK, 4, P>(a, st);
-      break;
+    case T256x256: launch_cfg<T256x256, AK, 4, B_ROWK, 4, P>(a, st); break;
     case T256x128: launch_cfg<T256x128, AK, 4, B_ROWK, 4, P>(a, st); break;
     case T128x256: launch_cfg<T128x256, AK, 4, B_ROWK, 4, P>(a, st); break;
     case T128x128: launch_cfg<T128x128, AK, 4, B_ROWK, 4, P>(a, st); break;

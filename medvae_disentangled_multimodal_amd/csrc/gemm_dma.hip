@@ -5,16 +5,6 @@
 
 namespace mvae {
 
-static int g_pingpong = -1;  // -1: not yet read (environment, then the build default)
-
-bool dma_pingpong() {
-  if (g_pingpong < 0) {
-    const char* e = getenv("MVAE_PINGPONG");
-    g_pingpong = e ? (atoi(e) != 0) : MVAE_PINGPONG_DEFAULT;
-  }
-  return g_pingpong != 0;
-}
-
 template <int P>
 static void conv_dma_p(int ak, GemmArgs& a, hipStream_t st, int cfg) {
   switch (ak) {
@@ -33,10 +23,7 @@ void conv_dma(int ak, GemmArgs& a, hipStream_t st, int cfg, int prec) {
 template <int BKIND, int P>
 static void wgrad_dma_cfg(GemmArgs& a, hipStream_t st, int cfg) {
   switch (cfg) {
-    case T256x256:
-      if (P == 4 && dma_pingpong()) launch_cfg<T256x256, A_COLM, 4, BKIND, 4, 6>(a, st);
-      else launch_cfg<T256x256, A_COLM, 4, BKIND, 4, P>(a, st);
-      break;
+    case T256x256: launch_cfg<T256x256, A_COLM, 4, BKIND, 4, P>(a, st); break;
     case T256x128: launch_cfg<T256x128, A_COLM, 4, BKIND, 4, P>(a, st); break;
     case T128x256: launch_cfg<T128x256, A_COLM, 4, BKIND, 4, P>(a, st); break;
     case T128x128: launch_cfg<T128x128, A_COLM, 4, BKIND, 4, P>(a, st); break;
@@ -56,12 +43,3 @@ void wgrad_dma(int bkind, GemmArgs& a, hipStream_t st, int cfg, int prec) {
 
 }  // namespace mvae
 
-extern "C" {
-// bf16 256x256 DMA GEMMs on the ping-pong loop (1) or the two-stage loop (0); -1 restores the environment / build
-// default. Returns the previous setting.
-int mvae_set_dma_pingpong(int on) {
-  const int prev = mvae::dma_pingpong();
-  mvae::g_pingpong = on < 0 ? -1 : (on != 0);
-  return prev;
-}
-}

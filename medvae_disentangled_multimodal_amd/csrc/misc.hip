@@ -237,17 +237,30 @@ __global__ void __launch_bounds__(256) pack_colsum_kernel(const float* __restric
   const long long r1 = std::min<long long>(rows, r0 + rows_per_chunk);
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   if (c < n) {
-    for (long long r = r0 + rg; r < r1; r += 4) {
-      const float4 v = *(const float4*)(x + r * n + c);
-      if constexpr (PLANAR) {  // hi plane, then the lo plane rows * n elements later
-        uint2 h, l;
-        planar4(v, h, l);
-        y[(r * n + c) >> 2] = h;
-        y[((rows * n) >> 2) + ((r * n + c) >> 2)] = l;
-      } else {
-        y[(r * n + c) >> 2] = uint2{pk_bf16x2(v.x, v.y), pk_bf16x2(v.z, v.w)};
+    // PU rows in flight per thread (the loads of a batch issue together; one 16-B load per iteration left the kernel
+    // latency-bound at ~1 TB/s), summed in row order: the same fp64 sums as a row-at-a-time walk (masked rows add 0)
+    constexpr int PU = 8;
+    for (long long r = r0 + rg; r < r1; r += 4 * PU) {
+      float4 v[PU];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const long long rr = r + 4 * u;
+        v[u] = rr < r1 ? *(const float4*)(x + rr * n + c) : float4{0.f, 0.f, 0.f, 0.f};
       }
-      a0 += v.x; a1 += v.y; a2 += v.z; a3 += v.w;
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const long long rr = r + 4 * u;
+        if (rr >= r1) break;
+        if constexpr (PLANAR) {  // hi plane, then the lo plane rows * n elements later
+          uint2 h, l;
+          planar4(v[u], h, l);
+          y[(rr * n + c) >> 2] = h;
+          y[((rows * n) >> 2) + ((rr * n + c) >> 2)] = l;
+        } else {
+          y[(rr * n + c) >> 2] = uint2{pk_bf16x2(v[u].x, v[u].y), pk_bf16x2(v[u].z, v[u].w)};
+        }
+        a0 += v[u].x; a1 += v[u].y; a2 += v[u].z; a3 += v[u].w;
+      }
     }
   }
   sh[rg][threadIdx.x & 63][0] = a0;
@@ -273,8 +286,16 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const float* __rest
   const long long r0 = (long long)blockIdx.y * rows_per_chunk;
   const long long r1 = std::min<long long>(rows, r0 + rows_per_chunk);
   double acc = 0;
-  if (col < n)
-    for (long long r = r0 + rg; r < r1; r += 4) acc += x[r * ld + col];
+  if (col < n) {
+    constexpr int PU = 8;  // rows in flight per thread, summed in row order
+    for (long long r = r0 + rg; r < r1; r += 4 * PU) {
+      float v[PU];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) v[u] = r + 4 * u < r1 ? x[(r + 4 * u) * ld + col] : 0.f;
+#pragma unroll
+      for (int u = 0; u < PU; ++u) acc += v[u];
+    }
+  }
   sh[threadIdx.x] = acc;
   __syncthreads();
   if (rg == 0 && col < n) part[(long long)blockIdx.y * n + col] = sh[threadIdx.x] + sh[threadIdx.x + 64] +
@@ -285,7 +306,15 @@ __global__ void colsum_final_kernel(const double* __restrict__ part, int chunks,
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
   if (col >= n) return;
   double s = 0;
-  for (int c = 0; c < chunks; ++c) s += part[(long long)c * n + col];
+  int c = 0;
+  for (; c + 16 <= chunks; c += 16) {  // 16 partial loads in flight, summed in chunk order
+    double v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = part[(long long)(c + j) * n + col];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += v[j];
+  }
+  for (; c < chunks; ++c) s += part[(long long)c * n + col];
   out[col] = (beta != 0.f ? beta * out[col] : 0.f) + (float)s;
 }
 

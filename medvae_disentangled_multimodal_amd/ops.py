@@ -405,12 +405,6 @@ def release_weight_buffers():
     _WT.tbase = _WT.tend = 0
 
 
-def set_dma_pingpong(on: int) -> int:
-    """bf16-mixed 256x256 GEMMs on the ping-pong LDS-DMA loop (1) or the two-stage loop (0); -1 = default. Returns
-    the previous setting (mvae_set_dma_pingpong)."""
-    return int(_lib.query("mvae_set_dma_pingpong", int(on)))
-
-
 def flat_weights_stale():
     _FLATW.fresh = False
     _WT.fresh = False

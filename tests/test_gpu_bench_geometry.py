@@ -8,10 +8,10 @@ the bench batch in the default fp32-class (3xBF16) arithmetic -- forward, input 
 the same ops.conv2d autograd path the model uses -- and are checked against float64 on a sampled subset: output rows
 (pixels x all channels), input-gradient rows, and weight-gradient columns (output channels x all taps / inputs).
 Tolerance 2e-4 relative per sampled block (the CONV_TOL of tests/test_gpu_kernels.py).
-The two deepest layers also run in the bf16-mixed arithmetic (config 5; every pass on packed bf16 operands through the
-LDS-DMA GEMM main loops, the ping-pong loop for 256x256 tiles and the two-stage loop): the float64 reference then uses
-the bf16-rounded operands of each GEMM, so only fp32 accumulation differs -- tolerance 1e-4 (sqrt(K) * 2^-24 for K =
-18,432 is ~8e-6)."""
+The two deepest layers (and a 64 x 32x32 x 256 layer with its stride-2 Downsample, 256 tiles of 256x256) also run in the
+bf16-mixed arithmetic (config 5; every pass on packed bf16 operands through the LDS-DMA GEMM main loop): the float64
+reference then uses the bf16-rounded operands of each GEMM, so only fp32 accumulation differs -- tolerance 1e-4
+(sqrt(K) * 2^-24 for K = 18,432 is ~8e-6)."""
 import math
 
 import pytest
@@ -30,12 +30,11 @@ C2 = [(256, 512, 512, 7, 7, 3, 1, (1, 1, 1, 1), False), (256, 512, 512, 7, 7, 1,
 C3 = [(512, 32, 32, 28, 28, 3, 1, (1, 1, 1, 1), False), (512, 64, 64, 14, 14, 3, 1, (1, 1, 1, 1), False),
       (512, 128, 128, 7, 7, 3, 1, (1, 1, 1, 1), False), (512, 128, 128, 7, 7, 1, 1, (0, 0, 0, 0), False),
       (512, 32, 32, 28, 28, 3, 2, (0, 0, 1, 1), False), (512, 64, 64, 14, 14, 3, 1, (1, 1, 1, 1), True)]
-# bf16-mixed GEMMs with 256x256 tiles on the ping-pong LDS-DMA loop (ops.set_dma_pingpong(1), "c5pp") and on the
-# two-stage loop ("c5tw"): the c4 / c5 layers above plus a 64 x 32x32 x 256 layer (fwd M = 65,536: 256 tiles of 256x256)
-# and its stride-2 Downsample
-PP = C4[:2] + [(64, 256, 256, 32, 32, 3, 1, (1, 1, 1, 1), False), (64, 256, 256, 64, 64, 3, 2, (0, 0, 1, 1), False)]
-LAYERS = [("c4", l, "32") for l in C4] + [("c5pp", l, "bf16-mixed") for l in PP] + \
-    [("c5tw", l, "bf16-mixed") for l in PP[:2]] + [("c2", l, "32") for l in C2] + [("c3", l, "32") for l in C3]
+# bf16-mixed (config 5): the c4 layers above plus a 64 x 32x32 x 256 layer (fwd M = 65,536: 256 tiles of 256x256) and
+# its stride-2 Downsample, every pass on the LDS-DMA main loop
+C5 = C4[:2] + [(64, 256, 256, 32, 32, 3, 1, (1, 1, 1, 1), False), (64, 256, 256, 64, 64, 3, 2, (0, 0, 1, 1), False)]
+LAYERS = [("c4", l, "32") for l in C4] + [("c5", l, "bf16-mixed") for l in C5] + \
+    [("c2", l, "32") for l in C2] + [("c3", l, "32") for l in C3]
 
 
 @pytest.fixture(scope="module")
@@ -81,14 +80,12 @@ def test_hot_conv_at_bench_batch(dev, cfg, layer, prec):
     bd = b.to(dev).requires_grad_()
     dy = torch.randn(n, co, ho, wo, generator=g)
     prev = ops.set_precision(prec)
-    pp = ops.set_dma_pingpong({"c5pp": 1, "c5tw": 0}.get(cfg, -1))
     try:
         y = ops.conv2d(xd, wd, bd, geom)
         y.backward(dy.to(dev).contiguous(memory_format=torch.channels_last))
         torch.cuda.synchronize()
     finally:
         ops.restore_math_mode(prev)
-        ops.set_dma_pingpong(pp)
     assert ops._lib.query("mvae_get_math_mode") == 0
     assert tuple(y.shape) == (n, co, ho, wo)
 
