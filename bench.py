@@ -373,8 +373,11 @@ def run_config(name, args, rank, world, dev, want_cpu=True, steps=None, warmup=N
     batches = [make_batch(cfg, dev, gen) for _ in range(2)]
 
     # the small configs (c1-c3: ~800 launches of a few microseconds per step) replay the whole step as one captured
-    # HIP graph -- same kernels and arithmetic, the host issues one launch per step; eager for c4 / c5 and N > 1
-    graphed = cfg.get("graph", False) and world == 1 and not args.eager
+    # HIP graph -- same kernels and arithmetic, the host issues one launch per step (N > 1: the graph holds the
+    # bucketed RCCL all-reduces too, or two graphs around an eager exchange on other backends); eager for c4 / c5
+    graphed = cfg.get("graph", False) and not args.eager
+    launch = ("hip graph (captured step" + ("" if world == 1 else f", dp capture {mod._dp_capture_mode()}") + ")"
+              if graphed else "eager")
     step = mod.fit_step_graphed if graphed else mod.fit_step
     for i in range(n_warm):
         mod.fit_step(batches[i % 2], i)
@@ -433,7 +436,7 @@ def run_config(name, args, rank, world, dev, want_cpu=True, steps=None, warmup=N
                        "model": cfg["cls"], "params": nparams, "global_batch": cfg["batch"] * world,
                        "per_gpu_batch": cfg["batch"], "resolution": cfg["res"], "parallelism": f"dp{world}",
                        "rccl_world_size": world, "backend": dist.get_backend() if world > 1 else None,
-                       "step_launch": "hip graph (captured step)" if graphed else "eager"},
+                       "step_launch": launch},
             "loss": round(loss_v, 6), "roofline": roofline, "cpu_baseline": cpu}
 
 

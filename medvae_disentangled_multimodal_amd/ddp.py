@@ -126,6 +126,10 @@ class DataParallel:
         g = self.module.flat.grad[lo:hi]
         self._works.append(dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
+    def backend(self) -> Optional[str]:
+        """the process group's backend ("nccl" = RCCL on ROCm, "gloo"); None without a process group."""
+        return dist.get_backend(self.group) if dist.is_initialized() else None
+
     def any_across_ranks(self, flags: torch.Tensor) -> torch.Tensor:
         """Element-wise OR of a small bool vector over all ranks (same call order on every rank)."""
         if self.world == 1:

@@ -14,6 +14,7 @@ Lightning optimisation step: zero_grad -> training_step -> backward -> [all-redu
 from __future__ import annotations
 
 import inspect
+import os
 from typing import Any, Dict, Optional, Tuple
 
 import torch
@@ -273,37 +274,71 @@ class VAELightningModule(_Base):
         return used.to(torch.int32)
 
     def fit_step_graphed(self, batch, batch_idx: int = 0, eps: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """fit_step replayed from a captured HIP graph: the whole optimisation step (forward, loss, backward,
-        non-finite zeroing, clip, Adam/AdamW) is captured once and then replayed, so the host issues one graph
-        launch per step instead of ~800 kernel launches (the small 28x28 configs are host-bound otherwise).
-        Same arithmetic and the same kernels as fit_step; dropout masks stay fresh per step through the device
-        dropout salt the graph advances (ops.dropout_salt); the reparameterisation noise comes from torch's
-        graph-safe generator. Requires static batch shapes (the batch is copied into the graph's input buffers),
-        a constant learning rate (a change re-captures), automatic optimisation without a process group, and at
-        least one eager fit_step before the first call (library / allocator state is built eagerly)."""
-        if self.process_group is not None or self.use_discriminator:
-            raise RuntimeError("fit_step_graphed: data-parallel and adversarial steps run eagerly (fit_step)")
+        """fit_step replayed from captured HIP graphs: the optimisation step (forward, loss, backward, gradient
+        exchange, non-finite zeroing, clip, Adam/AdamW) is captured once and then replayed, so the host issues one
+        or two graph launches per step instead of ~800 kernel launches (the small 28x28 configs are host-bound
+        otherwise). Same arithmetic and the same kernels as fit_step; dropout masks stay fresh per step through the
+        device dropout salt the graph advances (ops.dropout_salt); the reparameterisation noise comes from torch's
+        graph-safe generator. Requires static batch shapes (the batch is copied into the graph's input buffers), a
+        constant learning rate (a change re-captures), automatic optimisation, and at least one eager fit_step
+        before the first call (library / allocator / communicator state is built eagerly).
+
+        Data-parallel (ddp.DataParallel attached), two capture modes:
+          "whole" (RCCL, the "nccl" backend): ONE graph holding the step AND its bucketed gradient all-reduces,
+                  launched from the backward's readiness hooks exactly as in the eager step (RCCL collectives are
+                  capturable: they are kernels on RCCL's stream, ordered by events the capture records)
+          "split" (any other backend -- gloo cannot be captured -- or MVAE_DP_CAPTURE=split): graph 1 = forward +
+                  backward, then the exchange eagerly (synchronous bucketed all-reduce + the per-modality usage OR),
+                  graph 2 = the optimizer step reading the exchanged gradients and the usage mask from static
+                  buffers."""
+        if self.use_discriminator:
+            raise RuntimeError("fit_step_graphed: adversarial steps run eagerly (fit_step)")
         if self.optimizer is None or self.global_step_count == 0:
             raise RuntimeError("fit_step_graphed: run at least one eager fit_step first")
         ins = list(batch) + ([eps] if eps is not None else [])
+        mode = self._dp_capture_mode()
         # everything the captured launches freeze as host values: shapes, the optimizer's hyper-parameters
-        # (lr, betas, eps, weight decay), clip norm and gradient scale, the GEMM arithmetic
+        # (lr, betas, eps, weight decay), clip norm and gradient scale, the GEMM arithmetic, the exchange mode
         opt = self.optimizer
         hyper = tuple(sorted((k, tuple(v) if isinstance(v, (list, tuple)) else v)
                              for k, v in opt.param_groups[0].items() if k != "params"))
         key = (tuple((tuple(t.shape), t.dtype, t.device) for t in ins), eps is not None, hyper,
-               opt.max_grad_norm, getattr(opt, "grad_scale", None), id(opt), id(self.flat), self.precision)
+               opt.max_grad_norm, getattr(opt, "grad_scale", None), id(opt), id(self.flat), self.precision, mode,
+               id(self.process_group))
         g = getattr(self, "_graph", None)
         if g is None or g["key"] != key:
-            g = self._capture_step(ins, len(batch), batch_idx, key)
+            g = self._capture_step(ins, len(batch), batch_idx, key, mode)
         for dst, src in zip(g["inputs"], ins):
             if dst.data_ptr() != src.data_ptr():
                 dst.copy_(src)
-        g["graph"].replay()
+        if mode == "split":
+            g["graph"].replay()  # forward + backward
+            prev = ops.set_precision(self.precision)
+            try:
+                self.process_group.allreduce_gradients(self.flat)
+                used = self._used_mask()
+                if used is not None:
+                    g["used"].copy_(used)
+            finally:
+                ops.restore_math_mode(prev)
+            g["graph_opt"].replay()
+        else:
+            g["graph"].replay()
         self.global_step_count += 1
         return g["loss"]
 
-    def _capture_step(self, ins, nb, batch_idx, key):
+    def _dp_capture_mode(self) -> str:
+        """"single" (no data parallelism), "whole" or "split" (see fit_step_graphed)."""
+        pg = self.process_group
+        if pg is None or getattr(pg, "world", 1) == 1:
+            return "single"
+        forced = os.environ.get("MVAE_DP_CAPTURE")
+        if forced in ("whole", "split"):
+            return forced
+        backend = pg.backend() if hasattr(pg, "backend") else None
+        return "whole" if backend == "nccl" else "split"
+
+    def _capture_step(self, ins, nb, batch_idx, key, mode="single"):
         dev = ins[0].device
         static = [t.clone() for t in ins]
         salt = ops.dropout_salt(dev)
@@ -314,14 +349,33 @@ class VAELightningModule(_Base):
         graph = torch.cuda.CUDAGraph()
         step0 = self.global_step_count
         pinned = ops.ARENA.pinning = []  # the graph keeps every scratch buffer it bakes in (ops._Arena)
+        eps_in = static[nb] if len(static) > nb else None
+        rec = dict(inputs=static, salt=salt, key=key, arena=pinned)
         try:
-            with torch.cuda.graph(graph):  # recorded, not executed: capturing performs no optimisation step
-                salt.add_(1)
-                loss = self.fit_step(static[:nb], batch_idx, eps=static[nb] if len(static) > nb else None)
+            if mode != "split":
+                with torch.cuda.graph(graph):  # recorded, not executed: capturing performs no optimisation step
+                    salt.add_(1)
+                    loss = self.fit_step(static[:nb], batch_idx, eps=eps_in)
+            else:
+                graph_opt = torch.cuda.CUDAGraph()
+                used = torch.ones(len(self.flat.params), dtype=torch.int32, device=dev)
+                prev = ops.set_precision(self.precision)
+                try:
+                    with torch.cuda.graph(graph):
+                        salt.add_(1)
+                        loss = self._forward_backward(static[:nb], batch_idx, eps_in, exchange=False)
+                    with torch.cuda.graph(graph_opt, pool=graph.pool()):
+                        self._optimizer_phase(used=used if self._kind == "indices" else None, exchange=False)
+                finally:
+                    ops.flat_weights_stale()
+                    ops.restore_math_mode(prev)
+                loss = loss.detach()
+                rec.update(graph_opt=graph_opt, used=used)
         finally:
             ops.ARENA.pinning = None
         self.global_step_count = step0
-        self._graph = dict(graph=graph, inputs=static, loss=loss, salt=salt, key=key, arena=pinned)
+        rec.update(graph=graph, loss=loss)
+        self._graph = rec
         return self._graph
 
     def _adversarial_fit_step(self, batch, eps=None) -> torch.Tensor:
@@ -364,6 +418,26 @@ class VAELightningModule(_Base):
         self.global_step_count += 2
         return loss_g
 
+    def _forward_backward(self, batch, batch_idx, eps, exchange: bool = True) -> torch.Tensor:
+        """fit_step's first phase: gradients of this rank's batch in the flat buffer (exchange: the data-parallel
+        bucket all-reduces launched from the backward's readiness hooks)."""
+        self.model.train()
+        self.optimizer.zero_grad()
+        ops.prep_flat_weights(self.flat.data)  # every conv weight in the GEMM format, one launch
+        loss = self.training_step(batch, batch_idx, eps=eps)
+        if exchange and self.process_group is not None:
+            self.process_group.begin_backward()
+        loss.backward()
+        return loss
+
+    def _optimizer_phase(self, used: Optional[torch.Tensor] = None, exchange: bool = True):
+        """fit_step's second phase: finish the gradient exchange, then the fused optimizer step (used: the usage mask
+        buffer the split graph capture reads; default: computed here)."""
+        if exchange and self.process_group is not None:
+            self.process_group.allreduce_gradients(self.flat)
+        ops.flat_weights_stale()
+        self.optimizer.step(used=self._used_mask() if used is None else used)
+
     def fit_step(self, batch, batch_idx: int = 0, eps: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One optimisation step of Lightning's loop, fused (automatic optimisation, or the
         reference's manual generator/discriminator pair once the discriminator is active)."""
@@ -378,16 +452,8 @@ class VAELightningModule(_Base):
         self.model.train()
         prev = ops.set_precision(self.precision)
         try:
-            self.optimizer.zero_grad()
-            ops.prep_flat_weights(self.flat.data)  # every conv weight in the GEMM format, one launch
-            loss = self.training_step(batch, batch_idx, eps=eps)
-            if self.process_group is not None:
-                self.process_group.begin_backward()
-            loss.backward()
-            if self.process_group is not None:
-                self.process_group.allreduce_gradients(self.flat)
-            ops.flat_weights_stale()
-            self.optimizer.step(used=self._used_mask())
+            loss = self._forward_backward(batch, batch_idx, eps)
+            self._optimizer_phase()
         finally:
             ops.flat_weights_stale()
             ops.restore_math_mode(prev)

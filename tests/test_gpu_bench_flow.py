@@ -34,3 +34,23 @@ def test_bench_two_rank_flow_c4():
     assert out["cpu_baseline"] is None  # rank 0 at N = 1 only
     assert abs(out["value"] - 8 / (out["ms_per_step"] * 1e-3)) <= 1e-2 * out["value"]
     assert out["loss"] == out["loss"]  # finite, not NaN
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_rank_flow_c3_graphed():
+    """c3 (a captured-graph config) at N = 2: the step is graph-replayed under data parallelism too (gloo: "split"
+    capture, two graphs around the eager exchange)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, MVAE_BENCH_BACKEND="gloo", MVAE_BENCH_ONE_DEVICE="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "c3", "--batch", "64",
+           "--steps", "3", "--warmup", "1", "--no-kernel-timing"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=560)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 128
+    assert out["config"]["step_launch"] == "hip graph (captured step, dp capture split)"
+    assert out["value"] > 0 and out["loss"] == out["loss"]
