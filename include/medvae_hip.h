@@ -204,6 +204,16 @@ size_t mvae_gemm_workspace_bytes(int m, int n, int k, int batch);
 int mvae_softmax_rows(const float* x, float* y, long long rows, int n, void* stream);
 int mvae_softmax_rows_bwd(const float* y, const float* dy, float* dx, long long rows, int n, void* stream);
 
+/* Fused single-tile attention core for n <= 64 tokens per image (the 7x7 / 8x8 mid AttnBlocks,
+ * encoder_decoder.py:83-107): o = softmax(q k^T * scale, dim=2) v in ONE launch per direction, one workgroup per
+ * image, the n x n scores kept in LDS. q, k, v, o: [batch][n][c] fp32 (channels contiguous), c % 64 == 0;
+ * lse: [batch][64] fp32, the row log-sum-exp of the scaled scores written by the forward and read by the backward
+ * (which recomputes the scores: no score tensor in HBM). Products in the process-wide GEMM arithmetic. */
+int mvae_attention_small_fwd(const float* q, const float* k, const float* v, float* o, float* lse, int batch, int n,
+                             int c, float scale, void* stream);
+int mvae_attention_small_bwd(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                             float* dq, float* dk, float* dv, int batch, int n, int c, float scale, void* stream);
+
 /* ---- GroupNorm (+SiLU, +inverted dropout) -------------------------------------------------------
  * Normalize() = nn.GroupNorm(min(32,C), C, eps=1e-6) (encoder_decoder.py:28-33) fused with
  * nonlinearity() (:13-15) and ResnetBlock's nn.Dropout (:163). mean/rstd: [nb*groups].

@@ -1869,7 +1869,7 @@ void launch_cfg(GemmArgs& a, hipStream_t st) {
                    : CFG == T128x32 ? 32 : 128;
   constexpr int WGM = CFG == T256x128 || CFG == T128x32 ? 4 : 2;
 #ifdef MVAE_W4
-  constexpr int WGN = CFG == T128x256 ? 4 : 2;  // 256x256 on 4 waves (128x128 per wave)
+  constexpr int WGN = CFG == T128x256 ? 4 : (CFG == T128x16 || CFG == T128x32) ? 1 : 2;  // 256x256 on 4 waves
 #else
   constexpr int WGN = (CFG == T256x256 || CFG == T128x256) ? 4 : (CFG == T128x16 || CFG == T128x32) ? 1 : 2;
 #endif

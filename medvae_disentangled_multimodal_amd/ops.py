@@ -1059,7 +1059,19 @@ def _gemm(ta, tb, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batc
                   sB, float(beta), C.data_ptr(), ldc, sC, batch, None, _ptr(residual), ldc, sC, None, 0, st)
 
 
+ATTN_SMALL_MAXN = 64
+ATTN_FUSED = os.environ.get("MVAE_NO_ATTN_FUSED") is None
+
+
+def _attn_small_ok(q, n: int, c: int) -> bool:
+    return ATTN_FUSED and n <= ATTN_SMALL_MAXN and c % 64 == 0 and _al16(q)
+
+
 class AttnCoreFn(torch.autograd.Function):
+    """softmax(q k^T * C^-1/2, dim=2) v over the h*w tokens of each image (encoder_decoder.py:90-103). n <= 64 (the
+    7x7 / 8x8 mid blocks): the fused single-tile kernels, one launch per direction with the scores in LDS and only the
+    row log-sum-exp saved (csrc/attn.hip); larger n (c4 / c5's 16x16 level): two batched GEMMs around a row softmax."""
+
     @staticmethod
     def forward(ctx, q, k, v):
         q, k, v = nhwc(q), nhwc(k), nhwc(v)
@@ -1067,14 +1079,25 @@ class AttnCoreFn(torch.autograd.Function):
         n = h * w
         st = _stream(q)
         scale = float(c) ** -0.5
+        ctx.scale = scale
+        ctx.math = _MATH[0]
+        if _attn_small_ok(q, n, c):
+            o = torch.empty_like(q, memory_format=CL)
+            lse = torch.empty((b, ATTN_SMALL_MAXN), device=q.device, dtype=torch.float32)
+            fl = 4.0 * n * n * c * b  # S = Q K^T and O = P V
+            with _timed("attn_gemm", fl, (n, c, n, b)):
+                _lib.call("mvae_attention_small_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                          lse.data_ptr(), b, n, c, scale, st)
+            ctx.save_for_backward(q, k, v, lse)
+            ctx.fused = True
+            return o
+        ctx.fused = False
         s = torch.empty((b, n, n), device=q.device, dtype=torch.float32)
         _gemm(0, 1, n, n, c, scale, q, c, n * c, k, c, n * c, 0.0, s, n, n * n, b, st)
         _lib.call("mvae_softmax_rows", s.data_ptr(), s.data_ptr(), b * n, n, st)
         o = torch.empty_like(q, memory_format=CL)
         _gemm(0, 0, n, c, n, 1.0, s, n, n * n, v, c, n * c, 0.0, o, c, n * c, b, st)
         ctx.save_for_backward(q, k, v, s)
-        ctx.scale = scale
-        ctx.math = _MATH[0]
         return o
 
     @staticmethod
@@ -1089,6 +1112,17 @@ class AttnCoreFn(torch.autograd.Function):
         b, c, h, w = q.shape
         n = h * w
         st = _stream(q)
+        if ctx.fused:  # p = the row log-sum-exp; the kernel recomputes the scores
+            if not (do.is_contiguous(memory_format=CL) and _al16(do)):
+                do = do.contiguous(memory_format=CL)
+            dq = torch.empty_like(q, memory_format=CL)
+            dk = torch.empty_like(k, memory_format=CL)
+            dv = torch.empty_like(v, memory_format=CL)
+            # algorithm: S and dP (recomputed S, dO V^T) + dV, dQ, dK; reference: dP, dV, dQ, dK
+            with _timed("attn_gemm", 10.0 * n * n * c * b, (n, c, n, b), 8.0 * n * n * c * b):
+                _lib.call("mvae_attention_small_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), do.data_ptr(),
+                          p.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), b, n, c, ctx.scale, st)
+            return dq, dk, dv
         dp = torch.empty((b, n, n), device=q.device, dtype=torch.float32)
         _gemm(0, 1, n, n, c, 1.0, do, c, n * c, v, c, n * c, 0.0, dp, n, n * n, b, st)   # dP = dO V^T
         dv = torch.empty_like(v, memory_format=CL)

@@ -1,0 +1,103 @@
+"""Fused single-tile attention core (csrc/attn.hip, ops.AttnCoreFn for n <= 64 tokens): AttnBlock's
+softmax(q k^T * C^-1/2, dim=2) v and its backward (src/models/encoder_decoder.py:83-107) in one launch per direction,
+at the mid-block geometries of the configs -- c3 (49 tokens, C = 128), c2 / c1 (49, 512), c4 / c5 (64, 2048) -- and edge
+cases (1 token, ragged 17 tokens, C = 64). Checked against float64 torch in each GEMM arithmetic: 3xBF16 ("32"), exact
+fp32 ("32-exact") and bf16 ("bf16-mixed"; the float64 reference then rounds q, k, v to bf16 and the tolerance covers
+the bf16 rounding of P / dS inside the products), and against the unfused path (two batched GEMMs around a row
+softmax) in the same arithmetic."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(8, 128, 7, 7), (4, 512, 7, 7), (2, 2048, 8, 8), (3, 64, 1, 1), (3, 64, 1, 17), (5, 64, 8, 8)]
+TOL = {"32": (2e-5, 1e-4), "32-exact": (5e-6, 5e-6), "bf16-mixed": (1e-2, 2e-2)}
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _rel(a, b):
+    """relative L2 error; the denominator is floored at 1e-3 per element RMS (one token: softmax over a single key is
+    constant, so the reference dq = dk = 0 exactly and only the absolute error means anything)"""
+    a = a.detach().double().cpu().flatten()
+    b = b.detach().double().cpu().flatten()
+    return float((a - b).norm() / b.norm().clamp_min(1e-3 * b.numel() ** 0.5))
+
+
+def _ref(q, k, v, go):
+    b, c, h, w = q.shape
+    n = h * w
+    qr, kr, vr = (t.double().requires_grad_() for t in (q, k, v))
+    s = torch.bmm(qr.reshape(b, c, n).permute(0, 2, 1), kr.reshape(b, c, n)) * c ** -0.5
+    o = torch.bmm(vr.reshape(b, c, n), torch.softmax(s, 2).permute(0, 2, 1)).reshape(b, c, h, w)
+    o.backward(go.double())
+    return o, qr.grad, kr.grad, vr.grad
+
+
+def _run(dev, q, k, v, go, prec, fused):
+    from medvae_disentangled_multimodal_amd import ops
+    qd, kd, vd = (t.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_() for t in (q, k, v))
+    prev, saved = ops.set_precision(prec), ops.ATTN_FUSED
+    ops.ATTN_FUSED = fused
+    try:
+        o = ops.attention_core(qd, kd, vd)
+        o.backward(go.to(dev).contiguous(memory_format=torch.channels_last))
+        torch.cuda.synchronize()
+    finally:
+        ops.restore_math_mode(prev)
+        ops.ATTN_FUSED = saved
+    return o, qd.grad, kd.grad, vd.grad
+
+
+@pytest.mark.parametrize("prec", sorted(TOL))
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_fused_attention_matches_float64(dev, shape, prec):
+    from medvae_disentangled_multimodal_amd import ops
+    b, c, h, w = shape
+    assert ops._attn_small_ok(torch.empty(16, device=dev), h * w, c)
+    g = torch.Generator().manual_seed(c + h * w)
+    q, k, v = (torch.randn(shape, generator=g) for _ in range(3))
+    go = torch.randn(shape, generator=g)
+    qi, ki, vi = (t.bfloat16().float() for t in (q, k, v)) if prec == "bf16-mixed" else (q, k, v)
+    ref = _ref(qi, ki, vi, go)
+    got = _run(dev, q, k, v, go, prec, True)
+    tf, tb = TOL[prec]
+    assert _rel(got[0], ref[0]) < tf, ("out", _rel(got[0], ref[0]))
+    for name, a, r in zip(("dq", "dk", "dv"), got[1:], ref[1:]):
+        assert _rel(a, r) < tb, (name, _rel(a, r))
+
+
+@pytest.mark.parametrize("prec", ["32", "bf16-mixed"])
+def test_fused_attention_matches_unfused_path(dev, prec):
+    """same arithmetic, the two implementations: only the fp32 accumulation / softmax evaluation order differs."""
+    shape = (4, 512, 7, 7)
+    g = torch.Generator().manual_seed(11)
+    q, k, v, go = (torch.randn(shape, generator=g) for _ in range(4))
+    fused = _run(dev, q, k, v, go, prec, True)
+    unfused = _run(dev, q, k, v, go, prec, False)
+    tol = 2e-5 if prec == "32" else 5e-3
+    for a, r in zip(fused, unfused):
+        assert _rel(a, r) < tol
+
+
+def test_fused_attention_launch_count(dev):
+    """one launch forward, one backward (the unfused path: 3 + 5)."""
+    from medvae_disentangled_multimodal_amd import ops
+    shape = (2, 128, 7, 7)
+    g = torch.Generator().manual_seed(3)
+    q, k, v, go = (torch.randn(shape, generator=g) for _ in range(4))
+    qd, kd, vd = (t.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_() for t in (q, k, v))
+    ops.PROFILE = []
+    try:
+        o = ops.attention_core(qd, kd, vd)
+        o.backward(go.to(dev).contiguous(memory_format=torch.channels_last))
+        torch.cuda.synchronize()
+        rec = [r for r in ops.PROFILE if r[0] == "attn_gemm"]
+    finally:
+        ops.PROFILE = None
+    assert len(rec) == 2
