@@ -1063,8 +1063,19 @@ ATTN_SMALL_MAXN = 64
 ATTN_FUSED = os.environ.get("MVAE_NO_ATTN_FUSED") is None
 
 
+# the fused kernel runs one workgroup per image, so its K loops are latency-bound once C is large: measured
+# (tools/attn_bench.py, profiles/r04_attn_bench.txt) faster than the unfused path at 7x7x128 / 7x7x512 (c3 / c2:
+# fwd 1.7x / 1.1x) and slower at 8x8x2048 (c4 / c5: fwd 162 vs 137 us, bwd 380 vs 279 us) -- used up to this C
+ATTN_FUSED_MAXC = 512
+
+
 def _attn_small_ok(q, n: int, c: int) -> bool:
+    """the fused kernel's shape / alignment contract (and not switched off)"""
     return ATTN_FUSED and n <= ATTN_SMALL_MAXN and c % 64 == 0 and _al16(q)
+
+
+def _attn_use_fused(q, n: int, c: int) -> bool:
+    return _attn_small_ok(q, n, c) and c <= ATTN_FUSED_MAXC
 
 
 class AttnCoreFn(torch.autograd.Function):
@@ -1081,7 +1092,7 @@ class AttnCoreFn(torch.autograd.Function):
         scale = float(c) ** -0.5
         ctx.scale = scale
         ctx.math = _MATH[0]
-        if _attn_small_ok(q, n, c):
+        if _attn_use_fused(q, n, c):
             o = torch.empty_like(q, memory_format=CL)
             lse = torch.empty((b, ATTN_SMALL_MAXN), device=q.device, dtype=torch.float32)
             fl = 4.0 * n * n * c * b  # S = Q K^T and O = P V

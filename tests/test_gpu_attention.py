@@ -42,15 +42,16 @@ def _ref(q, k, v, go):
 def _run(dev, q, k, v, go, prec, fused):
     from medvae_disentangled_multimodal_amd import ops
     qd, kd, vd = (t.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_() for t in (q, k, v))
-    prev, saved = ops.set_precision(prec), ops.ATTN_FUSED
+    prev, saved, maxc = ops.set_precision(prec), ops.ATTN_FUSED, ops.ATTN_FUSED_MAXC
     ops.ATTN_FUSED = fused
+    ops.ATTN_FUSED_MAXC = 1 << 30  # the kernel at every C it supports (the dispatch uses it up to C = 512)
     try:
         o = ops.attention_core(qd, kd, vd)
         o.backward(go.to(dev).contiguous(memory_format=torch.channels_last))
         torch.cuda.synchronize()
     finally:
         ops.restore_math_mode(prev)
-        ops.ATTN_FUSED = saved
+        ops.ATTN_FUSED, ops.ATTN_FUSED_MAXC = saved, maxc
     return o, qd.grad, kd.grad, vd.grad
 
 
@@ -92,6 +93,7 @@ def test_fused_attention_launch_count(dev):
     g = torch.Generator().manual_seed(3)
     q, k, v, go = (torch.randn(shape, generator=g) for _ in range(4))
     qd, kd, vd = (t.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_() for t in (q, k, v))
+    assert ops._attn_use_fused(qd, 49, 128)
     ops.PROFILE = []
     try:
         o = ops.attention_core(qd, kd, vd)
