@@ -39,10 +39,9 @@ namespace mvae {
 // operand kinds
 // *_SPLIT kinds read operands already split into 3xBF16 hi/lo groups in HBM (split4_bf16 layout)
 enum { A_ROWK = 0, A_COLM = 1, A_CONV_FWD = 2, A_CONV_UPS = 3, A_CONV_DGRAD = 4, A_CONV_SUBPIX = 5, A_COLM_PIX = 6,
-       A_CONV_FWD_SPLIT = 7, A_CONV_DGRAD_SPLIT = 8, A_COLM_SPLIT = 9, A_COLM_T = 10 };
+       A_CONV_FWD_SPLIT = 7, A_CONV_DGRAD_SPLIT = 8, A_COLM_SPLIT = 9 };
 enum { B_ROWK = 0, B_COLN = 1, B_WGRAD_FWD = 2, B_WGRAD_UPS = 3, B_WGRAD_SUBPIX = 4, B_ROWK_SPLIT = 5,
-       B_WGRAD_FWD_SPLIT = 6, B_WGRAD_FWD_T = 7, B_WGRAD_FWD_SPLIT_T = 8 };
-// *_T: the transposed-staging wgrad loaders (ROW images of k-major operands, LoadColKT / LoadWgradXT)
+       B_WGRAD_FWD_SPLIT = 6 };
 // MODE_SUBPIX: one parity class (ph, pw) of "nearest-x2 upsample then 3x3 conv" as a stride-1 2x2 conv
 // on the low-resolution input whose padding shifts with the parity: pad = pad_t - ph (batch entry
 // bidx = 2*ph + pw carries the class)
@@ -498,13 +497,11 @@ struct LoadColK {
   static constexpr bool COL = true;
   static constexpr int C4 = ROWS / 4;                 // float4 per k-row
   static constexpr int NS = (BK * C4 + NT - 1) / NT;  // float4 per thread
-  static constexpr int KRN = NT / C4;                 // bias-sum contributors per row
   __amdgpu_buffer_rsrc_t rs;
   unsigned ld;
   int rows, K, row0, k, c4, kr;
   float4 v[NS];
   float bs[4] = {0.f, 0.f, 0.f, 0.f};  // A side: running row sums of every staged element
-  __device__ bool bs_ok() const { return true; }
   __device__ void init(const GemmArgs& a, const float* p, int row0_, int kb, int tid, int) {
     rs = make_rsrc(p, IS_A ? a.a_bytes : a.b_bytes);
     ld = (unsigned)(IS_A ? a.lda : a.ldb); rows = IS_A ? a.M : a.N; K = a.K;
@@ -569,8 +566,6 @@ struct LoadColPix {
   static constexpr bool COL = true;
   static constexpr int C4 = ROWS / 4;
   static constexpr int NS = (BK * C4 + NT - 1) / NT;
-  static constexpr int KRN = NT / C4;
-  __device__ bool bs_ok() const { return true; }
   __amdgpu_buffer_rsrc_t rs;
   unsigned ld;
   int rows, K, row0, k, c4, kr, krw, par_off;
@@ -752,187 +747,6 @@ struct LoadWgradX {
         st_presplit<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
       else
         st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
-    }
-  }
-  __device__ void advance() { k += BK; }
-  __device__ void load(const GemmArgs& a) {
-    prep(a);
-#pragma unroll
-    for (int i = 0; i < NS; ++i) load_slot(a, i);
-  }
-  __device__ void store(__bf16* img) {
-#pragma unroll
-    for (int i = 0; i < NS; ++i) store_slot(img, i);
-  }
-};
-
-// ------------------------------------------------------------------------------------------
-// Transposed staging for the weight gradient (MVAE_WGRAD_TR): both wgrad operands are k-major in HBM (k = output
-// pixel; dY [pixel][cout], X [pixel][cin]), which the COL loaders above stage as COL images -- read back with
-// ds_read_b64_tr_b16 on the 32x32x16 MFMA. These loaders instead transpose 4x4 blocks in registers and write ROW images,
-// so the wgrad runs the fwd / dgrad loop form: ds_read_b128 fragments on the 16x16x32 MFMA (the shape whose loop
-// structure measured faster, tools/micro/mfma_shape.hip). A thread owns one 4 (rows) x 4 (k) block per K-tile:
-// lane l -> k-quad l & 7, row quad (tid >> 3) -- the 8 lanes of a row quad write its rows' 64-B k-segments, so the
-// 8-B ds_writes of a wave cover all 32 banks evenly, and each load instruction reads 128-B row segments of 8 pixels.
-// Slot q = pixel q & 3 of block q >> 2 (one float4 load each); the block's 4 row writes happen at its slot 0 (the
-// software-pipelined main loop reloads slot q right after storing it, so every read of the block precedes reloads).
-// ------------------------------------------------------------------------------------------
-template <int ROWS, int NT>
-struct TrShape {
-  static constexpr int RQ = ROWS / 4;                    // row quads
-  static constexpr int BLK = RQ * (BK / 4);              // 4x4 blocks per K-tile
-  static constexpr int NB = (BLK + NT - 1) / NT;         // blocks per thread
-  static constexpr int NS = 4 * NB;                      // slots (one pixel row of a block each)
-};
-
-// A = dY^T: element (row = cout, k = pixel) at P[k*ld + row] (LoadColK's source), staged as a ROW image
-template <int ROWS, int NT, int PREC>
-struct LoadColKT {
-  static constexpr bool COL = false;
-  using SH = TrShape<ROWS, NT>;
-  static constexpr int NS = SH::NS;
-  static constexpr int KRN = BK / 4;  // bias-sum contributors per row: the k-quads
-  static_assert(SH::NB == 1, "LoadColKT: one block per thread (the bias row sums are per thread)");
-  __amdgpu_buffer_rsrc_t rs;
-  unsigned ld;
-  int rows, K, row0, k, kr, c4;  // kr = k-quad, c4 = row quad
-  float4 v[NS];
-  float bs[4] = {0.f, 0.f, 0.f, 0.f};
-  bool want_bs = true;
-  __device__ bool bs_ok() const { return c4 < SH::RQ; }
-  __device__ void init(const GemmArgs& a, const float* p, int row0_, int kb, int tid, int) {
-    rs = make_rsrc(p, a.a_bytes);
-    ld = (unsigned)a.lda; rows = a.M; K = a.K;
-    row0 = row0_; k = kb; kr = tid & 7; c4 = tid >> 3;
-  }
-  __device__ void prep(const GemmArgs&) {}
-  __device__ void load_slot(const GemmArgs&, int q) {
-    const int kk = k + kr * 4 + (q & 3);
-    const int col = row0 + c4 * 4;
-    const bool ok = (c4 < SH::RQ) & (kk < K) & (col < rows);
-    v[q] = bload4(rs, ok ? ((unsigned)kk * ld + (unsigned)col) * 4u : OOB);
-  }
-  __device__ void store_slot(__bf16* img, int q) {
-    if ((q & 3) != 0 || c4 >= SH::RQ) return;
-    const float4 r0{v[q].x, v[q + 1].x, v[q + 2].x, v[q + 3].x};
-    const float4 r1{v[q].y, v[q + 1].y, v[q + 2].y, v[q + 3].y};
-    const float4 r2{v[q].z, v[q + 1].z, v[q + 2].z, v[q + 3].z};
-    const float4 r3{v[q].w, v[q + 1].w, v[q + 2].w, v[q + 3].w};
-    constexpr int PL = Img<ROWS, false>::PLANE;
-    st_split<PREC>(img, PL, row_off(c4 * 4 + 0, kr), r0);
-    st_split<PREC>(img, PL, row_off(c4 * 4 + 1, kr), r1);
-    st_split<PREC>(img, PL, row_off(c4 * 4 + 2, kr), r2);
-    st_split<PREC>(img, PL, row_off(c4 * 4 + 3, kr), r3);
-    if (want_bs) {
-      bs[0] += (r0.x + r0.y) + (r0.z + r0.w);
-      bs[1] += (r1.x + r1.y) + (r1.z + r1.w);
-      bs[2] += (r2.x + r2.y) + (r2.z + r2.w);
-      bs[3] += (r3.x + r3.y) + (r3.z + r3.w);
-    }
-  }
-  __device__ void advance() { k += BK; }
-  __device__ void load(const GemmArgs& a) {
-#pragma unroll
-    for (int i = 0; i < NS; ++i) load_slot(a, i);
-  }
-  __device__ void store(__bf16* img) {
-#pragma unroll
-    for (int i = 0; i < NS; ++i) store_slot(img, i);
-  }
-};
-
-// B = im2col(X)^T of the weight gradient (LoadWgradX's element map: row n' = (r*S + s)*Cx + c, k = output pixel), staged
-// as a ROW image. Needs Cx % 4 == 0 (a row quad is 4 channels of one tap). PRESPLIT: X holds split4_bf16 groups, whose
-// hi / lo halves are re-paired per channel across the block's 4 pixels.
-template <int ROWS, int NT, int MODE, int PREC, bool PRESPLIT = false>
-struct LoadWgradXT {
-  static constexpr bool COL = false;
-  using SH = TrShape<ROWS, NT>;
-  static constexpr int NB = SH::NB;
-  static constexpr int NS = SH::NS;
-  __amdgpu_buffer_rsrc_t rs;
-  int kr, c4, k, pt, pl;
-  int cc[NB], rr[NB], ss[NB];
-  bool nv[NB];
-  int pb, poh, pow_;  // the lane's first pixel of the K-tile (k + 4 kr)
-  float4 v[NS];
-  __device__ int quad(int qb) const { return c4 + qb * (NT / 8); }
-  __device__ void init(const GemmArgs& a, const float* x, int row0, int kb, int tid, int bidx) {
-    rs = make_rsrc(x, a.b_bytes);
-    k = kb; kr = tid & 7; c4 = tid >> 3;
-    pt = a.pad_t - ((bidx + a.sub_par) >> 1);
-    pl = a.pad_l - ((bidx + a.sub_par) & 1);
-#pragma unroll
-    for (int qb = 0; qb < NB; ++qb) {
-      const int n = row0 + quad(qb) * 4;
-      nv[qb] = (quad(qb) < SH::RQ) & (n < a.N);
-      const int nn = nv[qb] ? n : 0;
-      const int tap = nn / a.Cx;
-      cc[qb] = nn - tap * a.Cx;
-      rr[qb] = tap / a.S;
-      ss[qb] = tap - rr[qb] * a.S;
-    }
-  }
-  __device__ void prep(const GemmArgs& a) {
-    const int p0 = min(k + kr * 4, a.K - 1);  // clamp: pixels past K are masked
-    pb = mdiv(p0, a.mg_hw);
-    const int rem = p0 - pb * (a.Ho * a.Wo);
-    poh = mdiv(rem, a.mg_wo);
-    pow_ = rem - poh * a.Wo;
-  }
-  __device__ void load_slot(const GemmArgs& a, int q) {
-    const int qb = q >> 2, j = q & 3;
-    int w_ = pow_ + j, h_ = poh, b_ = pb;
-    while (w_ >= a.Wo) {
-      w_ -= a.Wo;
-      ++h_;
-    }
-    while (h_ >= a.Ho) {
-      h_ -= a.Ho;
-      ++b_;
-    }
-    int ih = 0, iw = 0;
-    const bool tv = tap_src<MODE>(a, pt, pl, h_, w_, rr[qb], ss[qb], ih, iw);
-    const bool ok = nv[qb] & tv & (k + kr * 4 + j < a.K);
-    const unsigned off =
-        (((unsigned)b_ * (unsigned)(a.H * a.W) + (unsigned)(ih * a.W + iw)) * (unsigned)a.Cx + (unsigned)cc[qb]) * 4u;
-    v[q] = bload4(rs, ok ? off : OOB);
-  }
-  __device__ void store_slot(__bf16* img, int q) {
-    const int qb = q >> 2;
-    if ((q & 3) != 0 || quad(qb) >= SH::RQ) return;
-    constexpr int PL = Img<ROWS, false>::PLANE;
-    const int r0 = quad(qb) * 4;
-    if constexpr (PRESPLIT) {
-      typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
-      // pixel j's 16 B: {hi c0|c1, hi c2|c3, lo c0|c1, lo c2|c3}; channel e's 4 pixels -> one 8-B write per plane
-      unsigned w[4][4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        w[j][0] = __float_as_uint(v[q + j].x); w[j][1] = __float_as_uint(v[q + j].y);
-        w[j][2] = __float_as_uint(v[q + j].z); w[j][3] = __float_as_uint(v[q + j].w);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int wi = e >> 1;
-        u32x2_t hi, lo;
-        if (e & 1) {
-          hi = u32x2_t{(w[0][wi] >> 16) | (w[1][wi] & 0xFFFF0000u), (w[2][wi] >> 16) | (w[3][wi] & 0xFFFF0000u)};
-          lo = u32x2_t{(w[0][wi + 2] >> 16) | (w[1][wi + 2] & 0xFFFF0000u),
-                       (w[2][wi + 2] >> 16) | (w[3][wi + 2] & 0xFFFF0000u)};
-        } else {
-          hi = u32x2_t{(w[0][wi] & 0xFFFFu) | (w[1][wi] << 16), (w[2][wi] & 0xFFFFu) | (w[3][wi] << 16)};
-          lo = u32x2_t{(w[0][wi + 2] & 0xFFFFu) | (w[1][wi + 2] << 16), (w[2][wi + 2] & 0xFFFFu) | (w[3][wi + 2] << 16)};
-        }
-        const int off = row_off(r0 + e, kr);
-        *(u32x2_t*)(img + off) = hi;
-        if constexpr (PREC == 3) *(u32x2_t*)(img + PL + off) = lo;
-      }
-    } else {
-      st_split<PREC>(img, PL, row_off(r0 + 0, kr), float4{v[q].x, v[q + 1].x, v[q + 2].x, v[q + 3].x});
-      st_split<PREC>(img, PL, row_off(r0 + 1, kr), float4{v[q].y, v[q + 1].y, v[q + 2].y, v[q + 3].y});
-      st_split<PREC>(img, PL, row_off(r0 + 2, kr), float4{v[q].z, v[q + 1].z, v[q + 2].z, v[q + 3].z});
-      st_split<PREC>(img, PL, row_off(r0 + 3, kr), float4{v[q].w, v[q + 1].w, v[q + 2].w, v[q + 3].w});
     }
   }
   __device__ void advance() { k += BK; }
@@ -1339,12 +1153,6 @@ template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<8, ROWS, VEC, NT, true, PREC> : LoadConvA<ROWS, VEC, NT, MODE_DGRAD, PREC, true> {};
 template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<9, ROWS, VEC, NT, true, PREC> : LoadColK<ROWS, VEC, NT, true, PREC, true> {};
-template <int ROWS, int VEC, int NT, int PREC>
-struct Loader<10, ROWS, VEC, NT, true, PREC> : LoadColKT<ROWS, NT, PREC> {};
-template <int ROWS, int VEC, int NT, int PREC>
-struct Loader<7, ROWS, VEC, NT, false, PREC> : LoadWgradXT<ROWS, NT, MODE_FWD, PREC> {};
-template <int ROWS, int VEC, int NT, int PREC>
-struct Loader<8, ROWS, VEC, NT, false, PREC> : LoadWgradXT<ROWS, NT, MODE_FWD, PREC, true> {};
 
 template <int BM, int BN, int WGM, int WGN, int AK, int VA, int BKIND, int VB, int PREC>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
@@ -1533,8 +1341,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   LA la;
   LB lb;
   // wgrad: only the first column of tiles publishes the bias gradient (row sums of dY^T): the others skip the sums
-  if constexpr (AK == A_COLM || AK == A_COLM_PIX || AK == A_COLM_SPLIT || AK == A_COLM_T)
-    la.want_bs = a.bias_ws != nullptr && tn == 0;
+  if constexpr (AK == A_COLM || AK == A_COLM_PIX || AK == A_COLM_SPLIT) la.want_bs = a.bias_ws != nullptr && tn == 0;
   la.init(a, a.A + bidx * a.sA, m0, kb, tid, bidx);
   lb.init(a, a.B + bidx * a.sB, n0, kb, tid, bidx);
 
@@ -1699,17 +1506,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
 
   // wgrad: the conv bias gradient (row sums of A = dY^T over this split's pixels) falls out of the
   // A staging for free; one column of tiles (tn == 0) publishes it, fixed-order reduction in LDS.
-  if constexpr (AK == A_COLM || AK == A_COLM_PIX || AK == A_COLM_SPLIT || AK == A_COLM_T) {
+  if constexpr (AK == A_COLM || AK == A_COLM_PIX || AK == A_COLM_SPLIT) {
     if (a.bias_ws != nullptr && tn == 0) {
-      constexpr int KRN = LA::KRN;
+      constexpr int KRN = NT / (BM / 4);
       float* red = (float*)lds;
       __syncthreads();
-      if (la.bs_ok()) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) red[la.kr * BM + la.c4 * 4 + e] = la.bs[e];
-      }
+      for (int e = 0; e < 4; ++e) red[la.kr * BM + la.c4 * 4 + e] = la.bs[e];
       __syncthreads();
-      if (la.kr == 0 && la.bs_ok()) {
+      if (la.kr == 0) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float sum = 0.f;
@@ -2075,7 +1880,7 @@ void launch_cfg(GemmArgs& a, hipStream_t st) {
               !vec_epi_disabled();
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splits);
   constexpr bool presplit = AK == A_CONV_FWD_SPLIT || AK == A_CONV_DGRAD_SPLIT || AK == A_COLM_SPLIT ||
-                            BKIND == B_ROWK_SPLIT || BKIND == B_WGRAD_FWD_SPLIT || BKIND == B_WGRAD_FWD_SPLIT_T;
+                            BKIND == B_ROWK_SPLIT || BKIND == B_WGRAD_FWD_SPLIT;
   const int mm = math_mode();
   if constexpr (PO >= 0)
     hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, PO>), grid, dim3(64 * WGM * WGN), 0, st, a);
@@ -2123,22 +1928,6 @@ void launch_dma(GemmArgs& a, hipStream_t st, int cfg) {
 void conv_dma(int ak, GemmArgs& a, hipStream_t st, int cfg, int prec);
 // weight gradient on DMA-staged dY^T (COL) x im2col of X (B_WGRAD_FWD / B_WGRAD_SUBPIX)
 void wgrad_dma(int bkind, GemmArgs& a, hipStream_t st, int cfg, int prec);
-
-// the transposed-staging wgrad kinds (A_COLM_T x B_WGRAD_FWD(_SPLIT)_T) on the tile configs whose row quads a
-// workgroup covers in one block per thread
-inline bool wgrad_tr() {
-  static int v = getenv("MVAE_NO_WGRAD_TR") == nullptr;  // experiment knob: the COL-image wgrad loop
-  return v != 0;
-}
-template <int AK, int BKIND>
-void launch_tr(GemmArgs& a, hipStream_t st, int cfg) {
-  switch (cfg) {
-    case T256x256: launch_cfg<T256x256, AK, 4, BKIND, 4>(a, st); break;
-    case T256x128: launch_cfg<T256x128, AK, 4, BKIND, 4>(a, st); break;
-    case T128x256: launch_cfg<T128x256, AK, 4, BKIND, 4>(a, st); break;
-    default: launch_cfg<T128x128, AK, 4, BKIND, 4>(a, st); break;
-  }
-}
 
 template <int AK, int VA, int BKIND, int VB>
 void launch_small(GemmArgs& a, hipStream_t st, int cfg) {

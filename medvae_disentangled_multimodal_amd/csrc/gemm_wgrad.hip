@@ -146,9 +146,6 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
       else if (mode == 0) launch_small<A_COLM_SPLIT, 4, B_WGRAD_FWD, 1>(a, st, cfg);
       else if (vb) launch_big<A_COLM_SPLIT, 4, B_WGRAD_UPS, 4>(a, st, cfg);
       else launch_small<A_COLM_SPLIT, 4, B_WGRAD_UPS, 1>(a, st, cfg);
-    } else if (mode == 0 && va && vb && cfg <= T128x128 && wgrad_tr()) {  // transposed staging, ROW images
-      if (xsplit) launch_tr<A_COLM_T, B_WGRAD_FWD_SPLIT_T>(a, st, cfg);
-      else launch_tr<A_COLM_T, B_WGRAD_FWD_T>(a, st, cfg);
     } else if (xsplit) {
       if (va) launch_big<A_COLM, 4, B_WGRAD_FWD_SPLIT, 4>(a, st, cfg);
       else launch_small<A_COLM, 1, B_WGRAD_FWD_SPLIT, 4>(a, st, cfg);
