@@ -15,7 +15,8 @@
 #   tools/gpu_evidence.sh pmc      <tag> <shape> <pass> <prec>    conv counter sets (MFMA busy, waits, VALU / SALU /
 #                                                                 LDS issue) of one tools/conv_bench.py shape + pass
 #   tools/gpu_evidence.sh ab       <tag> <config> <variant...>    interleaved A/B of library builds variants/<v>/
-#                                                                 (tools/build_variant.sh) on one bench config
+#                                                                 (tools/build_variant.sh), "default" (in-tree) or
+#                                                                 "env:VAR=VAL[,...]" (in-tree under those settings)
 #   tools/gpu_evidence.sh loops    <tag> <variant...>              interleaved A/B of library builds on the GEMM main
 #                                                                 loops: tools/loop_bench.py (plain 4k GEMM + c4 3x3
 #                                                                 layers) and tools/dma_exp.py (per-pass conv), both
@@ -101,9 +102,13 @@ ab() {
   local cfg=$1; shift
   for r in 1 2; do
     for v in "$@"; do
-      MVAE_HIP_LIB=variants/$v/libmvae_hip.so timeout -k 10 300 python -u bench.py --config $cfg --steps 6 --warmup 2 \
-        --no-cpu-baseline > $OUT/ab_${cfg}_${v}_$r.json 2> $OUT/ab_${cfg}_${v}_$r.err || return $?
-      python3 tools/bench_brief.py $OUT/ab_${cfg}_${v}_$r.json "$v"
+      local lib=variants/$v/libmvae_hip.so envs=() tag=${v//[:=,]/_}
+      [ "$v" = default ] && lib=medvae_disentangled_multimodal_amd/libmvae_hip.so
+      # "env:VAR=VAL[,VAR=VAL]": the in-tree library under those environment settings
+      if [[ $v == env:* ]]; then lib=medvae_disentangled_multimodal_amd/libmvae_hip.so; IFS=, read -ra envs <<< "${v#env:}"; fi
+      env "${envs[@]}" MVAE_HIP_LIB=$lib timeout -k 10 300 python -u bench.py --config $cfg --steps 6 --warmup 2 \
+        --no-cpu-baseline --detail > $OUT/ab_${cfg}_${tag}_$r.json 2> $OUT/ab_${cfg}_${tag}_$r.err || return $?
+      python3 tools/bench_brief.py $OUT/ab_${cfg}_${tag}_$r.json "$v"
     done
   done
 }
