@@ -234,6 +234,19 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
                              unsigned long long seed, void* workspace, size_t workspace_bytes,
                              void* stream);
 size_t mvae_group_norm_workspace_bytes(int nb, int hw, int c);
+/* mvae_group_norm_bwd_nhwc that also writes dx as packed bf16 (dx_packed: 2 B per element at the element offsets,
+ * 8-B aligned -- the bf16-mixed GEMMs' operand format) and, when dbias is non-null, dbias[c] = bias_beta * dbias[c]
+ * + sum over rows of dx (fp64 partials in cs_workspace, fixed order): the output gradient and bias gradient of the
+ * convolution whose output this GroupNorm normalizes (ResnetBlock conv1 -> norm2, the next block's norm1), in the
+ * same pass as dx -- replaces mvae_pack_bf16_colsum over dx (the conv bias half of convolution_backward,
+ * encoder_decoder.py:141-163). x, dy, dx, dx_add 16-B aligned. */
+int mvae_group_norm_bwd_pack_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
+                                  const float* mean, const float* rstd, float* dx, const float* dx_add, float* dgamma,
+                                  float* dbeta, int nb, int hw, int c, int groups, int silu, float drop_p,
+                                  unsigned long long seed, void* workspace, size_t workspace_bytes, void* dx_packed,
+                                  float* dbias, float bias_beta, void* cs_workspace, size_t cs_workspace_bytes,
+                                  void* stream);
+size_t mvae_group_norm_colsum_workspace_bytes(int nb, int hw, int c);
 /* Path of mvae_group_norm_fwd_nhwc / _bwd_nhwc (process-wide): 0 = auto (small per-sample tensors -- the
  * 28x28 / 14x14 / 7x7 levels -- run the register-resident one-pass kernels: x read once per pass),
  * 1 = streaming only (statistics pass + apply pass). Both are deterministic; they agree to fp32 rounding. */

@@ -59,6 +59,12 @@ struct GnArgs {
   // process-wide dropout salt in device memory (mvae_set_dropout_salt): mixed into the seed, so a replayed HIP
   // graph -- whose kernel arguments, seeds included, are frozen -- still draws a fresh mask once the salt advances
   const unsigned long long* salt;
+  // backward, optional (mvae_group_norm_bwd_pack_nhwc): dx also written as packed bf16 (RNE, 2 B per element at the
+  // element offsets: the bf16-mixed GEMMs' operand format) and its per-channel column sums as fp64 partials
+  // (streaming kernel: [nb * chunks][C], resident kernel: [nb][C]) -- the consuming conv's output gradient and bias
+  // gradient, without a separate pass over dx
+  uint2* dxp;
+  double* csp;
 };
 __device__ __forceinline__ unsigned long long drop_seed(const GnArgs& a) {
   return a.salt ? a.seed ^ (*a.salt * 0xD1B54A32D192ED03ull) : a.seed;
@@ -372,8 +378,10 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
   const int b = blockIdx.y;
   const int cpg = a.C / a.G;
   const long long sbase = (long long)b * a.hw * a.C;
+  __shared__ double csr[256][4];  // (a.csp) per-thread column sums, combined over the row phases in fixed order
   for (int cg0 = 0; cg0 < (a.C >> 2); cg0 += 256) {
     GnMap mp(a, cg0);
+    double cs[4] = {0.0, 0.0, 0.0, 0.0};
     if (mp.act) {
       float m[4], rs[4], gm[4], bt[4], q1[4], q2[4], q3[4];
 #pragma unroll
@@ -428,11 +436,50 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
             o[0] += av[u].x; o[1] += av[u].y; o[2] += av[u].z; o[3] += av[u].w;
           }
           *(float4*)(op + (long long)r * a.C) = float4{o[0], o[1], o[2], o[3]};
+          if (a.dxp != nullptr) {
+            a.dxp[off >> 2] = uint2{pk_bf16x2(o[0], o[1]), pk_bf16x2(o[2], o[3])};
+            cs[0] += o[0]; cs[1] += o[1]; cs[2] += o[2]; cs[3] += o[3];
+          }
         }
       }
     }
+    if (a.csp != nullptr) {  // (uniform) one partial row per (sample, chunk): the row phases summed in order
+      const int tid = threadIdx.x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) csr[tid][e] = cs[e];
+      __syncthreads();
+      if (mp.act && mp.rph == 0) {
+        double t[4] = {0.0, 0.0, 0.0, 0.0};
+        const int C4l = (a.C >> 2) >= 256 ? 256 : (a.C >> 2);
+        for (int q = 0; q < mp.rpar; ++q)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) t[e] += csr[q * C4l + (tid % C4l)][e];
+        double* o = a.csp + ((long long)b * gridDim.x + blockIdx.x) * a.C + mp.c4 * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = t[e];
+      }
+      __syncthreads();
+    }
     if ((a.C >> 2) < 256) break;
   }
+}
+
+// out[c] = beta * out[c] + sum over nparts partial rows (fixed order): the bias gradient from the column-sum partials
+__global__ void __launch_bounds__(256) gn_colsum_final_kernel(const double* __restrict__ part, int nparts, int C,
+                                                              float* __restrict__ out, float beta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  int q = 0;
+  for (; q + 8 <= nparts; q += 8) {  // 8 partial loads in flight, summed in order
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = part[(long long)(q + j) * C + c];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j];
+  }
+  for (; q < nparts; ++q) s += part[(long long)q * C + c];
+  out[c] = (beta != 0.f ? beta * out[c] : 0.f) + (float)s;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -729,12 +776,27 @@ __device__ __forceinline__ void gn_bwd_unit(const GnArgs& a, int SC, int u, cons
     q3[e] = sm.gk3[c4 * 4 + e];
   }
   const __amdgpu_buffer_rsrc_t dr = un.rsrc(dx);
+  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((__bf16*)a.dxp + un.ubase), (short)0, (int)(un.bytes >> 1), 0x00020000);
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
     // av is zero when there is no residual-branch gradient; rows past hw: the store is dropped
     const float4 o{dv[i].x * q1[0] + xv[i].x * q2[0] + q3[0] + av[i].x, dv[i].y * q1[1] + xv[i].y * q2[1] + q3[1] + av[i].y,
                    dv[i].z * q1[2] + xv[i].z * q2[2] + q3[2] + av[i].z, dv[i].w * q1[3] + xv[i].w * q2[3] + q3[3] + av[i].w};
     gn_res_store(dr, vo + (unsigned)(i * rstep), gn_bits(o));
+    if (a.dxp != nullptr) {  // packed bf16 at half the byte offsets (8-B stores; rows past hw: dropped)
+      typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{pk_bf16x2(o.x, o.y), pk_bf16x2(o.z, o.w)}, pr,
+                                            (vo >> 1) + (unsigned)(i * (rstep >> 1)), 0, 0);
+      if (rph + i * rpar < a.hw) {
+        cs[0] += o.x; cs[1] += o.y; cs[2] += o.z; cs[3] += o.w;
+      }
+    }
+  }
+  if (a.csp != nullptr) {  // (uniform) per-unit column sums -> csp[b][c0 .. c0 + SC)
+    gn_slab_reduce<4>(cs, C4, sm.red, sm.chs);
+    for (int t = tid; t < SC; t += GN_RES_NT) a.csp[(long long)un.b * a.C + un.c0 + t] = (double)sm.chs[t];
   }
 }
 
@@ -1086,11 +1148,49 @@ int mvae_group_norm_fwd_part_nhwc(const float* x, const double* part, const floa
 }
 
 // dx = d/dx of the fused forward [+ dx_add when non-null]; dgamma/dbeta are ACCUMULATED (+=) when non-null.
+// pack (non-null dxp): also dxp = packed bf16 of dx and dbias = bias_beta * dbias + column sums of dx (the consuming
+// conv's bf16 output gradient and bias gradient; partials in cs_ws)
+static int gn_bwd(const float* x, const float* dy, const float* gamma, const float* beta, const float* mean,
+                  const float* rstd, float* dx, const float* dx_add, float* dgamma, float* dbeta, int nb, int hw, int c,
+                  int groups, int silu, float drop_p, unsigned long long seed, void* workspace, size_t workspace_bytes,
+                  void* dxp, float* dbias, float bias_beta, void* cs_ws, void* stream);
 int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
                              const float* mean, const float* rstd, float* dx, const float* dx_add,
                              float* dgamma, float* dbeta,
                              int nb, int hw, int c, int groups, int silu, float drop_p,
                              unsigned long long seed, void* workspace, size_t workspace_bytes, void* stream) {
+  return gn_bwd(x, dy, gamma, beta, mean, rstd, dx, dx_add, dgamma, dbeta, nb, hw, c, groups, silu, drop_p, seed,
+                workspace, workspace_bytes, nullptr, nullptr, 0.f, nullptr, stream);
+}
+
+// column-sum partials of mvae_group_norm_bwd_pack_nhwc: [nb * chunks][C] fp64 (streaming) or [nb][C] (resident)
+size_t mvae_group_norm_colsum_workspace_bytes(int nb, int hw, int c) {
+  return (size_t)nb * std::max(1, gn_chunks(nb, hw)) * c * sizeof(double);
+}
+
+int mvae_group_norm_bwd_pack_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
+                                  const float* mean, const float* rstd, float* dx, const float* dx_add, float* dgamma,
+                                  float* dbeta, int nb, int hw, int c, int groups, int silu, float drop_p,
+                                  unsigned long long seed, void* workspace, size_t workspace_bytes, void* dx_packed,
+                                  float* dbias, float bias_beta, void* cs_workspace, size_t cs_workspace_bytes,
+                                  void* stream) {
+  if (dx_packed == nullptr || ((uintptr_t)dx_packed & 7) || ((uintptr_t)dx & 15) || ((uintptr_t)x & 15) ||
+      ((uintptr_t)dy & 15) || (dx_add && ((uintptr_t)dx_add & 15)) || (dbias && cs_workspace == nullptr)) {
+    set_error("group_norm_bwd_pack: 16-B aligned x / dy / dx, 8-B aligned packed output, a column-sum workspace");
+    return MVAE_EINVAL;
+  }
+  if (dbias && cs_workspace_bytes < mvae_group_norm_colsum_workspace_bytes(nb, hw, c)) {
+    set_error("group_norm_bwd_pack: column-sum workspace too small");
+    return MVAE_EWORKSPACE;
+  }
+  return gn_bwd(x, dy, gamma, beta, mean, rstd, dx, dx_add, dgamma, dbeta, nb, hw, c, groups, silu, drop_p, seed,
+                workspace, workspace_bytes, dx_packed, dbias, bias_beta, cs_workspace, stream);
+}
+
+static int gn_bwd(const float* x, const float* dy, const float* gamma, const float* beta, const float* mean,
+                  const float* rstd, float* dx, const float* dx_add, float* dgamma, float* dbeta, int nb, int hw, int c,
+                  int groups, int silu, float drop_p, unsigned long long seed, void* workspace, size_t workspace_bytes,
+                  void* dxp, float* dbias, float bias_beta, void* cs_ws, void* stream) {
   if (nb <= 0 || hw <= 0 || c <= 0 || (c & 3) || groups <= 0 || c % groups) {
     set_error("group_norm_bwd: bad geometry");
     return MVAE_EINVAL;
@@ -1106,6 +1206,8 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
   a.chunks = gn_chunks(nb, hw);
   a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
   a.ws = (double*)workspace;
+  a.dxp = (uint2*)dxp;
+  a.csp = dbias ? (double*)cs_ws : nullptr;
   int it = 0;
   int sc = gn_resident_slab(nb, hw, c, groups, &it, 8);
   // the backward holds x and dy of two units (2 waves/SIMD): with 64-B row segments (sc < 32) it streams at
@@ -1120,9 +1222,12 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
     else hipLaunchKernelGGL(gn_bwd_resident_kernel<8>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, pws, dx);
     if (dgamma || dbeta)
       hipLaunchKernelGGL(gn_param_reduce_kernel, dim3(c), dim3(256), 0, st, (const double*)pws, nb, c, dgamma, dbeta);
+    if (dbias)
+      hipLaunchKernelGGL(gn_colsum_final_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st, (const double*)a.csp, nb, c,
+                         dbias, bias_beta);
     return launch_status();
   }
-  if (const int sc2 = gn_unit2_slab(hw, c, groups)) {
+  if (const int sc2 = dxp ? 0 : gn_unit2_slab(hw, c, groups)) {  // (the packed output: streaming chain)
     double* pws = (double*)workspace;
     const int units = nb * (c / sc2);
     int dev = 0, cus = 0;
@@ -1151,6 +1256,9 @@ int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma
                        dbeta);
   }
   hipLaunchKernelGGL(gn_dx_kernel, dim3(a.chunks, nb), dim3(256), 0, st, a, k1, k2, k3, dx);
+  if (dbias)
+    hipLaunchKernelGGL(gn_colsum_final_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st, (const double*)a.csp,
+                       nb * a.chunks, c, dbias, bias_beta);
   return launch_status();
 }
 

@@ -786,10 +786,38 @@ class GradSink:
         return g
 
 
+# bf16-mixed mode: a conv output that a GroupNorm normalizes carries a DyPack request. The GroupNorm backward then writes
+# its dx -- this conv's output gradient -- also as packed bf16 with the conv bias gradient summed in the same pass
+# (mvae_group_norm_bwd_pack_nhwc), and the conv backward takes both from it instead of a pack_bf16_colsum pass over dy.
+DYPACK_ATTR = "_mvae_dypack"
+DYPACK = os.environ.get("MVAE_NO_DYPACK") is None
+
+
+class DyPack:
+    __slots__ = ("bias_ref", "packed", "dx_ptr", "dx_version", "dx_shape", "bias_done", "db")
+
+    def __init__(self, bias_ref):
+        self.bias_ref = bias_ref
+        self.packed = self.dx_ptr = self.dx_version = self.dx_shape = self.db = None
+        self.bias_done = False
+
+    def take(self, dy):
+        """(packed dy, bias gradient done, returned bias gradient) when the GroupNorm backward produced them from
+        exactly this gradient tensor (same storage, untouched since), else None; consumed once."""
+        packed, ptr, ver, shp = self.packed, self.dx_ptr, self.dx_version, self.dx_shape
+        out = (packed, self.bias_done, self.db)
+        self.packed = self.dx_ptr = self.dx_version = self.dx_shape = self.db = None
+        self.bias_done = False
+        if packed is None or dy.data_ptr() != ptr or dy._version != ver or tuple(dy.shape) != shp or \
+                not dy.is_contiguous(memory_format=CL):
+            return None
+        return out
+
+
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, geom: ConvGeom, res_sink=None, x_sink=None, gn_part=None,
-                gn_link=None):
+                gn_link=None, dypack=None):
         _check(x, "conv input")
         xs = bool(getattr(x, XSPLIT_ATTR, False))
         xb16 = bool(getattr(x, BF16_ATTR, False))
@@ -810,6 +838,7 @@ class Conv2dFn(torch.autograd.Function):
         ctx.bias_ref = bias
         ctx.res_sink, ctx.x_sink = res_sink, x_sink
         ctx.gn_link = gn_link
+        ctx.dypack = dypack
         return y
 
     @staticmethod
@@ -829,7 +858,12 @@ class Conv2dFn(torch.autograd.Function):
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         bias_done = False
         dyb = None
-        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+        got = ctx.dypack.take(dy) if ctx.dypack is not None else None
+        if got is not None:  # packed dy (and the bias gradient) from the GroupNorm backward that produced dy
+            dyb, bias_done, db_ret = got
+            if not want_b:
+                db_ret = None
+        elif ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             # bf16-mixed: pack dy once for both GEMMs; the bias gradient comes out of the same pass
             bt = _main_grad(ctx.bias_ref) if want_b else None
             if want_b and bt is None:
@@ -871,7 +905,7 @@ class Conv2dFn(torch.autograd.Function):
             _grad_done(ctx.weight_ref)
         if want_b and db_ret is None:
             _grad_done(ctx.bias_ref)
-        return dx, dw_ret, db_ret, dres, None, None, None, None, None
+        return dx, dw_ret, db_ret, dres, None, None, None, None, None, None
 
 
 # The GroupNorm statistics of a conv output emitted by its GEMM epilogue travel with the output tensor
@@ -894,9 +928,15 @@ def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink
     link = getattr(x, GN_BWD_ATTR, None)
     if link is not None and not link.matches(x):
         link = None
-    y = Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink, part, link)
+    dyp = None
+    if gn_stats and DYPACK and _dma_fmt() == 2 and not geom.pointwise and weight.shape[0] % 8 == 0 and \
+            geom.kh * geom.kw <= 32 and torch.is_grad_enabled():
+        dyp = DyPack(bias)
+    y = Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink, part, link, dyp)
     if part is not None:
         setattr(y, GN_PART_ATTR, (part, y._version))
+    if dyp is not None:
+        setattr(y, DYPACK_ATTR, (dyp, y._version))
     return y
 
 
@@ -944,7 +984,7 @@ class GnBwdLink:
 class GroupNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool, drop_p: float, seed: int,
-                y_split: bool = False, grad_sink=None, part=None, link=None):
+                y_split: bool = False, grad_sink=None, part=None, link=None, dypack=None):
         _check(x, "group_norm input")
         x = nhwc(x)
         n, c, h, w = x.shape
@@ -968,6 +1008,7 @@ class GroupNormFn(torch.autograd.Function):
         ctx.gamma_ref, ctx.beta_ref = gamma, beta
         ctx.grad_sink = grad_sink
         ctx.link = link
+        ctx.dypack = dypack
         if link is not None:
             link.x, link.gamma, link.beta, link.mean, link.rstd = x, gamma, beta, mean, rstd
         return y
@@ -1001,6 +1042,27 @@ class GroupNormFn(torch.autograd.Function):
                           gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
                           _ptr(add), _ptr(dg), _ptr(db), n, h * w, c, groups, silu, ws.data_ptr(), ws.numel(),
                           _stream(x))
+            elif ctx.dypack is not None and _al16(dy, dx) and (add is None or _al16(add)):
+                # also dx as packed bf16 and the producing conv's bias gradient (DyPack)
+                req = ctx.dypack
+                packed = torch.empty(x.numel() * 2, device=x.device, dtype=torch.uint8)
+                bref = req.bias_ref
+                tgt, bbeta = None, 0.0
+                if bref is not None and bref.requires_grad:
+                    tgt = _main_grad(bref)
+                    if tgt is not None:
+                        bbeta = 1.0
+                    else:
+                        tgt = req.db = torch.empty(c, device=x.device, dtype=torch.float32)
+                csb = _lib.query("mvae_group_norm_colsum_workspace_bytes", n, h * w, c)
+                cs = ARENA.get("gncs", csb, x.device) if tgt is not None else None
+                _lib.call("mvae_group_norm_bwd_pack_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(),
+                          beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(add), _ptr(dg),
+                          _ptr(db), n, h * w, c, groups, silu, drop_p, seed, ws.data_ptr(), ws.numel(),
+                          packed.data_ptr(), _ptr(tgt), float(bbeta), _ptr(cs), cs.numel() if cs is not None else 0,
+                          _stream(x))
+                req.packed, req.dx_ptr, req.dx_version, req.dx_shape = packed, dx.data_ptr(), dx._version, tuple(dx.shape)
+                req.bias_done = tgt is not None
             else:
                 _lib.call("mvae_group_norm_bwd_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
                           mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(add), _ptr(dg), _ptr(db), n, h * w,
@@ -1009,7 +1071,7 @@ class GroupNormFn(torch.autograd.Function):
             _grad_done(ctx.gamma_ref)
         if ctx.needs_input_grad[2] and db_ret is None:
             _grad_done(ctx.beta_ref)
-        return dx, dg_ret, db_ret, None, None, None, None, None, None, None, None, None
+        return dx, dg_ret, db_ret, None, None, None, None, None, None, None, None, None, None
 
 
 # Activations handed to a convolution in the pre-split 3xBF16 operand layout carry this attribute
@@ -1039,7 +1101,11 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
             x.shape[1] % groups == 0 and x.is_contiguous(memory_format=CL)
         part = part[0] if ok else None
     link = GnBwdLink(groups, silu) if (for_conv and GN_BWD_FUSED and drop_p == 0.0 and x.requires_grad) else None
-    y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink, part, link)
+    dyp = getattr(x, DYPACK_ATTR, None)
+    if dyp is not None:
+        delattr(x, DYPACK_ATTR)  # one GroupNorm per conv output
+        dyp = dyp[0] if dyp[1] == x._version and x.is_contiguous(memory_format=CL) and _al16(x) else None
+    y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink, part, link, dyp)
     if split >= 2:
         setattr(y, BF16_ATTR, True)
     elif split:

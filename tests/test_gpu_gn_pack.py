@@ -1,0 +1,115 @@
+"""GroupNorm backward that also emits the producing conv's bf16 output gradient and bias gradient
+(mvae_group_norm_bwd_pack_nhwc, ops.DyPack): the bf16-mixed mode's replacement for a pack_bf16_colsum pass over dy
+(the conv bias half of convolution_backward, encoder_decoder.py:141-163). Checked on both GroupNorm backward paths
+(streaming chain at large per-sample sizes, register-resident at small ones): dx bitwise equal to the plain backward,
+the packed output bitwise equal to mvae_pack_bf16(dx), the bias gradient equal to float64 column sums of dx; and a
+bf16-mixed training step whose gradients match the step with the separate pack pass."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+# (nb, h, w, C, groups): 64x64x128 takes the streaming chain, 8x8x512 / 7x7x256 the resident kernel
+SHAPES = [(4, 64, 64, 128, 32), (8, 8, 8, 512, 32), (6, 7, 7, 256, 32)]
+
+
+@pytest.mark.parametrize("add", [False, True])
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_gn_bwd_pack_matches_plain_backward(dev, shape, add):
+    from medvae_disentangled_multimodal_amd._lib import call, query
+    nb, h, w, c, g = shape
+    gen = torch.Generator(device=dev).manual_seed(nb * c + h)
+    x = torch.randn(nb, h, w, c, device=dev, generator=gen)
+    dy = torch.randn(nb, h, w, c, device=dev, generator=gen)
+    gamma = 1 + 0.1 * torch.randn(c, device=dev, generator=gen)
+    beta = 0.1 * torch.randn(c, device=dev, generator=gen)
+    dadd = torch.randn(nb, h, w, c, device=dev, generator=gen) if add else None
+    mean = x.view(nb, h * w, g, c // g).mean((1, 3)).reshape(-1).contiguous()
+    rstd = (x.view(nb, h * w, g, c // g).var((1, 3), unbiased=False) + 1e-6).rsqrt().reshape(-1).contiguous()
+    ws = torch.empty(query("mvae_group_norm_workspace_bytes", nb, h * w, c), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    dx0 = torch.empty_like(x)
+    dg0, db0 = torch.zeros(c, device=dev), torch.zeros(c, device=dev)
+    call("mvae_group_norm_bwd_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(),
+         rstd.data_ptr(), dx0.data_ptr(), ptr(dadd), dg0.data_ptr(), db0.data_ptr(), nb, h * w, c, g, 1, 0.0, 0,
+         ws.data_ptr(), ws.numel(), st)
+    dx1 = torch.empty_like(x)
+    dg1, db1 = torch.zeros(c, device=dev), torch.zeros(c, device=dev)
+    packed = torch.empty(x.numel() * 2, dtype=torch.uint8, device=dev)
+    bias = torch.randn(c, device=dev, generator=gen)
+    bias0 = bias.clone()
+    cs = torch.empty(query("mvae_group_norm_colsum_workspace_bytes", nb, h * w, c), dtype=torch.uint8, device=dev)
+    call("mvae_group_norm_bwd_pack_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+         mean.data_ptr(), rstd.data_ptr(), dx1.data_ptr(), ptr(dadd), dg1.data_ptr(), db1.data_ptr(), nb, h * w, c, g,
+         1, 0.0, 0, ws.data_ptr(), ws.numel(), packed.data_ptr(), bias.data_ptr(), 1.0, cs.data_ptr(), cs.numel(), st)
+    ref_packed = torch.empty_like(packed)
+    call("mvae_pack_bf16", dx0.data_ptr(), ref_packed.data_ptr(), x.numel(), st)
+    torch.cuda.synchronize()
+    assert torch.equal(dx1, dx0)
+    assert torch.equal(dg1, dg0) and torch.equal(db1, db0)
+    assert torch.equal(packed, ref_packed)
+    ref_bias = bias0.double() + dx0.double().sum((0, 1, 2))
+    err = float((bias.double() - ref_bias).abs().max() / ref_bias.abs().max())
+    assert err < 1e-6, err
+
+
+def _model_grads(dev, dypack: bool, calls=None):
+    import medvae_disentangled_multimodal_amd as M
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    kw = dict(input_channels=3, latent_dim=8, hidden_channels=64, ch_mult=(1, 2), num_res_blocks=1,
+              attn_resolutions=[], dropout=0.0, resolution=32)
+    torch.manual_seed(0)
+    model = M.BaseVAE(**kw).to(dev)
+    mod = M.VAELightningModule(model, {"type": "adam", "lr": 1e-4}, {"type": "none"}, {"type": "vae"},
+                               gradient_clip_val=None, precision="bf16-mixed")
+    mod.configure_optimizers()
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(4, 3, 32, 32, generator=g) * 2 - 1).to(dev)
+    eps = torch.randn(4, 8, 16, 16, generator=g).to(dev)
+    saved, real_call = ops.DYPACK, _lib.call
+    ops.DYPACK = dypack
+    if calls is not None:
+        def counting(name, *args):
+            calls[name] = calls.get(name, 0) + 1
+            return real_call(name, *args)
+        _lib.call = counting
+    try:
+        prev = ops.set_precision("bf16-mixed")
+        try:
+            mod.optimizer.zero_grad()
+            ops.prep_flat_weights(mod.flat.data)
+            loss = mod.training_step((x, torch.zeros(4, 1, dtype=torch.long, device=dev)), 0, eps=eps)
+            loss.backward()
+            ops.flat_weights_stale()
+        finally:
+            ops.restore_math_mode(prev)
+        torch.cuda.synchronize()
+    finally:
+        ops.DYPACK = saved
+        _lib.call = real_call
+    return mod.flat.grad.detach().double().cpu(), mod.flat
+
+
+def test_bf16_step_with_gn_packed_dy_matches_pack_pass(dev):
+    """the same bf16-mixed step with the conv output gradients packed by the GroupNorm backward and by the separate
+    pack pass: identical packed operands, so only the bias gradients' summation order differs."""
+    c_fused, c_pass = {}, {}
+    g_fused, flat = _model_grads(dev, True, c_fused)
+    g_pass, _ = _model_grads(dev, False, c_pass)
+    assert c_fused.get("mvae_group_norm_bwd_pack_nhwc", 0) >= 4
+    assert c_fused.get("mvae_pack_bf16_colsum", 0) + c_fused["mvae_group_norm_bwd_pack_nhwc"] == \
+        c_pass.get("mvae_pack_bf16_colsum", 0)
+    rel = float((g_fused - g_pass).norm() / g_pass.norm())
+    assert rel < 1e-5, rel
+    for p, off, name in zip(flat.params, flat.offsets, flat.names):
+        a, b = g_fused[off:off + p.numel()], g_pass[off:off + p.numel()]
+        assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max())), name
