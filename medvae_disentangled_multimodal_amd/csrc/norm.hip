@@ -764,9 +764,11 @@ __device__ __forceinline__ void gn_bwd_unit(const GnArgs& a, int SC, int u, cons
       sm.gk3[gl * cpg + j] = k3;
     }
   }
-  // the residual branch's gradient: loaded here, its latency behind the finalize barrier
-  float4 av[IT];
-  gn_res_load<IT>(a.dx_add, a, SC, u, vo, rstep, a.dx_add != nullptr, av);
+  // the residual branch's gradient: loaded here, its latency behind the finalize barrier (IT = 16: in batches of 4
+  // rows in the store loop -- 16 more rows would not fit the registers)
+  constexpr int AV = IT > 8 ? 4 : IT;
+  float4 av[AV];
+  if constexpr (IT <= 8) gn_res_load<IT>(a.dx_add, a, SC, u, vo, rstep, a.dx_add != nullptr, av);
   __syncthreads();
   float q1[4], q2[4], q3[4];
 #pragma unroll
@@ -779,11 +781,26 @@ __device__ __forceinline__ void gn_bwd_unit(const GnArgs& a, int SC, int u, cons
   const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)((__bf16*)a.dxp + un.ubase), (short)0, (int)(un.bytes >> 1), 0x00020000);
   float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t ar = un.rsrc(a.dx_add);
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
+    if constexpr (IT > 8) {
+      if (i % AV == 0) {
+#pragma unroll
+        for (int j = 0; j < AV; ++j) {
+          if (a.dx_add != nullptr) {
+            const gn_u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(ar, vo, (i + j) * rstep, 0);
+            av[j] = float4{__uint_as_float(t.x), __uint_as_float(t.y), __uint_as_float(t.z), __uint_as_float(t.w)};
+          } else {
+            av[j] = float4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+      }
+    }
+    const float4 w = av[i % AV];
     // av is zero when there is no residual-branch gradient; rows past hw: the store is dropped
-    const float4 o{dv[i].x * q1[0] + xv[i].x * q2[0] + q3[0] + av[i].x, dv[i].y * q1[1] + xv[i].y * q2[1] + q3[1] + av[i].y,
-                   dv[i].z * q1[2] + xv[i].z * q2[2] + q3[2] + av[i].z, dv[i].w * q1[3] + xv[i].w * q2[3] + q3[3] + av[i].w};
+    const float4 o{dv[i].x * q1[0] + xv[i].x * q2[0] + q3[0] + w.x, dv[i].y * q1[1] + xv[i].y * q2[1] + q3[1] + w.y,
+                   dv[i].z * q1[2] + xv[i].z * q2[2] + q3[2] + w.z, dv[i].w * q1[3] + xv[i].w * q2[3] + q3[3] + w.w};
     gn_res_store(dr, vo + (unsigned)(i * rstep), gn_bits(o));
     if (a.dxp != nullptr) {  // packed bf16 at half the byte offsets (8-B stores; rows past hw: dropped)
       typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
@@ -800,16 +817,27 @@ __device__ __forceinline__ void gn_bwd_unit(const GnArgs& a, int SC, int u, cons
   }
 }
 
+// IT = 13 (a whole 128-B row segment per unit at the 28x28 levels' 32-channel slabs): no next-unit prefetch -- its
+// registers would not fit
 template <int IT>
 __global__ void __launch_bounds__(GN_RES_NT) gn_bwd_resident_kernel(GnArgs a, int SC, int units, double* __restrict__ pws,
                                                                     float* __restrict__ dx) {
   __shared__ GnBwdSmem sm;
   const int C4 = SC >> 2, rpar = GN_RES_NT / C4, c4 = threadIdx.x & (C4 - 1), rph = threadIdx.x / C4;
   const int G = gridDim.x;
-  float4 xa[IT], da[IT], xb[IT], db[IT];
   const unsigned vo = (unsigned)(rph * a.C + c4 * 4) * 4u;
   const int rstep = rpar * a.C * 4;
   int u = blockIdx.x;
+  if constexpr (IT > 8) {
+    float4 xa[IT], da[IT];
+    for (; u < units; u += G) {
+      gn_res_load<IT>(a.x, a, SC, u, vo, rstep, true, xa);
+      gn_res_load<IT>(a.dy, a, SC, u, vo, rstep, true, da);
+      gn_bwd_unit<IT>(a, SC, u, xa, da, sm, pws, dx);
+    }
+    return;
+  }
+  float4 xa[IT], da[IT], xb[IT], db[IT];
   gn_res_load<IT>(a.x, a, SC, u, vo, rstep, u < units, xa);
   gn_res_load<IT>(a.dy, a, SC, u, vo, rstep, u < units, da);
   while (u < units) {  // ping-pong prefetch of x and dy, as in the forward
@@ -994,6 +1022,10 @@ __global__ void __launch_bounds__(256) gn_param_reduce_kernel(const double* __re
 // 1 streaming only); before any call, MVAE_GN_RESIDENT=0 selects streaming only.
 // Largest slab (of >= 16 channels: 64-B row segments) with <= max_it rows per thread (forward 16: one 128-B
 // row segment per 8 lanes at the 28x28x32 level, 41 -> 33 us; backward 8: two units of x and dy in registers).
+static bool gn_fwd_it13() {
+  static const int v = getenv("MVAE_GN_FWD_IT16") == nullptr;  // experiment knob: the forward's 28x28 levels on 16 rows
+  return v != 0;
+}
 static int gn_resident_slab(int nb, int hw, int C, int G, int* items, int max_it) {
   if (g_gn_path < 0) {
     const char* e = getenv("MVAE_GN_RESIDENT");
@@ -1006,7 +1038,7 @@ static int gn_resident_slab(int nb, int hw, int C, int G, int* items, int max_it
     if ((c4 & (c4 - 1)) || c4 > GN_RES_NT || C % sc || sc % cpg) continue;
     const int rpar = GN_RES_NT / c4, it = (hw + rpar - 1) / rpar;
     if (it > max_it) continue;
-    *items = it <= 4 ? 4 : it <= 8 ? 8 : 16;
+    *items = it <= 4 ? 4 : it <= 8 ? 8 : (it <= 13 && (max_it < 16 || gn_fwd_it13())) ? 13 : 16;  // 13: 28x28 at 32-ch slabs
     return sc;
   }
   return 0;
@@ -1101,10 +1133,12 @@ int mvae_group_norm_fwd_nhwc(const float* x, const float* gamma, const float* be
     a.silu = silu; a.drop_p = drop_p; a.seed = seed; a.y_split = y_split; a.salt = dropout_salt();
     const int units = nb * (c / sc);
     const void* k = it == 4 ? (const void*)gn_fwd_resident_kernel<4>
-                  : it == 8 ? (const void*)gn_fwd_resident_kernel<8> : (const void*)gn_fwd_resident_kernel<16>;
+                  : it == 8 ? (const void*)gn_fwd_resident_kernel<8>
+                  : it == 13 ? (const void*)gn_fwd_resident_kernel<13> : (const void*)gn_fwd_resident_kernel<16>;
     const dim3 grid(gn_res_grid(k, units));
     if (it == 4) hipLaunchKernelGGL(gn_fwd_resident_kernel<4>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, y, mean, rstd, eps);
     else if (it == 8) hipLaunchKernelGGL(gn_fwd_resident_kernel<8>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, y, mean, rstd, eps);
+    else if (it == 13) hipLaunchKernelGGL(gn_fwd_resident_kernel<13>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, y, mean, rstd, eps);
     else hipLaunchKernelGGL(gn_fwd_resident_kernel<16>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, y, mean, rstd, eps);
     return launch_status();
   }
@@ -1209,17 +1243,23 @@ static int gn_bwd(const float* x, const float* dy, const float* gamma, const flo
   a.dxp = (uint2*)dxp;
   a.csp = dbias ? (double*)cs_ws : nullptr;
   int it = 0;
-  int sc = gn_resident_slab(nb, hw, c, groups, &it, 8);
+  static const int bwd_max_it = [] {
+    const char* e = getenv("MVAE_GN_RES_BWD_IT");  // rows per thread allowed in the resident backward (8 or 13)
+    return e ? std::min(13, atoi(e)) : 13;
+  }();
+  int sc = gn_resident_slab(nb, hw, c, groups, &it, bwd_max_it);
   // the backward holds x and dy of two units (2 waves/SIMD): with 64-B row segments (sc < 32) it streams at
   // ~3.1 TB/s, below the streaming kernels on tensors past ~64 MB (c2's 28x28x128 level: 140 vs 124 us)
   if (sc > 0 && sc < 32 && (long long)nb * hw * c * 4 > (64LL << 20)) sc = 0;
   if (sc) {
     double* pws = (double*)workspace;  // [2][C][nb] fp64 (within the [nb][chunks][C][2] partial area)
     const int units = nb * (c / sc);
-    const void* k = it == 4 ? (const void*)gn_bwd_resident_kernel<4> : (const void*)gn_bwd_resident_kernel<8>;
+    const void* k = it == 4 ? (const void*)gn_bwd_resident_kernel<4>
+                  : it == 8 ? (const void*)gn_bwd_resident_kernel<8> : (const void*)gn_bwd_resident_kernel<13>;
     const dim3 grid(gn_res_grid(k, units));
     if (it == 4) hipLaunchKernelGGL(gn_bwd_resident_kernel<4>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, pws, dx);
-    else hipLaunchKernelGGL(gn_bwd_resident_kernel<8>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, pws, dx);
+    else if (it == 8) hipLaunchKernelGGL(gn_bwd_resident_kernel<8>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, pws, dx);
+    else hipLaunchKernelGGL(gn_bwd_resident_kernel<13>, grid, dim3(GN_RES_NT), 0, st, a, sc, units, pws, dx);
     if (dgamma || dbeta)
       hipLaunchKernelGGL(gn_param_reduce_kernel, dim3(c), dim3(256), 0, st, (const double*)pws, nb, c, dgamma, dbeta);
     if (dbias)
