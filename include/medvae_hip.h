@@ -70,6 +70,15 @@ int mvae_set_dropout_salt(const void* salt_dev);
 int mvae_conv2d_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y,
                      int nb, int h, int w_, int cin, int cout, int kh, int kw, int stride, int pad_t,
                      int pad_l, int ho, int wo, int mode, void* stream);
+/* Direct 3x3 / stride-1 / pad-1 convolution at 32 input and 32 output channels (the 28x28 level of the c3 model,
+ * hidden 32; encoder_decoder.py:123-146): a workgroup stages a band of input rows with its halo once into LDS and
+ * runs the 9 taps as 16x16x32 MFMA products from it (no per-K-tile gather). y = conv(x, w) [+ bias][+ residual];
+ * mode | MVAE_CONV_DGRAD_DIRECT: the input gradient instead -- x := dy, y := dx, w = the forward conv's weights
+ * (flipped and transposed inside), no bias / residual / split weights. mode | MVAE_CONV_XSPLIT / MVAE_CONV_WSPLIT as
+ * for mvae_conv2d_nhwc. NHWC fp32, KRSC weights, W <= 62. Arithmetic = the process-wide GEMM math mode. */
+#define MVAE_CONV_DGRAD_DIRECT 512
+int mvae_conv2d_direct32_nhwc(const float* x, const float* w, const float* bias, const float* residual, float* y,
+                              int n, int h, int w_, int mode, void* stream);
 /* mvae_conv2d_nhwc with a split-K workspace (same nn.Conv2d forward / input-gradient semantics): a launch whose
  * output tiles leave most of the chip idle for a partial round (small spatial sizes at wide channels, e.g. the 7x7
  * level at 512 channels of BetaVAE at 28x28) splits K over `workspace` (fp32 partials, summed in a fixed order

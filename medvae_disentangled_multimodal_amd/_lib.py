@@ -27,6 +27,7 @@ SIGNATURES = {
     "mvae_get_math_mode": (I, []),
     "mvae_set_dropout_salt": (I, [P]),
     "mvae_conv2d_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P]),
+    "mvae_conv2d_direct32_nhwc": (I, [P, P, P, P, P, I, I, I, I, P]),
     "mvae_conv2d_ws_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),
     "mvae_conv2d_split_workspace_bytes": (Z, [I, I, I, I, I, I, I]),
     "mvae_conv2d_gnstats_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P]),

@@ -70,6 +70,7 @@ constexpr int MVAE_CONV_XSPLIT = 32;  // conv mode flag: the input activation x 
 constexpr int MVAE_CONV_DYSPLIT = 64;  // wgrad mode flag: the output gradient dy holds split4_bf16 groups
 constexpr int MVAE_CONV_BF16 = 128;    // conv mode flag: the gathered operand and the weights are packed bf16 (PREC 4)
 constexpr int MVAE_CONV_PLANAR = 256;  // conv mode flag: ... are planar 3xBF16 (bf16 hi plane, then lo plane; PREC 5)
+constexpr int MVAE_CONV_DGRAD_DIRECT = 512;  // mvae_conv2d_direct32_nhwc: the input gradient (transposed conv of dy)
 
 // Exact division by a runtime constant d for 0 <= n < 2^31 (Granlund-Montgomery, N = 31):
 // q = (n * m) >> (31 + l), l = ceil(log2 d), m = floor(2^(31+l) / d) + 1 (< 2^32).

@@ -192,6 +192,15 @@ DIRECT_WGRAD = os.environ.get("MVAE_NO_DIRECT_WGRAD") is None
 MVAE_CONV_WSPLIT = 16
 MVAE_CONV_XSPLIT = 32
 MVAE_CONV_DYSPLIT = 64
+MVAE_CONV_DGRAD_DIRECT = 512
+# 3x3 / stride-1 / pad-1 convs at 32 -> 32 channels (c3's 28x28 level): the direct stencil kernel
+# (mvae_conv2d_direct32_nhwc) for the forward and the input gradient instead of the implicit GEMM
+DIRECT32 = os.environ.get("MVAE_NO_DIRECT32") is None
+
+
+def _direct32(g, c: int, co: int, wd: int) -> bool:
+    return (DIRECT32 and c == 32 and co == 32 and g.kh == 3 and g.kw == 3 and g.stride == 1 and not g.upsample and
+            (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and wd <= 62)
 # the output gradient of a conv split once into 3xBF16 hi/lo groups (mvae_split_bf16) and handed pre-split to
 # both of its GEMMs (input gradient: gathered A operand; weight gradient: dY^T A operand). Off by default: measured
 # on c4 (same box, interleaved) the dgrad GEMMs gain 2.5 % but the wgrad GEMMs lose 2.5 % and the split pass
@@ -524,6 +533,9 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
         elif sub:
             _lib.call("mvae_conv2d_upsample_nhwc", x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n,
                       h, wd, c, co, int(split), st)
+        elif gn_part is None and _direct32(g, c, co, wd):
+            _lib.call("mvae_conv2d_direct32_nhwc", x.data_ptr(), wptr, _ptr(b), _ptr(res), y.data_ptr(), n, h, wd,
+                      (MVAE_CONV_WSPLIT if split else 0) | (MVAE_CONV_XSPLIT if x_split else 0), st)
         else:
             mode = (1 if g.upsample else 0) | (MVAE_CONV_WSPLIT if split else 0) | (MVAE_CONV_XSPLIT if x_split else 0)
             if gn_part is not None:
@@ -635,6 +647,12 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
         with _timed("conv_dgrad", flops * 4 / 9, shp, flops):
             _lib.call("mvae_conv2d_nhwc", dya.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
                       4, 4, 2, 1, 1, h, wd, wflag | xflag, st)
+        return dx
+    if _direct32(g, c, co, wd) and _al16(w):
+        # 32 -> 32 channels (c3's 28x28 level): the direct stencil kernel with the flipped, transposed taps
+        with _timed("conv_dgrad", flops, shp):
+            _lib.call("mvae_conv2d_direct32_nhwc", dya.data_ptr(), w.data_ptr(), None, None, dx.data_ptr(), n, h, wd,
+                      MVAE_CONV_DGRAD_DIRECT | xflag, st)
         return dx
     wtp = _weight_t(w, co, g.kh, g.kw, c, int(split), c * g.kh * g.kw * co * 4, st)
     if g.stride == 2 and h % 2 == 0 and wd % 2 == 0 and g.kh <= 4 and g.kw <= 4 and STRIDE2_CLASSES:
