@@ -88,6 +88,17 @@ CASES = {
         optimizer=dict(type="adamw", lr=1e-4, weight_decay=1e-4, betas=[0.9, 0.999]),
         clip=1.0,
     ),
+    # Config 1 exactly (chest_base_vae at 28x28x1 with the 3-level ch_mult, hidden 128, z 256, two ResnetBlocks per
+    # level; configs/experiment/chest_base_vae.yaml, BASELINE config 1).
+    "base_c1_full": dict(
+        cls="BaseVAE",
+        kwargs=dict(input_channels=1, latent_dim=256, hidden_channels=128, ch_mult=[1, 2, 4],
+                    num_res_blocks=2, attn_resolutions=[16], dropout=0.0, resolution=28),
+        batch=2, cond="none", full=True,
+        loss=dict(type="vae", recon_loss_type="mse", kl_weight=1.0, recon_weight=1.0),
+        optimizer=dict(type="adamw", lr=2e-4, weight_decay=1e-4, betas=[0.9, 0.999]),
+        clip=1.0,
+    ),
     # Config 3 architecture (disentangled_multi_modal_cvae_quick) at B=16: every modality, repeated
     # modalities, and out-of-range ids 7, 9 and 17 (routing clamps them to 4; the separation loss keeps
     # each as its own centroid, so ids >= 16 must work too).
@@ -125,6 +136,8 @@ FULL_GRADS = {
                      "encoder.norm_out.weight"],
     "beta_c2_full": ["encoder.conv_in.weight", "decoder.conv_out.weight", "decoder.mid.attn_1.proj_out.bias",
                      "encoder.down.1.block.0.nin_shortcut.weight", "decoder.up.0.block.2.norm2.weight"],
+    "base_c1_full": ["encoder.conv_in.weight", "decoder.conv_out.weight", "decoder.mid.attn_1.v.bias",
+                     "encoder.down.2.block.1.norm2.bias", "decoder.up.1.block.2.conv1.bias"],
     "dis_c3_b16": ["modality_input_projectors.0.weight", "modality_output_projectors.3.weight",
                    "modality_decoders.4.0.weight", "modality_decoders.1.2.bias", "modality_decoders.2.2.weight",
                    "encoder.conv_in.weight"],

@@ -165,7 +165,7 @@ def test_state_dict_roundtrip_and_names():
         assert torch.equal(sd[k], ref[k]), k
 
 
-@pytest.mark.parametrize("name", ["cvae_c4_full", "beta_c2_full", "dis_c3_b16"])
+@pytest.mark.parametrize("name", ["cvae_c4_full", "beta_c2_full", "dis_c3_b16", "base_c1_full"])
 def test_training_step_exact_fp32_matches_reference(name):
     """The trainer's "32-exact" precision (every conv / bmm on the f32-input MFMA, no operand rounding -- the
     arithmetic of the bench's c4x line) against the reference at the exact BASELINE architectures: outputs, loss
