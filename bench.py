@@ -536,7 +536,7 @@ def main():
     extra, parity = None, None
     if full:  # the other BASELINE configs on the same box, same clock (their own images/s; not summed)
         extra = {}
-        for c in ("c2", "c3", "c5", "c4x"):
+        for c in ("c1", "c2", "c3", "c5", "c4x"):
             # c4x (exact fp32, ~4x the 3xBF16 step time): a short timed region, and the c4 line's CPU baseline (same
             # model and step on the CPU)
             short = c == "c4x"
