@@ -133,3 +133,34 @@ def test_overlap_with_rank_dependent_unused_parameters():
     ga0 = a.bias.grad.clone()
     assert torch.allclose(res["b_w"], gb0, atol=1e-6)         # only rank 0 contributed
     assert torch.allclose(res["a_b"], ga0 + ga1, atol=1e-6)   # summed over ranks
+
+
+def test_dp_capture_mode_selection(monkeypatch):
+    """fit_step_graphed's data-parallel capture mode: single process -> "single"; RCCL ("nccl") ->
+    the whole step with its bucket all-reduces in one graph; any other backend (gloo cannot be captured) -> two graphs
+    around an eager exchange; MVAE_DP_CAPTURE forces either."""
+    from medvae_disentangled_multimodal_amd.lightning_module import VAELightningModule
+
+    class PG:
+        def __init__(self, world, backend):
+            self.world, self._b = world, backend
+
+        def backend(self):
+            return self._b
+
+    mod = VAELightningModule.__new__(VAELightningModule)
+    monkeypatch.delenv("MVAE_DP_CAPTURE", raising=False)
+    mod.process_group = None
+    assert mod._dp_capture_mode() == "single"
+    mod.process_group = PG(1, "nccl")
+    assert mod._dp_capture_mode() == "single"
+    mod.process_group = PG(2, "nccl")
+    assert mod._dp_capture_mode() == "whole"
+    mod.process_group = PG(2, "gloo")
+    assert mod._dp_capture_mode() == "split"
+    monkeypatch.setenv("MVAE_DP_CAPTURE", "split")
+    mod.process_group = PG(8, "nccl")
+    assert mod._dp_capture_mode() == "split"
+    monkeypatch.setenv("MVAE_DP_CAPTURE", "whole")
+    mod.process_group = PG(2, "gloo")
+    assert mod._dp_capture_mode() == "whole"
