@@ -533,7 +533,7 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
         elif sub:
             _lib.call("mvae_conv2d_upsample_nhwc", x.data_ptr(), wg.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), n,
                       h, wd, c, co, int(split), st)
-        elif gn_part is None and _direct32(g, c, co, wd):
+        elif gn_part is None and _direct32(g, c, co, wd) and _al16(x, wg) and (res is None or _al16(res)):
             _lib.call("mvae_conv2d_direct32_nhwc", x.data_ptr(), wptr, _ptr(b), _ptr(res), y.data_ptr(), n, h, wd,
                       (MVAE_CONV_WSPLIT if split else 0) | (MVAE_CONV_XSPLIT if x_split else 0), st)
         else:
@@ -648,7 +648,7 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
             _lib.call("mvae_conv2d_nhwc", dya.data_ptr(), wt.data_ptr(), None, None, dx.data_ptr(), n, ho, wo, co, c,
                       4, 4, 2, 1, 1, h, wd, wflag | xflag, st)
         return dx
-    if _direct32(g, c, co, wd) and _al16(w):
+    if _direct32(g, c, co, wd) and _al16(w, dya):
         # 32 -> 32 channels (c3's 28x28 level): the direct stencil kernel with the flipped, transposed taps
         with _timed("conv_dgrad", flops, shp):
             _lib.call("mvae_conv2d_direct32_nhwc", dya.data_ptr(), w.data_ptr(), None, None, dx.data_ptr(), n, h, wd,
