@@ -832,6 +832,34 @@ class DyPack:
         return out
 
 
+# Input and weight gradients of one conv on two streams: the weight-gradient GEMM runs on a per-device side stream
+# while the input-gradient GEMM runs on the current one, so the partial last wave of either fills with the other's
+# tiles. Only for convs up to MVAE_BWD_OVERLAP_MAX_GF GFLOP (default 200): c3 +1.7 %, c2 +0.6 % img/s; the c4 convs
+# (1.2 TFLOP each) already fill the chip and lose 3 % to the contention; c1 / c5 neutral (profiles/r04_bwd_overlap_ab.txt).
+# MVAE_BWD_OVERLAP=0: one stream. Streams and events are made outside graph capture and reused.
+BWD_OVERLAP = os.environ.get("MVAE_BWD_OVERLAP", "1") != "0"
+BWD_OVERLAP_MAX_FLOPS = float(os.environ.get("MVAE_BWD_OVERLAP_MAX_GF", "200")) * 1e9
+_SIDE = {}
+
+
+def _bwd_side(t: torch.Tensor):
+    if not BWD_OVERLAP or not t.is_cuda:
+        return None
+    side = _SIDE.get(t.device)
+    if side is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        side = _SIDE[t.device] = (torch.cuda.Stream(t.device), torch.cuda.Event(), torch.cuda.Event())
+    return side
+
+
+def _overlap_ok(x, dy, g) -> bool:
+    n, c, _, _ = x.shape
+    _, co, ho, wo = dy.shape
+    # (image-side convs -- cout 3 / latent channels -- run memory-bound special kernels: c4 lost 0.35 % overlapping them)
+    return not g.pointwise and min(c, co) >= 32 and 2.0 * n * ho * wo * co * c * g.kh * g.kw <= BWD_OVERLAP_MAX_FLOPS
+
+
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, geom: ConvGeom, res_sink=None, x_sink=None, gn_part=None,
@@ -890,11 +918,9 @@ class Conv2dFn(torch.autograd.Function):
             if not bias_done:
                 db_ret = None
         dys = split_dy(dy) if not g.pointwise and not _subpixel_upsample(g) and dyb is None else None
-        if ctx.needs_input_grad[0]:
-            dx = conv2d_dgrad_raw(dy, w, x.shape, g, link if ctx.x_sink is None else None, dys=dys, dyb=dyb)
-            if ctx.x_sink is not None and ctx.x_sink.park(dx):
-                dx = None
-        if ctx.needs_input_grad[1]:
+
+        def wgrad():
+            nonlocal dw_ret, bias_done
             tgt = _main_grad(ctx.weight_ref)
             btgt = _main_grad(ctx.bias_ref) if want_b and not bias_done else None
             want_b_w = want_b and not bias_done
@@ -907,6 +933,27 @@ class Conv2dFn(torch.autograd.Function):
             else:
                 dw_ret = torch.empty_like(w, memory_format=CL)
                 conv2d_wgrad_raw(dy, x, dw_ret, 0.0, g, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16)
+
+        side = _bwd_side(dy) if ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and \
+            _main_grad(ctx.weight_ref) is not None and _overlap_ok(x, dy, g) else None
+        if side is not None:
+            # the weight gradient on the side stream, concurrent with the input gradient (their scratch buffers are
+            # disjoint: "ws" / "xbf" vs "wt" / "wcls" / "convsplit"); joined before returning
+            stream, ev_fork, ev_join = side
+            main = torch.cuda.current_stream(dy.device)
+            ev_fork.record(main)
+            stream.wait_event(ev_fork)
+            with torch.cuda.stream(stream):
+                wgrad()
+            ev_join.record(stream)
+        if ctx.needs_input_grad[0]:
+            dx = conv2d_dgrad_raw(dy, w, x.shape, g, link if ctx.x_sink is None else None, dys=dys, dyb=dyb)
+            if ctx.x_sink is not None and ctx.x_sink.park(dx):
+                dx = None
+        if side is not None:
+            main.wait_event(ev_join)
+        elif ctx.needs_input_grad[1]:
+            wgrad()
         if ctx.has_bias and ctx.needs_input_grad[2] and not bias_done:
             tgt = _main_grad(ctx.bias_ref)
             n, co, ho, wo = dy.shape
