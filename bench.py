@@ -499,6 +499,92 @@ def parity_block(dev):
             "seconds": round(time.perf_counter() - t0, 1)}
 
 
+STDOUT_LINE_LIMIT = 8192  # bytes: the driver keeps only the tail of stdout (round 4's 25.8 KB line was not parsed)
+_DTYPE_SHORT = {"bf16": "bf16", "fp32 (exact": "fp32-exact", "fp32 (3xBF16": "fp32-3xbf16"}
+
+
+def _short_dtype(d):
+    for k, v in _DTYPE_SHORT.items():
+        if d and d.startswith(k):
+            return v
+    return d
+
+
+def _compact_roofline(r):
+    """the roofline of one config without notes, PMC detail or per-launch tables: the figures the driver checks"""
+    if not r:
+        return None
+    out = {k: r[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "algorithmic_bytes_per_launch",
+                             "launches_per_step", "avg_launch_us", "gemm_ms_per_step", "instrumented_step_ms")
+           if k in r}
+    out["kernel"] = "gemm3x_kernel"
+    if r.get("by_pass"):  # per pass: [launches, ms per step, TFLOP/s]
+        out["by_pass"] = {k: [v["launches"], v["ms"], v["TFLOP/s"]] for k, v in r["by_pass"].items()}
+    for fam in ("hbm_kernels", "hbm_loss_kernels"):
+        h = r.get(fam)
+        if h:
+            out[fam] = {k: h[k] for k in ("achieved", "peak", "unit", "frac", "ms_per_step", "traffic_over_algorithmic")
+                        if k in h}
+    return out
+
+
+def compact_line(full):
+    """The ONE stdout JSON line (rank 0), at most STDOUT_LINE_LIMIT bytes: the headline fields, the headline config's
+    roofline (no notes / PMC detail), its cpu_baseline, one short entry per extra config and the parity summary. The
+    full record (`full`: notes, PMC traffic detail, per-family tables) goes to the detail file and stderr."""
+    out = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "loss")
+           if k in full}
+    out["roofline"] = _compact_roofline(full.get("roofline"))
+    cb = full.get("cpu_baseline")
+    out["cpu_baseline"] = None if not cb else {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample") if k in cb}
+    if full.get("configs"):
+        cfgs = {}
+        for name, c in full["configs"].items():
+            r = c.get("roofline") or {}
+            e = {"value": c["value"], "ms_per_step": c["ms_per_step"], "steps": c.get("steps"),
+                 "dtype": _short_dtype(c.get("dtype")), "frac": r.get("frac"), "peak": r.get("peak")}
+            if r.get("by_pass"):
+                e["TFLOP/s_by_pass"] = {k: v["TFLOP/s"] for k, v in r["by_pass"].items()}
+            h = r.get("hbm_kernels")
+            if h:
+                e["gn_hbm_frac"] = h.get("frac")
+            cpu = c.get("cpu_baseline")
+            e["cpu_baseline"] = None if not cpu else cpu.get("value")
+            cfgs[name] = e
+        out["configs"] = cfgs
+    p = full.get("parity")
+    if p:
+        out["parity"] = {k: p[k] for k in ("tolerance", "pass", "max_rel_err", "condition_map_bitwise") if k in p}
+        out["parity"]["case"] = "cvae_c4_full"
+    if full.get("detail_file"):
+        out["detail_file"] = full["detail_file"]
+    s = json.dumps(out, separators=(",", ":"))
+    if len(s) > STDOUT_LINE_LIMIT:  # never lose the headline: drop the per-config block first
+        out.pop("configs", None)
+        s = json.dumps(out, separators=(",", ":"))
+    return s
+
+
+def write_detail(full, path):
+    """the full record (every roofline table, note and PMC detail) to `path`; returns the path written (None when it
+    could not be). stderr gets one readable line per config and pass."""
+    for name, c in [(full.get("config", {}).get("model", "head"), full)] + list((full.get("configs") or {}).items()):
+        r = c.get("roofline") or {}
+        bp = " ".join(f"{k}={v['TFLOP/s']}" for k, v in (r.get("by_pass") or {}).items())
+        print(f"[bench detail] {name}: {c.get('value')} img/s, {c.get('ms_per_step')} ms/step, frac {r.get('frac')} of "
+              f"{r.get('peak')} {r.get('unit')}; TF/s by pass: {bp}", file=sys.stderr, flush=True)
+    try:
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(full, f, indent=1)
+        return path
+    except OSError:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -513,6 +599,8 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--detail", action="store_true", help="per-shape GEMM launch timings on stderr")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python (no HIP-graph replay)")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="where the full record (all roofline tables and notes) is written; stdout carries the compact line")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -563,7 +651,8 @@ def main():
             out["configs"] = extra
         if parity is not None:
             out["parity"] = parity
-        print(json.dumps(out), flush=True)
+        out["detail_file"] = write_detail(out, args.detail_out)
+        print(compact_line(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -305,9 +305,18 @@ class VAELightningModule(_Base):
         key = (tuple((tuple(t.shape), t.dtype, t.device) for t in ins), eps is not None, hyper,
                opt.max_grad_norm, getattr(opt, "grad_scale", None), id(opt), id(self.flat), self.precision, mode,
                id(self.process_group))
+        if getattr(self, "_graph_failed", None) == key:  # this step's capture failed before: eager steps
+            return self.fit_step(batch, batch_idx, eps=eps)
         g = getattr(self, "_graph", None)
         if g is None or g["key"] != key:
-            g = self._capture_step(ins, len(batch), batch_idx, key, mode)
+            try:
+                g = self._capture_step(ins, len(batch), batch_idx, key, mode)
+            except RuntimeError as e:  # (e.g. a collective the runtime cannot record): fall back to eager steps
+                import warnings
+                warnings.warn(f"fit_step_graphed: step capture failed ({e}); running eager steps")
+                self._graph_failed = key
+                torch.cuda.synchronize(ins[0].device)
+                return self.fit_step(batch, batch_idx, eps=eps)
         for dst, src in zip(g["inputs"], ins):
             if dst.data_ptr() != src.data_ptr():
                 dst.copy_(src)
@@ -332,11 +341,12 @@ class VAELightningModule(_Base):
         pg = self.process_group
         if pg is None or getattr(pg, "world", 1) == 1:
             return "single"
+        # "whole" (the bucket all-reduces recorded inside the step graph) is opt-in: RCCL capture has not run on this
+        # build's 1-GPU boxes, while "split" is bitwise-tested against the eager DP step (tests/test_gpu_ddp.py)
         forced = os.environ.get("MVAE_DP_CAPTURE")
         if forced in ("whole", "split"):
             return forced
-        backend = pg.backend() if hasattr(pg, "backend") else None
-        return "whole" if backend == "nccl" else "split"
+        return "split"
 
     def _capture_step(self, ins, nb, batch_idx, key, mode="single"):
         dev = ins[0].device

@@ -48,7 +48,9 @@ def nhwc(t: torch.Tensor) -> torch.Tensor:
 
 
 class _Arena:
-    """Per-device scratch buffers reused across launches (all work is ordered on one stream).
+    """Per-device, per-stream scratch buffers reused across launches: the work of one stream is ordered, so a buffer
+    keyed by (name, device, stream) is never used by two kernels at once -- the side-stream weight gradient of the
+    two-stream conv backward (Conv2dFn._backward) gets buffers of its own whatever names it asks for.
 
     A buffer that is outgrown is replaced (and its memory returned to the caching allocator). A captured
     HIP graph bakes in the raw pointers of the buffers it used, so while a capture records (`pinning`
@@ -62,7 +64,8 @@ class _Arena:
         self.pinning = None
 
     def get(self, key: str, nbytes: int, device) -> torch.Tensor:
-        k = (key, str(device))
+        dev = torch.device(device)
+        k = (key, str(dev), torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0)
         t = self.bufs.get(k)
         if t is None or t.numel() < nbytes:
             t = torch.empty(max(int(nbytes * 1.25) + 256, 256), dtype=torch.uint8, device=device)
@@ -843,7 +846,9 @@ _SIDE = {}
 
 
 def _bwd_side(t: torch.Tensor):
-    if not BWD_OVERLAP or not t.is_cuda:
+    # (off while bench.py's instrumented step records per-launch HIP events: concurrent kernels would overlap the
+    # brackets and overstate each launch's duration)
+    if not BWD_OVERLAP or PROFILE is not None or not t.is_cuda:
         return None
     side = _SIDE.get(t.device)
     if side is None:
@@ -909,6 +914,11 @@ class Conv2dFn(torch.autograd.Function):
             dyb, bias_done, db_ret = got
             if not want_b:
                 db_ret = None
+            elif bias_done:
+                bt = _main_grad(ctx.bias_ref)
+                if bt is not None:  # into the flat slot now that dy is known to be the GroupNorm's dx
+                    bt.add_(db_ret)
+                    db_ret = None
         elif ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             # bf16-mixed: pack dy once for both GEMMs; the bias gradient comes out of the same pass
             bt = _main_grad(ctx.bias_ref) if want_b else None
@@ -937,8 +947,8 @@ class Conv2dFn(torch.autograd.Function):
         side = _bwd_side(dy) if ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and \
             _main_grad(ctx.weight_ref) is not None and _overlap_ok(x, dy, g) else None
         if side is not None:
-            # the weight gradient on the side stream, concurrent with the input gradient (their scratch buffers are
-            # disjoint: "ws" / "xbf" vs "wt" / "wcls" / "convsplit"); joined before returning
+            # the weight gradient on the side stream, concurrent with the input gradient (the arena keys its scratch
+            # buffers by stream, so the two never share one); joined before returning
             stream, ev_fork, ev_join = side
             main = torch.cuda.current_stream(dy.device)
             ev_fork.record(main)
@@ -1114,11 +1124,10 @@ class GroupNormFn(torch.autograd.Function):
                 bref = req.bias_ref
                 tgt, bbeta = None, 0.0
                 if bref is not None and bref.requires_grad:
-                    tgt = _main_grad(bref)
-                    if tgt is not None:
-                        bbeta = 1.0
-                    else:
-                        tgt = req.db = torch.empty(c, device=x.device, dtype=torch.float32)
+                    # a private buffer, never the flat gradient slot: the conv adds it there only if DyPack.take()
+                    # accepts dy (a rejected dy -- another branch summed in by autograd -- gets its bias gradient from
+                    # the real dy instead, and nothing partial is left in the slot)
+                    tgt = req.db = torch.empty(c, device=x.device, dtype=torch.float32)
                 csb = _lib.query("mvae_group_norm_colsum_workspace_bytes", n, h * w, c)
                 cs = ARENA.get("gncs", csb, x.device) if tgt is not None else None
                 _lib.call("mvae_group_norm_bwd_pack_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(),

@@ -135,10 +135,105 @@ def test_overlap_with_rank_dependent_unused_parameters():
     assert torch.allclose(res["a_b"], ga0 + ga1, atol=1e-6)   # summed over ranks
 
 
+W8_IDS = ([0, 1, 0, 1, 0, 0, 1, 1, 0, 1, 1, 0, 0, 1, 0, 0, 1, 1, 0, 1, 3, 1, 0, 0, 1, 0, 1, 1, 0, 1, 0, 0],  # step 0
+          [1, 0, 0, 1, 1, 1, 0, 0, 0, 0, 1, 1, 0, 1, 1, 0, 1, 0, 0, 1, 1, 0, 0, 1, 0, 1, 1, 0, 1, 0, 0, 1])  # step 1
+# head 2 is used by no rank (never updated), head 3 only by rank 5 at step 0 (updated on every replica at step 0 only)
+
+
+class _Heads(torch.nn.Module):
+    """A shared trunk and per-modality heads (the disentangled model's routing in miniature)."""
+
+    def __init__(self):
+        super().__init__()
+        self.trunk = torch.nn.Linear(6, 8)
+        self.heads = torch.nn.ModuleList([torch.nn.Linear(8, 3) for _ in range(4)])
+
+    def forward(self, x, ids):
+        h = torch.tanh(self.trunk(x))
+        return torch.stack([self.heads[int(i)](h[j]) for j, i in enumerate(ids)])
+
+
+def _w8_data(step):
+    g = torch.Generator().manual_seed(11 + step)
+    return torch.randn(32, 6, generator=g), torch.randn(32, 3, generator=g), torch.tensor(W8_IDS[step])
+
+
+def _w8_opt_step(model, opt, grads, used_heads, clip):
+    """torch AdamW over the parameters the used-mask keeps (the rest get no update and no step count, like
+    FusedAdam's `used` mask), after the global-norm clip of lightning_module.py:452-466"""
+    for name, p in model.named_parameters():
+        keep = not name.startswith("heads.") or used_heads[int(name.split(".")[1])]
+        p.grad = grads[name].clone() if keep else None
+    torch.nn.utils.clip_grad_norm_([p for p in model.parameters() if p.grad is not None], clip)
+    opt.step()
+
+
+def _worker_w8(rank, world, init_file, out_file):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    from medvae_disentangled_multimodal_amd import ddp
+    torch.manual_seed(300 + rank)  # different init everywhere: the broadcast must fix it
+    model = _Heads()
+    mod = _Mod(model)
+    dp = ddp.DataParallel(mod, bucket_bytes=96)
+    assert mod.optimizer.grad_scale == 1.0 / 8 and len(dp.buckets) > 3
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2, betas=(0.5, 0.999), weight_decay=1e-5)
+    used_log = []
+    for step in range(2):
+        x, y, ids = _w8_data(step)
+        sl = slice(rank * 4, rank * 4 + 4)
+        mod.flat.zero_grad()
+        loss = torch.nn.functional.mse_loss(model(x[sl], ids[sl]), y[sl])
+        dp.begin_backward()
+        loss.backward()
+        dp.allreduce_gradients(mod.flat)
+        present = torch.zeros(4, dtype=torch.bool)
+        present[ids[sl]] = True
+        used = dp.any_across_ranks(present)  # the per-modality used-mask, OR-ed over ranks
+        used_log.append(used.tolist())
+        grads = {n: p._mvae_main_grad * mod.optimizer.grad_scale for n, p in model.named_parameters()}
+        _w8_opt_step(model, opt, grads, used.tolist(), 1.0)
+    mine = mod.flat.data.clone()
+    allp = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allp, mine)
+    if rank == 0:
+        torch.save({"params": mine, "replicas_equal": all(torch.equal(mine, q) for q in allp), "used": used_log},
+                   out_file)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_world8_matches_concatenated_batch_and_replicas_agree():
+    """8 gloo ranks (the node's real width): bucket plan, grad_scale 1/8, rank-dependent unused parameters with the
+    OR-ed used-mask, two AdamW steps; the replicas stay bitwise identical and equal the single-process steps on the
+    concatenated 8x batch."""
+    with tempfile.TemporaryDirectory() as d:
+        init_file = os.path.join(d, "init")
+        out_file = os.path.join(d, "out.pt")
+        mp.spawn(_worker_w8, args=(8, init_file, out_file), nprocs=8, join=True)
+        res = torch.load(out_file, weights_only=True)
+    assert res["replicas_equal"]
+    assert res["used"] == [[True, True, False, True], [True, True, False, False]]
+    torch.manual_seed(300)  # rank 0's initial weights (the broadcast)
+    ref = _Heads()
+    head2 = ref.heads[2].weight.detach().clone()
+    opt = torch.optim.AdamW(ref.parameters(), lr=1e-2, betas=(0.5, 0.999), weight_decay=1e-5)
+    for step in range(2):
+        x, y, ids = _w8_data(step)
+        ref.zero_grad()
+        torch.nn.functional.mse_loss(ref(x, ids), y).backward()
+        used = [bool((ids == h).any()) for h in range(4)]
+        _w8_opt_step(ref, opt, {n: p.grad for n, p in ref.named_parameters()}, used, 1.0)
+    from medvae_disentangled_multimodal_amd.optim import FlatParameters
+    f = FlatParameters(ref, torch.device("cpu"))
+    assert torch.equal(ref.heads[2].weight.detach(), head2)  # never used: never moved
+    err = ((res["params"] - f.data).norm() / f.data.norm()).item()
+    assert err < 1e-5, err
+
+
 def test_dp_capture_mode_selection(monkeypatch):
-    """fit_step_graphed's data-parallel capture mode: single process -> "single"; RCCL ("nccl") ->
-    the whole step with its bucket all-reduces in one graph; any other backend (gloo cannot be captured) -> two graphs
-    around an eager exchange; MVAE_DP_CAPTURE forces either."""
+    """fit_step_graphed's data-parallel capture mode: single process -> "single"; any backend ->
+    "split" (two graphs around an eager exchange: the mode whose run is bitwise-tested); MVAE_DP_CAPTURE=whole records
+    the bucket all-reduces inside the one step graph (RCCL capture, opt-in: never run on this build's 1-GPU boxes)."""
     from medvae_disentangled_multimodal_amd.lightning_module import VAELightningModule
 
     class PG:
@@ -155,7 +250,7 @@ def test_dp_capture_mode_selection(monkeypatch):
     mod.process_group = PG(1, "nccl")
     assert mod._dp_capture_mode() == "single"
     mod.process_group = PG(2, "nccl")
-    assert mod._dp_capture_mode() == "whole"
+    assert mod._dp_capture_mode() == "split"
     mod.process_group = PG(2, "gloo")
     assert mod._dp_capture_mode() == "split"
     monkeypatch.setenv("MVAE_DP_CAPTURE", "split")

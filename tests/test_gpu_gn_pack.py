@@ -113,3 +113,49 @@ def test_bf16_step_with_gn_packed_dy_matches_pack_pass(dev):
     for p, off, name in zip(flat.params, flat.offsets, flat.names):
         a, b = g_fused[off:off + p.numel()], g_pass[off:off + p.numel()]
         assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max())), name
+
+
+def _dypack_rejection_grads(dev, dypack: bool, calls):
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    from medvae_disentangled_multimodal_amd.optim import FlatParameters
+    torch.manual_seed(3)
+    m = torch.nn.ModuleDict(dict(c1=torch.nn.Conv2d(16, 32, 3, padding=1), n=torch.nn.GroupNorm(8, 32),
+                                 c2=torch.nn.Conv2d(32, 16, 3, padding=1))).to(dev)
+    flat = FlatParameters(m, dev)
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 16, 16, 16, generator=g).to(dev).contiguous(memory_format=torch.channels_last)
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1)
+    saved, real_call = ops.DYPACK, _lib.call
+
+    def counting(name, *args):
+        calls[name] = calls.get(name, 0) + 1
+        return real_call(name, *args)
+    ops.DYPACK, _lib.call = dypack, counting
+    prev = ops.set_precision("bf16-mixed")
+    try:
+        y = ops.conv2d(x, m["c1"].weight, m["c1"].bias, geom, gn_stats=True)
+        h = ops.group_norm(y, m["n"].weight, m["n"].bias, 8, silu=True, for_conv=16)
+        out = ops.conv2d(h, m["c2"].weight, m["c2"].bias, geom)
+        # y has a second consumer with no GradSink: autograd sums its gradient into the GroupNorm's dx, so the conv
+        # backward's dy is not the tensor the GroupNorm packed
+        loss = out.square().mean() + (y * 0.25).sum()
+        flat.zero_grad()
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        ops.restore_math_mode(prev)
+        ops.DYPACK, _lib.call = saved, real_call
+    return {n: p._mvae_main_grad.detach().double().cpu().clone() for n, p in m.named_parameters()}
+
+
+def test_dypack_rejected_dy_leaves_no_partial_bias_grad(dev):
+    """when DyPack.take() rejects dy (another branch summed in after the GroupNorm backward), the conv's bias
+    gradient comes from the real dy alone -- the GroupNorm's column sums must not have been added to the flat slot."""
+    c_on, c_off = {}, {}
+    g_on = _dypack_rejection_grads(dev, True, c_on)
+    g_off = _dypack_rejection_grads(dev, False, c_off)
+    assert c_on.get("mvae_group_norm_bwd_pack_nhwc", 0) == 1  # the request was made ...
+    assert c_on.get("mvae_pack_bf16_colsum", 0) == c_off.get("mvae_pack_bf16_colsum", 0)  # ... and rejected
+    for name in g_off:
+        rel = float((g_on[name] - g_off[name]).norm() / g_off[name].norm())
+        assert rel < 1e-6, (name, rel)
