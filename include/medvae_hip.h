@@ -223,6 +223,16 @@ int mvae_attention_small_fwd(const float* q, const float* k, const float* v, flo
 int mvae_attention_small_bwd(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                              float* dq, float* dk, float* dv, int batch, int n, int c, float scale, void* stream);
 
+/* Query-block fused attention for 64 <= n <= 256 tokens, n % 64 == 0, c % 128 == 0 (c4 / c5's 16x16 AttnBlocks and the
+ * 8x8 mid blocks at C = 2048, encoder_decoder.py:83-107): one workgroup per (64-query block, image).
+ * fwd: o = softmax(q k^T * scale, dim=2) v in one launch; p [batch][n][n] receives P (the backward's saved tensor).
+ * bwd: from P and dout: dq = dS k and ds [batch][n][n] = scale * P o (dP - rowsum(P o dP)), dP = dout v^T, in one
+ * launch; dv = P^T dout and dk = ds^T q are left to mvae_gemm_strided_batched (sums over every query block). */
+int mvae_attention_tile_fwd(const float* q, const float* k, const float* v, float* o, float* p, int batch, int n, int c,
+                            float scale, void* stream);
+int mvae_attention_tile_bwd(const float* k, const float* v, const float* dout, const float* p, float* dq, float* ds,
+                            int batch, int n, int c, float scale, void* stream);
+
 /* ---- GroupNorm (+SiLU, +inverted dropout) -------------------------------------------------------
  * Normalize() = nn.GroupNorm(min(32,C), C, eps=1e-6) (encoder_decoder.py:28-33) fused with
  * nonlinearity() (:13-15) and ResnetBlock's nn.Dropout (:163). mean/rstd: [nb*groups].

@@ -59,6 +59,8 @@ SIGNATURES = {
     "mvae_softmax_rows_bwd": (I, [P, P, P, L, I, P]),
     "mvae_attention_small_fwd": (I, [P, P, P, P, P, I, I, I, F, P]),
     "mvae_attention_small_bwd": (I, [P, P, P, P, P, P, P, P, I, I, I, F, P]),
+    "mvae_attention_tile_fwd": (I, [P, P, P, P, P, I, I, I, F, P]),
+    "mvae_attention_tile_bwd": (I, [P, P, P, P, P, P, I, I, I, F, P]),
     "mvae_group_norm_fwd_nhwc": (I, [P, P, P, P, P, P, I, I, I, I, F, I, F, c_uint64, I, P, Z, P]),
     "mvae_group_norm_fwd_part_nhwc": (I, [P, P, P, P, P, P, P, I, I, I, I, F, I, F, c_uint64, I, P, Z, P]),
     "mvae_group_norm_bwd_nhwc": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, c_uint64, P, Z, P]),

@@ -41,7 +41,11 @@ namespace mvae {
 enum { A_ROWK = 0, A_COLM = 1, A_CONV_FWD = 2, A_CONV_UPS = 3, A_CONV_DGRAD = 4, A_CONV_SUBPIX = 5, A_COLM_PIX = 6,
        A_CONV_FWD_SPLIT = 7, A_CONV_DGRAD_SPLIT = 8, A_COLM_SPLIT = 9 };
 enum { B_ROWK = 0, B_COLN = 1, B_WGRAD_FWD = 2, B_WGRAD_UPS = 3, B_WGRAD_SUBPIX = 4, B_ROWK_SPLIT = 5,
-       B_WGRAD_FWD_SPLIT = 6 };
+       B_WGRAD_FWD_SPLIT = 6, B_WGRAD_P2 = 7, B_WGRAD_P2_SPLIT = 8 };
+// B_WGRAD_P2(_SPLIT): the weight gradient's im2col gather of a stride-1 conv whose output is the input's size and whose
+// H and W are powers of two (the c4 / c5 levels 64, 32, 16, 8): the source pixel of output pixel p through tap (r, s) is
+// p + (r - pad_t) W + (s - pad_l), valid where h + r - pad_t and w + s - pad_l stay inside the image, and h, w come from p
+// by shift and mask -- no per-K-tile division or stepping (GemmArgs::lw = log2 W)
 // MODE_SUBPIX: one parity class (ph, pw) of "nearest-x2 upsample then 3x3 conv" as a stride-1 2x2 conv
 // on the low-resolution input whose padding shifts with the parity: pad = pad_t - ph (batch entry
 // bidx = 2*ph + pw carries the class)
@@ -102,6 +106,7 @@ struct GemmArgs {
   unsigned a_lo = 0, b_lo = 0;  // PREC 5: byte offset of the operand's lo plane from its hi plane
   // gather geometry: source X is [nb][H][W][Cx]; output pixels are [nb][Ho][Wo]
   int H, W, Cx, Ho, Wo, R, S, stride, stride_shift, pad_t, pad_l;
+  int lw = 0;  // log2 W (B_WGRAD_P2 gathers)
   int tiles_m, tiles_n;
   Magic mg_cx, mg_s, mg_hw, mg_wo;  // divisions by Cx, S, Ho*Wo, Wo (gather index decomposition)
   // conv K-order permutation (perm_rs = R*S, 1 = identity; needs Cx % 32 == 0): K-tile t covers channel
@@ -116,6 +121,10 @@ struct GemmArgs {
   int sub_w2 = 0, sub_par = 0;
   int out_remap = 0;  // epilogue writes C row sub_pixel(m) (conv outputs); else row m
   int vec_epi = 0;    // set by launch_cfg: 16-B epilogue through LDS is legal (see gemm3x_kernel)
+  // tile order within one split: the N tiles are cut into xcd_groups column groups and the tiles ordered (group, m,
+  // n in group), so the contiguous run of tiles an XCD gets spans fewer B panels (1 = plain row-major order; set by
+  // launch_cfg from MVAE_XCD_GROUPS when 0)
+  int xcd_groups = 0;
   // GroupNorm statistics of the output for the following Normalize (16-B epilogue only): per 32-row block
   // and 4-channel group, {sum y, sum y^2} in fp64 at gn_part[((row/32) * (N/4) + col/4) * 2]
   double* gn_part = nullptr;
@@ -762,6 +771,64 @@ struct LoadWgradX {
   }
 };
 
+// COL image of the weight gradient's B operand for B_WGRAD_P2(_SPLIT) (see the enum): element (n = (r*S+s)*Cx + c,
+// k = pixel p) = X[p + (r - pad_t) W + (s - pad_l)][c] where the shifted pixel stays in the image. A lane's 4 columns
+// are one tap and 4 channels for the whole launch (tap offset `ldelta` fixed at init); a k-row (pixel) needs only a mask
+// and a shift for its (h, w) -- wave-uniform when C4 % 64 == 0 -- instead of LoadWgradX's division and row stepping
+template <int ROWS, int NT, int PREC, bool PRESPLIT>
+struct LoadWgradXP2 {
+  static constexpr bool COL = true;
+  static constexpr int C4 = ROWS / 4;
+  static constexpr int NS = (BK * C4 + NT - 1) / NT;
+  __amdgpu_buffer_rsrc_t rs;
+  int c4, kr, krw, k, dr, ds;
+  unsigned ldelta, cx4;
+  bool nv;
+  float4 v[NS];
+  __device__ void init(const GemmArgs& a, const float* x, int row0, int kb, int tid, int) {
+    rs = make_rsrc(x, a.b_bytes);
+    k = kb; c4 = tid % C4; kr = tid / C4;
+    const int n = row0 + c4 * 4;
+    nv = n < a.N;
+    const int nn = nv ? n : 0;
+    const int tap = nn / a.Cx, c = nn - tap * a.Cx;
+    const int r = tap / a.S, s = tap - r * a.S;
+    dr = r - a.pad_t;
+    ds = s - a.pad_l;
+    ldelta = (unsigned)(((dr * a.W + ds) * a.Cx + c) * 4);  // (wraps for negative shifts; used only when valid)
+    cx4 = (unsigned)a.Cx * 4u;
+    krw = (C4 % 64 == 0) ? __builtin_amdgcn_readfirstlane(kr) : kr;
+  }
+  __device__ void prep(const GemmArgs&) {}
+  __device__ void load_slot(const GemmArgs& a, int i) {
+    const int krow = kr + i * (NT / C4);
+    const int p = k + krw + i * (NT / C4);
+    const int w = p & (a.W - 1), h = (p >> a.lw) & (a.H - 1);
+    const bool ok = (krow < BK) & (p < a.K) & nv & ((unsigned)(h + dr) < (unsigned)a.H) &
+                    ((unsigned)(w + ds) < (unsigned)a.W);
+    v[i] = bload4(rs, ok ? (unsigned)p * cx4 + ldelta : OOB);
+  }
+  __device__ void store_slot(__bf16* img, int i) {
+    constexpr int P_ = Img<ROWS, true>::PITCH;
+    const int krow = kr + i * (NT / C4);
+    if (krow < BK) {
+      if constexpr (PRESPLIT)
+        st_presplit<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
+      else
+        st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
+    }
+  }
+  __device__ void advance() { k += BK; }
+  __device__ void load(const GemmArgs& a) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) load_slot(a, i);
+  }
+  __device__ void store(__bf16* img) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) store_slot(img, i);
+  }
+};
+
 // ------------------------------------------------------------------------------------------
 // LDS-DMA operand staging (buffer_load_dwordx4 ... lds): no staging registers, no VALU split, no ds_write.
 //   PREC 4 (bf16-mixed): operands STORED as packed bf16 by their producers; 64-deep stages.
@@ -1025,6 +1092,48 @@ struct DmaWgradX {
   __device__ void advance() { k += KT; }
 };
 
+// DmaWgradX for B_WGRAD_P2 (stride 1, output = input size, H and W powers of two): a k-row's source is its own pixel
+// shifted by the lane's fixed tap offset, valid by a mask-and-shift test of (h, w) -- no divisions per stage
+template <int ROWS, int NT, int KT>
+struct DmaWgradXP2 {
+  using S = DmaColShape<ROWS, NT, KT>;
+  __amdgpu_buffer_rsrc_t rs[2];
+  int kr0, k, K, w, dr, ds;
+  unsigned ldelta, cx2;
+  bool nv;
+  unsigned off_[S::NI];
+  bool ok_[S::NI];
+  __device__ void init(const GemmArgs& a, const __bf16* x, int row0, int kb, int tid, int) {
+    plane_rsrc(rs, x, a.b_bytes, a.b_lo);
+    const int lane = tid & 63;
+    w = tid >> 6;
+    kr0 = w * S::KPI + lane / S::CPR;
+    const int lc = (lane % S::CPR) ^ (dcswz<ROWS>(kr0) >> 3);
+    const int n = row0 + lc * 8;
+    nv = n < a.N;
+    const int nn = nv ? n : 0;
+    const int tap = nn / a.Cx, c = nn - tap * a.Cx;
+    const int r = tap / a.S, s = tap - r * a.S;
+    dr = r - a.pad_t;
+    ds = s - a.pad_l;
+    ldelta = (unsigned)(((dr * a.W + ds) * a.Cx + c) * 2);
+    cx2 = (unsigned)a.Cx * 2u;
+    k = kb; K = a.K;
+  }
+  __device__ void prep(const GemmArgs& a) {
+#pragma unroll
+    for (int i = 0; i < S::NI; ++i) {
+      const int p = k + kr0 + i * S::NW * S::KPI;
+      const int ww = p & (a.W - 1), h = (p >> a.lw) & (a.H - 1);
+      ok_[i] = nv & (p < K) & ((unsigned)(h + dr) < (unsigned)a.H) & ((unsigned)(ww + ds) < (unsigned)a.W);
+      off_[i] = (unsigned)p * cx2 + ldelta;
+    }
+  }
+  __device__ unsigned src(int i) const { return ok_[i] ? off_[i] : OOB; }
+  __device__ void issue(const GemmArgs&, __bf16* img, int i, int pl_) { dma16(rs[pl_], img + (i * S::NW + w) * 512, src(i)); }
+  __device__ void advance() { k += KT; }
+};
+
 // Fragment reads of the DMA main loop as inline asm: the compiler then neither sinks them to just ahead of their
 // MFMAs nor waits for the in-flight LDS-DMA before them (it cannot tell a transpose read of stage t from the DMA
 // writing stage t+1); the loop places its own counted lgkmcnt waits (LDS reads return in order).
@@ -1078,6 +1187,8 @@ template <int ROWS, int NT, int KT>
 struct DmaLoader<B_WGRAD_FWD, ROWS, NT, false, KT> : DmaWgradX<ROWS, NT, MODE_FWD, KT> {};
 template <int ROWS, int NT, int KT>
 struct DmaLoader<B_WGRAD_SUBPIX, ROWS, NT, false, KT> : DmaWgradX<ROWS, NT, MODE_SUBPIX, KT> {};
+template <int ROWS, int NT, int KT>
+struct DmaLoader<B_WGRAD_P2, ROWS, NT, false, KT> : DmaWgradXP2<ROWS, NT, KT> {};
 
 // one MFMA product step: 3xBF16 (lo*hi + hi*lo + hi*hi, small terms first) or plain bf16
 __device__ __forceinline__ f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
@@ -1154,6 +1265,10 @@ template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<8, ROWS, VEC, NT, true, PREC> : LoadConvA<ROWS, VEC, NT, MODE_DGRAD, PREC, true> {};
 template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<9, ROWS, VEC, NT, true, PREC> : LoadColK<ROWS, VEC, NT, true, PREC, true> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<B_WGRAD_P2, ROWS, VEC, NT, false, PREC> : LoadWgradXP2<ROWS, NT, PREC, false> {};
+template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<B_WGRAD_P2_SPLIT, ROWS, VEC, NT, false, PREC> : LoadWgradXP2<ROWS, NT, PREC, true> {};
 
 template <int BM, int BN, int WGM, int WGN, int AK, int VA, int BKIND, int VB, int PREC>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
@@ -1186,7 +1301,19 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   }
   const int z = lin / ntile;
   const int tile = lin - z * ntile;
-  const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+  int tm, tn;
+  if (a.xcd_groups > 1 && a.tiles_n > 1) {  // grouped order (GemmArgs::xcd_groups), bijective on [0, ntile)
+    const int gw = (a.tiles_n + a.xcd_groups - 1) / a.xcd_groups;
+    const int ng = (a.tiles_n + gw - 1) / gw;
+    const int g = min(tile / (a.tiles_m * gw), ng - 1);
+    const int rem = tile - g * a.tiles_m * gw;
+    const int width = g == ng - 1 ? a.tiles_n - g * gw : gw;
+    tm = rem / width;
+    tn = g * gw + (rem - tm * width);
+  } else {
+    tm = tile / a.tiles_n;
+    tn = tile - tm * a.tiles_n;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
   const int bidx = z / a.splits, split = z - bidx * a.splits;
   const int kb = split * a.k_split;
@@ -1215,7 +1342,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
     // clock, which no issue order recovers.)
     constexpr int KT = PREC == 5 ? 32 : 64;
     constexpr int NPL = PREC == 5 ? 2 : 1;  // LDS images per operand (hi, lo)
-    constexpr bool ACOL = AK == A_COLM, BCOL = BKIND == B_WGRAD_FWD || BKIND == B_WGRAD_SUBPIX;
+    constexpr bool ACOL = AK == A_COLM, BCOL = BKIND == B_WGRAD_FWD || BKIND == B_WGRAD_SUBPIX || BKIND == B_WGRAD_P2;
     static_assert(ACOL == BCOL && MF == (ACOL ? 32 : 16), "DMA main loop: ROW x ROW (MF 16) or COL x COL (MF 32)");
     using DA = DmaLoader<AK == A_ROWK ? 0 : AK, BM, NT, true, KT>;
     using DB = DmaLoader<BKIND == B_ROWK ? 0 : BKIND, BN, NT, false, KT>;
@@ -1855,6 +1982,13 @@ inline int choose_tile(const GemmArgs& a, bool allow_big, bool can_split) {
 }
 
 inline bool al16(const void* p);
+inline int xcd_groups_env() {  // experiment knob: MVAE_XCD_GROUPS=G orders the tiles in G column groups
+  static int v = [] {
+    const char* e = getenv("MVAE_XCD_GROUPS");
+    return e ? std::max(1, atoi(e)) : 1;
+  }();
+  return v;
+}
 // pre-split (3xBF16 value-split) operands cannot feed the exact-fp32 GEMM
 inline bool split_forbidden() { return math_mode() == MATH_FP32; }
 inline bool vec_epi_disabled() {
@@ -1876,12 +2010,13 @@ void launch_cfg(GemmArgs& a, hipStream_t st) {
 #endif
   a.tiles_m = cdiv(a.M, BM);
   a.tiles_n = cdiv(a.N, BN);
+  if (a.xcd_groups <= 0) a.xcd_groups = xcd_groups_env();
   a.vec_epi = a.splits == 1 && !a.out_remap && (a.N & 3) == 0 && (a.ldc & 3) == 0 && (a.sC & 3) == 0 && al16(a.C) &&
               (!a.res || ((a.ldr & 3) == 0 && (a.sR & 3) == 0 && al16(a.res))) && (!a.bias || al16(a.bias)) &&
               !vec_epi_disabled();
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splits);
   constexpr bool presplit = AK == A_CONV_FWD_SPLIT || AK == A_CONV_DGRAD_SPLIT || AK == A_COLM_SPLIT ||
-                            BKIND == B_ROWK_SPLIT || BKIND == B_WGRAD_FWD_SPLIT;
+                            BKIND == B_ROWK_SPLIT || BKIND == B_WGRAD_FWD_SPLIT || BKIND == B_WGRAD_P2_SPLIT;
   const int mm = math_mode();
   if constexpr (PO >= 0)
     hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, PO>), grid, dim3(64 * WGM * WGN), 0, st, a);

@@ -70,6 +70,12 @@ static void ups_wgrad_shape(GemmArgs& a, int nb, int h, int wd, int cin, int cou
 }
 static size_t ups_part_bytes(const GemmArgs& a) { return (size_t)a.batch * a.splits * a.M * a.N * sizeof(float); }
 
+static bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+static bool wgrad_p2_enabled() {  // MVAE_NO_WGRAD_P2=1: the general gather (LoadWgradX / DmaWgradX) everywhere
+  static const bool v = getenv("MVAE_NO_WGRAD_P2") == nullptr;
+  return v;
+}
+
 static void wgrad_shape(GemmArgs& a, int nb, int cin, int cout, int kh, int kw, int ho, int wo) {
   a.M = cout; a.N = kh * kw * cin; a.K = nb * ho * wo; a.batch = 1;
 }
@@ -138,8 +144,17 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
     plan_splits(a, cfg, workspace, workspace_bytes - bias_bytes);
     // bias partials live after the split-K partials
     a.bias_ws = dbias ? (float*)((char*)workspace + ((splitk_ws_bytes(a) + 255) & ~(size_t)255)) : nullptr;
+    // stride-1 "same" convs at power-of-two H, W: the shift-and-mask im2col gather (B_WGRAD_P2)
+    const bool p2 = wgrad_p2_enabled() && mode == 0 && stride == 1 && ho == h && wo == wd && pow2(h) && pow2(wd);
+    if (p2) {
+      a.lw = 0;
+      while ((1 << a.lw) < wd) ++a.lw;
+    }
     if (bf) {
-      wgrad_dma(B_WGRAD_FWD, a, st, cfg, pln ? 5 : 4);
+      wgrad_dma(p2 ? B_WGRAD_P2 : B_WGRAD_FWD, a, st, cfg, pln ? 5 : 4);
+    } else if (p2 && !dysplit && va && (xsplit || vb)) {
+      if (xsplit) launch_big<A_COLM, 4, B_WGRAD_P2_SPLIT, 4>(a, st, cfg);
+      else launch_big<A_COLM, 4, B_WGRAD_P2, 4>(a, st, cfg);
     } else if (dysplit) {
       if (xsplit) launch_big<A_COLM_SPLIT, 4, B_WGRAD_FWD_SPLIT, 4>(a, st, cfg);
       else if (mode == 0 && vb) launch_big<A_COLM_SPLIT, 4, B_WGRAD_FWD, 4>(a, st, cfg);

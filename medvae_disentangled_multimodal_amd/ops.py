@@ -1218,6 +1218,17 @@ def _attn_use_fused(q, n: int, c: int) -> bool:
     return _attn_small_ok(q, n, c) and c <= ATTN_FUSED_MAXC
 
 
+# query-block fused attention (csrc/attn_tile.hip) for 64 <= n <= 256 tokens, n % 64 == 0, C % 128 == 0: c4 / c5's
+# 16x16 level (n = 256, C = 1024) and, past ATTN_FUSED_MAXC, the 8x8 mid blocks (n = 64, C = 2048). Forward one launch
+# (scores, softmax and P V in one workgroup per 64 queries; P saved for the backward); backward one launch for dP, dS and
+# dQ plus the two batched GEMMs dV = P^T dO and dK = dS^T Q. MVAE_NO_ATTN_TILE=1 restores the unfused path.
+ATTN_TILE = os.environ.get("MVAE_NO_ATTN_TILE") is None
+
+
+def _attn_use_tile(q, n: int, c: int) -> bool:
+    return ATTN_TILE and 64 <= n <= 256 and n % 64 == 0 and c % 128 == 0 and _al16(q) and q.shape[0] <= 65535
+
+
 class AttnCoreFn(torch.autograd.Function):
     """softmax(q k^T * C^-1/2, dim=2) v over the h*w tokens of each image (encoder_decoder.py:90-103). n <= 64 (the
     7x7 / 8x8 mid blocks): the fused single-tile kernels, one launch per direction with the scores in LDS and only the
@@ -1244,6 +1255,14 @@ class AttnCoreFn(torch.autograd.Function):
             return o
         ctx.fused = False
         s = torch.empty((b, n, n), device=q.device, dtype=torch.float32)
+        ctx.tile = _attn_use_tile(q, n, c)
+        if ctx.tile:  # S, softmax and P V in one launch; P (s) saved for the backward
+            o = torch.empty_like(q, memory_format=CL)
+            with _timed("attn_gemm", 4.0 * n * n * c * b, (n, c, n, b)):
+                _lib.call("mvae_attention_tile_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                          s.data_ptr(), b, n, c, scale, st)
+            ctx.save_for_backward(q, k, v, s)
+            return o
         _gemm(0, 1, n, n, c, scale, q, c, n * c, k, c, n * c, 0.0, s, n, n * n, b, st)
         _lib.call("mvae_softmax_rows", s.data_ptr(), s.data_ptr(), b * n, n, st)
         o = torch.empty_like(q, memory_format=CL)
@@ -1273,6 +1292,19 @@ class AttnCoreFn(torch.autograd.Function):
             with _timed("attn_gemm", 10.0 * n * n * c * b, (n, c, n, b), 8.0 * n * n * c * b):
                 _lib.call("mvae_attention_small_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), do.data_ptr(),
                           p.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), b, n, c, ctx.scale, st)
+            return dq, dk, dv
+        if ctx.tile:
+            if not (do.is_contiguous(memory_format=CL) and _al16(do)):
+                do = do.contiguous(memory_format=CL)
+            dq = torch.empty_like(q, memory_format=CL)
+            ds = torch.empty((b, n, n), device=q.device, dtype=torch.float32)
+            with _timed("attn_gemm", 4.0 * n * n * c * b, (n, c, n, b)):  # dP = dO V^T, dQ = dS K
+                _lib.call("mvae_attention_tile_bwd", k.data_ptr(), v.data_ptr(), do.data_ptr(), p.data_ptr(),
+                          dq.data_ptr(), ds.data_ptr(), b, n, c, ctx.scale, st)
+            dv = torch.empty_like(v, memory_format=CL)
+            _gemm(1, 0, n, c, n, 1.0, p, n, n * n, do, c, n * c, 0.0, dv, c, n * c, b, st)  # dV = P^T dO
+            dk = torch.empty_like(k, memory_format=CL)
+            _gemm(1, 0, n, c, n, 1.0, ds, n, n * n, q, c, n * c, 0.0, dk, c, n * c, b, st)  # dK = dS^T Q (scale in dS)
             return dq, dk, dv
         dp = torch.empty((b, n, n), device=q.device, dtype=torch.float32)
         _gemm(0, 1, n, n, c, 1.0, do, c, n * c, v, c, n * c, 0.0, dp, n, n * n, b, st)   # dP = dO V^T

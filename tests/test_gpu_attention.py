@@ -103,3 +103,69 @@ def test_fused_attention_launch_count(dev):
     finally:
         ops.PROFILE = None
     assert len(rec) == 2
+
+
+# query-block fused attention (csrc/attn_tile.hip): the 16x16 level of c4 / c5 (n = 256, C = 1024), the 8x8 mid blocks
+# at C = 2048 (n = 64), and n = 128 / 192
+TILE_SHAPES = [(2, 1024, 16, 16), (2, 2048, 8, 8), (3, 128, 8, 16), (2, 256, 12, 16)]
+
+
+def _run_tile(dev, q, k, v, go, prec, tile):
+    from medvae_disentangled_multimodal_amd import ops
+    qd, kd, vd = (t.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_() for t in (q, k, v))
+    prev, saved = ops.set_precision(prec), (ops.ATTN_FUSED, ops.ATTN_TILE)
+    ops.ATTN_FUSED, ops.ATTN_TILE = False, tile
+    try:
+        o = ops.attention_core(qd, kd, vd)
+        o.backward(go.to(dev).contiguous(memory_format=torch.channels_last))
+        torch.cuda.synchronize()
+    finally:
+        ops.restore_math_mode(prev)
+        ops.ATTN_FUSED, ops.ATTN_TILE = saved
+    return o, qd.grad, kd.grad, vd.grad
+
+
+@pytest.mark.parametrize("prec", sorted(TOL))
+@pytest.mark.parametrize("shape", TILE_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_tile_attention_matches_float64(dev, shape, prec):
+    from medvae_disentangled_multimodal_amd import ops
+    b, c, h, w = shape
+    assert ops._attn_use_tile(torch.empty((b, 16), device=dev), h * w, c)
+    g = torch.Generator().manual_seed(c + h * w + 1)
+    q, k, v = (torch.randn(shape, generator=g) for _ in range(3))
+    go = torch.randn(shape, generator=g)
+    qi, ki, vi = (t.bfloat16().float() for t in (q, k, v)) if prec == "bf16-mixed" else (q, k, v)
+    ref = _ref(qi, ki, vi, go)
+    got = _run_tile(dev, q, k, v, go, prec, True)
+    tf, tb = TOL[prec]
+    assert _rel(got[0], ref[0]) < tf, ("out", _rel(got[0], ref[0]))
+    for name, a, r in zip(("dq", "dk", "dv"), got[1:], ref[1:]):
+        assert _rel(a, r) < tb, (name, _rel(a, r))
+
+
+@pytest.mark.parametrize("prec", ["32", "bf16-mixed"])
+def test_tile_attention_matches_unfused_path(dev, prec):
+    shape = (2, 1024, 16, 16)
+    g = torch.Generator().manual_seed(12)
+    q, k, v, go = (torch.randn(shape, generator=g) for _ in range(4))
+    tile = _run_tile(dev, q, k, v, go, prec, True)
+    unfused = _run_tile(dev, q, k, v, go, prec, False)
+    tol = 2e-5 if prec == "32" else 5e-3
+    for a, r in zip(tile, unfused):
+        assert _rel(a, r) < tol
+
+
+def test_tile_attention_launch_count(dev):
+    """forward one launch; backward one launch + the dV / dK batched GEMMs (the unfused path: 2 GEMMs + softmax forward,
+    4 GEMMs + softmax backward)."""
+    from medvae_disentangled_multimodal_amd import ops
+    shape = (2, 1024, 16, 16)
+    g = torch.Generator().manual_seed(3)
+    q, k, v, go = (torch.randn(shape, generator=g) for _ in range(4))
+    ops.PROFILE = []
+    try:
+        _run_tile(dev, q, k, v, go, "32", True)
+        rec = [r for r in ops.PROFILE if r[0] == "attn_gemm"]
+    finally:
+        ops.PROFILE = None
+    assert len(rec) == 4

@@ -685,3 +685,28 @@ def test_groupnorm_backward_partials_from_conv_dgrad(dev, n, c, co, h, silu):
     F.conv2d(yr, wr, None, 1, 1).backward(gy.double())
     for a, b in zip(fz, (xr.grad, gr.grad, br.grad, wr.grad)):
         assert rel(a, b) < 1e-4
+
+
+@pytest.mark.parametrize("n,ci,co,h,w", [(4, 64, 128, 16, 16), (2, 256, 64, 8, 32), (3, 64, 64, 64, 8), (16, 128, 256, 8, 8)])
+@pytest.mark.parametrize("x_split", [False, True])
+def test_wgrad_pow2_gather(dev, n, ci, co, h, w, x_split):
+    """The shift-and-mask im2col gather of the weight gradient (B_WGRAD_P2: stride-1 'same' 3x3 convs at power-of-two
+    H, W -- every c4 / c5 level), plain and on a pre-split 3xBF16 input (the GroupNorm -> conv edge), non-square images
+    included: dW and the fused bias gradient against float64."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    g = torch.Generator().manual_seed(n * ci + h * w)
+    x = torch.randn(n, ci, h, w, generator=g)
+    dy = torch.randn(n, co, h, w, generator=g)
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
+    xd, dyd = cl(x, dev), cl(dy, dev)
+    if x_split:
+        xs = torch.empty_like(xd)
+        _lib.call("mvae_split_bf16", xd.data_ptr(), xs.data_ptr(), xd.numel(), ops._stream(xd))
+        xd = xs
+    dw = torch.zeros(co, ci, 3, 3, device=dev).contiguous(memory_format=torch.channels_last)
+    db = torch.zeros(co, device=dev)
+    ops.conv2d_wgrad_raw(dyd, xd, dw, 0.0, geom, db=db, x_split=x_split)
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_weight(x.double(), (co, ci, 3, 3), dy.double(), padding=1)
+    assert rel(dw, ref) < CONV_TOL
+    assert rel(db, dy.double().sum((0, 2, 3))) < 1e-5

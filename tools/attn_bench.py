@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Attention core timing at the configs' fused geometries (c4 / c5 mid blocks 8x8x2048, c2 7x7x512, c3 7x7x128):
-the fused single-tile kernels (csrc/attn.hip) against the unfused path (batched GEMMs around the row softmax), forward
-and backward, HIP events on the launch stream. tools/attn_bench.py [precision]"""
+"""Attention core timing at the configs' geometries (c4 / c5 16x16x1024 and mid blocks 8x8x2048, c2 7x7x512, c3
+7x7x128): the fused single-tile kernels (csrc/attn.hip, n <= 64), the query-block fused kernels (csrc/attn_tile.hip,
+64 <= n <= 256) and the unfused path (batched GEMMs around the row softmax), forward and backward, HIP events on the
+launch stream. tools/attn_bench.py [precision]"""
 import json
 import os
 import sys
@@ -10,7 +11,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 from medvae_disentangled_multimodal_amd import ops  # noqa: E402
 
-SHAPES = [("c4_8x8x2048", 256, 2048, 8), ("c2_7x7x512", 256, 512, 7), ("c3_7x7x128", 512, 128, 7)]
+SHAPES = [("c4_16x16x1024", 256, 1024, 16), ("c4_8x8x2048", 256, 2048, 8), ("c2_7x7x512", 256, 512, 7),
+          ("c3_7x7x128", 512, 128, 7)]
+VARIANTS = {"small": (True, False), "tile": (False, True), "unfused": (False, False)}  # (ATTN_FUSED, ATTN_TILE)
 
 
 def timed(fn, reps=20):
@@ -37,8 +40,11 @@ def main():
         n = h * h
         fl_f, fl_b = 4.0 * n * n * c * b, 8.0 * n * n * c * b
         row = {}
-        for fused in (True, False):
-            ops.ATTN_FUSED = fused
+        ops.ATTN_FUSED_MAXC = 1 << 30
+        for name, (fused, tile) in VARIANTS.items():
+            if (name == "small" and not ops._attn_small_ok(q, n, c)) or (name == "tile" and not ops._attn_use_tile(q, n, c)):
+                continue
+            ops.ATTN_FUSED, ops.ATTN_TILE = fused, tile
             qq, kk, vv = (t.detach().requires_grad_() for t in (q, k, v))
             tf = timed(lambda: ops.attention_core(qq, kk, vv))
             o = ops.attention_core(qq, kk, vv)
@@ -46,7 +52,7 @@ def main():
             def bwd():
                 torch.autograd.grad(o, (qq, kk, vv), go, retain_graph=True)
             tb = timed(bwd)
-            row["fused" if fused else "unfused"] = {"fwd_us": round(tf * 1e3, 1), "bwd_us": round(tb * 1e3, 1),
+            row[name] = {"fwd_us": round(tf * 1e3, 1), "bwd_us": round(tb * 1e3, 1),
                                                     "fwd_TF/s": round(fl_f / tf / 1e9, 1),
                                                     "bwd_TF/s": round(fl_b / tb / 1e9, 1)}
         out[lab] = row

@@ -44,13 +44,13 @@ suite() {
 
 bench() {
   if [ $# -eq 0 ]; then
-    timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || return $?
+    timeout -k 10 600 python -u bench.py --detail-out $OUT/bench_detail.json > $OUT/bench.json 2> $OUT/bench.err || return $?
     cut -c1-600 $OUT/bench.json
     return 0
   fi
   for c in "$@"; do
     timeout -k 10 400 python -u bench.py --config $c --steps 10 --warmup 3 --no-cpu-baseline --detail \
-      > $OUT/bench_$c.json 2> $OUT/bench_$c.err || return $?
+      --detail-out $OUT/bench_${c}_detail.json > $OUT/bench_$c.json 2> $OUT/bench_$c.err || return $?
     python3 tools/bench_brief.py $OUT/bench_$c.json $c
   done
 }
@@ -107,7 +107,7 @@ ab() {
       # "env:VAR=VAL[,VAR=VAL]": the in-tree library under those environment settings
       if [[ $v == env:* ]]; then lib=medvae_disentangled_multimodal_amd/libmvae_hip.so; IFS=, read -ra envs <<< "${v#env:}"; fi
       env "${envs[@]}" MVAE_HIP_LIB=$lib timeout -k 10 300 python -u bench.py --config $cfg --steps 6 --warmup 2 \
-        --no-cpu-baseline --detail > $OUT/ab_${cfg}_${tag}_$r.json 2> $OUT/ab_${cfg}_${tag}_$r.err || return $?
+        --no-cpu-baseline --detail --detail-out $OUT/ab_${cfg}_${tag}_${r}_detail.json > $OUT/ab_${cfg}_${tag}_$r.json 2> $OUT/ab_${cfg}_${tag}_$r.err || return $?
       python3 tools/bench_brief.py $OUT/ab_${cfg}_${tag}_$r.json "$v"
     done
   done
