@@ -1221,8 +1221,11 @@ def _attn_use_fused(q, n: int, c: int) -> bool:
 # query-block fused attention (csrc/attn_tile.hip) for 64 <= n <= 256 tokens, n % 64 == 0, C % 128 == 0: c4 / c5's
 # 16x16 level (n = 256, C = 1024) and, past ATTN_FUSED_MAXC, the 8x8 mid blocks (n = 64, C = 2048). Forward one launch
 # (scores, softmax and P V in one workgroup per 64 queries; P saved for the backward); backward one launch for dP, dS and
-# dQ plus the two batched GEMMs dV = P^T dO and dK = dS^T Q. MVAE_NO_ATTN_TILE=1 restores the unfused path.
-ATTN_TILE = os.environ.get("MVAE_NO_ATTN_TILE") is None
+# dQ plus the two batched GEMMs dV = P^T dO and dK = dS^T Q. Opt-in (MVAE_ATTN_TILE=1): measured at c4's 16x16x1024
+# (tools/attn_bench.py, profiles/r05_attn_bench.txt) it is slower than the unfused path -- fwd 513 vs 366 us, bwd 847 vs
+# 704 us: one 141 KB workgroup per CU walks 96 short K-tiles (12-24 MFMAs per wave each) behind one tile of prefetch, so
+# every K-tile waits on a global load; the batched GEMMs' 256x256 tiles do not
+ATTN_TILE = os.environ.get("MVAE_ATTN_TILE") is not None
 
 
 def _attn_use_tile(q, n: int, c: int) -> bool:

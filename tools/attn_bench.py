@@ -42,9 +42,9 @@ def main():
         row = {}
         ops.ATTN_FUSED_MAXC = 1 << 30
         for name, (fused, tile) in VARIANTS.items():
+            ops.ATTN_FUSED, ops.ATTN_TILE = fused, tile
             if (name == "small" and not ops._attn_small_ok(q, n, c)) or (name == "tile" and not ops._attn_use_tile(q, n, c)):
                 continue
-            ops.ATTN_FUSED, ops.ATTN_TILE = fused, tile
             qq, kk, vv = (t.detach().requires_grad_() for t in (q, k, v))
             tf = timed(lambda: ops.attention_core(qq, kk, vv))
             o = ops.attention_core(qq, kk, vv)
