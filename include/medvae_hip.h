@@ -266,6 +266,15 @@ int mvae_group_norm_bwd_pack_nhwc(const float* x, const float* dy, const float* 
                                   float* dbias, float bias_beta, void* cs_workspace, size_t cs_workspace_bytes,
                                   void* stream);
 size_t mvae_group_norm_colsum_workspace_bytes(int nb, int hw, int c);
+/* The same with dx also written as split4_bf16 groups (dx_split: 4 B per element at dx's element offsets, 16-B
+ * aligned; mvae_split_bf16's layout) -- the fp32-class (3xBF16) GEMMs' pre-split dY operand of the producing conv's
+ * input and weight gradients (MVAE_CONV_XSPLIT / MVAE_CONV_DYSPLIT), with the conv bias gradient as above. */
+int mvae_group_norm_bwd_split_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
+                                   const float* mean, const float* rstd, float* dx, const float* dx_add, float* dgamma,
+                                   float* dbeta, int nb, int hw, int c, int groups, int silu, float drop_p,
+                                   unsigned long long seed, void* workspace, size_t workspace_bytes, void* dx_split,
+                                   float* dbias, float bias_beta, void* cs_workspace, size_t cs_workspace_bytes,
+                                   void* stream);
 /* Path of mvae_group_norm_fwd_nhwc / _bwd_nhwc (process-wide): 0 = auto (small per-sample tensors -- the
  * 28x28 / 14x14 / 7x7 levels -- run the register-resident one-pass kernels: x read once per pass),
  * 1 = streaming only (statistics pass + apply pass). Both are deterministic; they agree to fp32 rounding. */

@@ -507,6 +507,7 @@ struct LoadColK {
   static constexpr bool COL = true;
   static constexpr int C4 = ROWS / 4;                 // float4 per k-row
   static constexpr int NS = (BK * C4 + NT - 1) / NT;  // float4 per thread
+  static constexpr bool KROW_CHECK = NS * (NT / C4) != BK;  // false: every thread's k-rows are < BK
   __amdgpu_buffer_rsrc_t rs;
   unsigned ld;
   int rows, K, row0, k, c4, kr;
@@ -522,7 +523,7 @@ struct LoadColK {
     const int col = row0 + c4 * 4;
     const int krow = kr + i * (NT / C4);
     const int kk = k + krow;
-    const bool kv = (krow < BK) & (kk < K);
+    const bool kv = (!KROW_CHECK || krow < BK) & (kk < K);
     const unsigned base = ((unsigned)kk * ld + (unsigned)col) * 4u;
     if (VEC == 4) {
       v[i] = bload4(rs, (kv & (col < rows)) ? base : OOB);
@@ -537,23 +538,17 @@ struct LoadColK {
   __device__ void store_slot(__bf16* img, int i) {
     constexpr int P_ = Img<ROWS, true>::PITCH;
     const int krow = kr + i * (NT / C4);
-    if (krow < BK) {
+    if (!KROW_CHECK || krow < BK) {
       if constexpr (PRESPLIT) {
         st_presplit<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
-        if (IS_A && want_bs) {  // element value = hi + lo
-          const unsigned h01 = __float_as_uint(v[i].x), h23 = __float_as_uint(v[i].y);
-          const unsigned l01 = __float_as_uint(v[i].z), l23 = __float_as_uint(v[i].w);
-          bs[0] += __uint_as_float(h01 << 16) + __uint_as_float(l01 << 16);
-          bs[1] += __uint_as_float(h01 & 0xFFFF0000u) + __uint_as_float(l01 & 0xFFFF0000u);
-          bs[2] += __uint_as_float(h23 << 16) + __uint_as_float(l23 << 16);
-          bs[3] += __uint_as_float(h23 & 0xFFFF0000u) + __uint_as_float(l23 & 0xFFFF0000u);
-        }
+        // (a pre-split A = dY^T carries no bias sums: its producer -- the GroupNorm backward, or the host's bias pass
+        // over the fp32 dy -- sums the conv bias gradient; mvae_conv2d_wgrad_nhwc rejects dbias with MVAE_CONV_DYSPLIT)
       } else {
         st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
-        if constexpr (IS_A) {
-          if (want_bs) {
-            bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
-          }
+        if constexpr (IS_A) {  // (masked, not branched: a uniform branch here splits the pipelined K loop)
+          const float wm = want_bs ? 1.f : 0.f;
+          bs[0] = fmaf(wm, v[i].x, bs[0]); bs[1] = fmaf(wm, v[i].y, bs[1]);
+          bs[2] = fmaf(wm, v[i].z, bs[2]); bs[3] = fmaf(wm, v[i].w, bs[3]);
         }
       }
     }
@@ -576,6 +571,7 @@ struct LoadColPix {
   static constexpr bool COL = true;
   static constexpr int C4 = ROWS / 4;
   static constexpr int NS = (BK * C4 + NT - 1) / NT;
+  static constexpr bool KROW_CHECK = NS * (NT / C4) != BK;
   __amdgpu_buffer_rsrc_t rs;
   unsigned ld;
   int rows, K, row0, k, c4, kr, krw, par_off;
@@ -596,7 +592,7 @@ struct LoadColPix {
   __device__ void load_slot(const GemmArgs&, int i) {
     const int col = row0 + c4 * 4;
     const int krow = kr + i * (NT / C4);
-    const bool kv = (krow < BK) & (k + krow < K);
+    const bool kv = (!KROW_CHECK || krow < BK) & (k + krow < K);
     const unsigned base = (pix[i] * ld + (unsigned)col) * 4u;
     if (VEC == 4) {
       v[i] = bload4(rs, (kv & (col < rows)) ? base : OOB);
@@ -610,11 +606,11 @@ struct LoadColPix {
   __device__ void store_slot(__bf16* img, int i) {
     constexpr int P_ = Img<ROWS, true>::PITCH;
     const int krow = kr + i * (NT / C4);
-    if (krow < BK) {
+    if (!KROW_CHECK || krow < BK) {
       st_split<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
-      if (want_bs) {
-        bs[0] += v[i].x; bs[1] += v[i].y; bs[2] += v[i].z; bs[3] += v[i].w;
-      }
+      const float wm = want_bs ? 1.f : 0.f;  // (masked, not branched)
+      bs[0] = fmaf(wm, v[i].x, bs[0]); bs[1] = fmaf(wm, v[i].y, bs[1]);
+      bs[2] = fmaf(wm, v[i].z, bs[2]); bs[3] = fmaf(wm, v[i].w, bs[3]);
     }
   }
   bool want_bs = true;
@@ -643,6 +639,7 @@ struct LoadWgradX {
   static constexpr bool FAST = false;
   static constexpr int C4 = ROWS / 4;
   static constexpr int NS = (BK * C4 + NT - 1) / NT;
+  static constexpr bool KROW_CHECK = NS * (NT / C4) != BK;
   __amdgpu_buffer_rsrc_t rs;
   int c4, kr, krw, k;
   int cc[4], rr[4], ss[4];
@@ -719,7 +716,7 @@ struct LoadWgradX {
   __device__ void load_slot(const GemmArgs& a, int i) {
     const unsigned img = (unsigned)(a.H * a.W);
     const int krow = kr + i * (NT / C4);
-    const bool kv = (krow < BK) & (k + krow < a.K);
+    const bool kv = (!KROW_CHECK || krow < BK) & (k + krow < a.K);
 #ifdef MVAE_WGRAD_XFAKE
     if (VEC == 4) {
       v[i] = bload4(rs, (kv & nv[0]) ? (unsigned)(((k + krow) * a.Cx + cc[0]) * 4) : OOB);
@@ -752,7 +749,7 @@ struct LoadWgradX {
   __device__ void store_slot(__bf16* img, int i) {
     constexpr int P_ = Img<ROWS, true>::PITCH;
     const int krow = kr + i * (NT / C4);
-    if (krow < BK) {
+    if (!KROW_CHECK || krow < BK) {
       if constexpr (PRESPLIT)
         st_presplit<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
       else
@@ -780,6 +777,7 @@ struct LoadWgradXP2 {
   static constexpr bool COL = true;
   static constexpr int C4 = ROWS / 4;
   static constexpr int NS = (BK * C4 + NT - 1) / NT;
+  static constexpr bool KROW_CHECK = NS * (NT / C4) != BK;
   __amdgpu_buffer_rsrc_t rs;
   int c4, kr, krw, k, dr, ds;
   unsigned ldelta, cx4;
@@ -804,14 +802,14 @@ struct LoadWgradXP2 {
     const int krow = kr + i * (NT / C4);
     const int p = k + krw + i * (NT / C4);
     const int w = p & (a.W - 1), h = (p >> a.lw) & (a.H - 1);
-    const bool ok = (krow < BK) & (p < a.K) & nv & ((unsigned)(h + dr) < (unsigned)a.H) &
+    const bool ok = (!KROW_CHECK || krow < BK) & (p < a.K) & nv & ((unsigned)(h + dr) < (unsigned)a.H) &
                     ((unsigned)(w + ds) < (unsigned)a.W);
     v[i] = bload4(rs, ok ? (unsigned)p * cx4 + ldelta : OOB);
   }
   __device__ void store_slot(__bf16* img, int i) {
     constexpr int P_ = Img<ROWS, true>::PITCH;
     const int krow = kr + i * (NT / C4);
-    if (krow < BK) {
+    if (!KROW_CHECK || krow < BK) {
       if constexpr (PRESPLIT)
         st_presplit<PREC>(img, Img<ROWS, true>::PLANE, krow * P_ + ((c4 * 4) ^ col_swz(krow)), v[i]);
       else

@@ -98,8 +98,8 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
               "aligned dy / x, no fused bias");
     return MVAE_EINVAL;
   }
-  if (dysplit && (cout % 4 != 0 || !al16(dy))) {
-    set_error("wgrad: a pre-split dy needs cout %% 4 == 0, 16-B alignment");
+  if (dysplit && (cout % 4 != 0 || !al16(dy) || dbias != nullptr)) {
+    set_error("wgrad: a pre-split dy needs cout %% 4 == 0, 16-B alignment and no fused bias (sum it from the fp32 dy)");
     return MVAE_EINVAL;
   }
   if (mode != 0 && mode != 1) { set_error("wgrad: mode must be 0 or 1"); return MVAE_EINVAL; }
@@ -152,8 +152,10 @@ int mvae_conv2d_wgrad_nhwc(const float* dy, const float* x, float* dw, float* db
     }
     if (bf) {
       wgrad_dma(p2 ? B_WGRAD_P2 : B_WGRAD_FWD, a, st, cfg, pln ? 5 : 4);
-    } else if (p2 && !dysplit && va && (xsplit || vb)) {
-      if (xsplit) launch_big<A_COLM, 4, B_WGRAD_P2_SPLIT, 4>(a, st, cfg);
+    } else if (p2 && va && (xsplit || vb)) {
+      if (dysplit && xsplit) launch_big<A_COLM_SPLIT, 4, B_WGRAD_P2_SPLIT, 4>(a, st, cfg);
+      else if (dysplit) launch_big<A_COLM_SPLIT, 4, B_WGRAD_P2, 4>(a, st, cfg);
+      else if (xsplit) launch_big<A_COLM, 4, B_WGRAD_P2_SPLIT, 4>(a, st, cfg);
       else launch_big<A_COLM, 4, B_WGRAD_P2, 4>(a, st, cfg);
     } else if (dysplit) {
       if (xsplit) launch_big<A_COLM_SPLIT, 4, B_WGRAD_FWD_SPLIT, 4>(a, st, cfg);

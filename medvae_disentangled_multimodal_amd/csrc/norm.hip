@@ -65,6 +65,8 @@ struct GnArgs {
   // gradient, without a separate pass over dx
   uint2* dxp;
   double* csp;
+  int dxp_split;  // dxp format: 0 = packed bf16 (bf16-mixed), 1 = split4_bf16 groups (3xBF16: 4 B per element at the
+                  // fp32 element offsets, mvae_split_bf16's layout -- the pre-split dY operand of the fp32-class GEMMs)
 };
 __device__ __forceinline__ unsigned long long drop_seed(const GnArgs& a) {
   return a.salt ? a.seed ^ (*a.salt * 0xD1B54A32D192ED03ull) : a.seed;
@@ -437,7 +439,10 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
           }
           *(float4*)(op + (long long)r * a.C) = float4{o[0], o[1], o[2], o[3]};
           if (a.dxp != nullptr) {
-            a.dxp[off >> 2] = uint2{pk_bf16x2(o[0], o[1]), pk_bf16x2(o[2], o[3])};
+            if (a.dxp_split)
+              ((uint4*)a.dxp)[off >> 2] = split4_bf16(float4{o[0], o[1], o[2], o[3]});
+            else
+              a.dxp[off >> 2] = uint2{pk_bf16x2(o[0], o[1]), pk_bf16x2(o[2], o[3])};
             cs[0] += o[0]; cs[1] += o[1]; cs[2] += o[2]; cs[3] += o[3];
           }
         }
@@ -788,8 +793,9 @@ __device__ __forceinline__ void gn_bwd_unit(const GnArgs& a, int SC, int u, cons
     q3[e] = sm.gk3[c4 * 4 + e];
   }
   const __amdgpu_buffer_rsrc_t dr = un.rsrc(dx);
-  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((__bf16*)a.dxp + un.ubase), (short)0, (int)(un.bytes >> 1), 0x00020000);
+  const __amdgpu_buffer_rsrc_t pr = a.dxp_split  // split4: fp32 offsets; packed bf16: half of them
+      ? __builtin_amdgcn_make_buffer_rsrc((void*)((float*)a.dxp + un.ubase), (short)0, (int)un.bytes, 0x00020000)
+      : __builtin_amdgcn_make_buffer_rsrc((void*)((__bf16*)a.dxp + un.ubase), (short)0, (int)(un.bytes >> 1), 0x00020000);
   float cs[4] = {0.f, 0.f, 0.f, 0.f};
   const __amdgpu_buffer_rsrc_t ar = un.rsrc(a.dx_add);
 #pragma unroll
@@ -812,10 +818,15 @@ __device__ __forceinline__ void gn_bwd_unit(const GnArgs& a, int SC, int u, cons
     const float4 o{dv[i].x * q1[0] + xv[i].x * q2[0] + q3[0] + w.x, dv[i].y * q1[1] + xv[i].y * q2[1] + q3[1] + w.y,
                    dv[i].z * q1[2] + xv[i].z * q2[2] + q3[2] + w.z, dv[i].w * q1[3] + xv[i].w * q2[3] + q3[3] + w.w};
     gn_res_store(dr, vo + (unsigned)(i * rstep), gn_bits(o));
-    if (a.dxp != nullptr) {  // packed bf16 at half the byte offsets (8-B stores; rows past hw: dropped)
-      typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{pk_bf16x2(o.x, o.y), pk_bf16x2(o.z, o.w)}, pr,
-                                            (vo >> 1) + (unsigned)(i * (rstep >> 1)), 0, 0);
+    if (a.dxp != nullptr) {  // packed bf16 at half the byte offsets (8-B stores) or split4 at the fp32 offsets (16-B
+      typedef __attribute__((ext_vector_type(2))) unsigned u32x2;  // stores); rows past hw: dropped
+      if (a.dxp_split) {
+        const uint4 q = split4_bf16(o);
+        gn_res_store(pr, vo + (unsigned)(i * rstep), gn_u32x4{q.x, q.y, q.z, q.w});
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{pk_bf16x2(o.x, o.y), pk_bf16x2(o.z, o.w)}, pr,
+                                              (vo >> 1) + (unsigned)(i * (rstep >> 1)), 0, 0);
+      }
       if (rph + i * rpar < a.hw) {
         cs[0] += o.x; cs[1] += o.y; cs[2] += o.z; cs[3] += o.w;
       }
@@ -1197,7 +1208,7 @@ int mvae_group_norm_fwd_part_nhwc(const float* x, const double* part, const floa
 static int gn_bwd(const float* x, const float* dy, const float* gamma, const float* beta, const float* mean,
                   const float* rstd, float* dx, const float* dx_add, float* dgamma, float* dbeta, int nb, int hw, int c,
                   int groups, int silu, float drop_p, unsigned long long seed, void* workspace, size_t workspace_bytes,
-                  void* dxp, float* dbias, float bias_beta, void* cs_ws, void* stream);
+                  void* dxp, float* dbias, float bias_beta, void* cs_ws, void* stream, int dxp_split = 0);
 int mvae_group_norm_bwd_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
                              const float* mean, const float* rstd, float* dx, const float* dx_add,
                              float* dgamma, float* dbeta,
@@ -1231,10 +1242,31 @@ int mvae_group_norm_bwd_pack_nhwc(const float* x, const float* dy, const float* 
                 workspace, workspace_bytes, dx_packed, dbias, bias_beta, cs_workspace, stream);
 }
 
+// as mvae_group_norm_bwd_pack_nhwc, with dx also written as split4_bf16 groups (the 3xBF16 GEMMs' pre-split operand,
+// 4 B per element at dx's element offsets; 16-B aligned) instead of packed bf16
+int mvae_group_norm_bwd_split_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
+                                   const float* mean, const float* rstd, float* dx, const float* dx_add, float* dgamma,
+                                   float* dbeta, int nb, int hw, int c, int groups, int silu, float drop_p,
+                                   unsigned long long seed, void* workspace, size_t workspace_bytes, void* dx_split,
+                                   float* dbias, float bias_beta, void* cs_workspace, size_t cs_workspace_bytes,
+                                   void* stream) {
+  if (dx_split == nullptr || ((uintptr_t)dx_split & 15) || ((uintptr_t)dx & 15) || ((uintptr_t)x & 15) ||
+      ((uintptr_t)dy & 15) || (dx_add && ((uintptr_t)dx_add & 15)) || (dbias && cs_workspace == nullptr)) {
+    set_error("group_norm_bwd_split: 16-B aligned x / dy / dx / split output, a column-sum workspace");
+    return MVAE_EINVAL;
+  }
+  if (dbias && cs_workspace_bytes < mvae_group_norm_colsum_workspace_bytes(nb, hw, c)) {
+    set_error("group_norm_bwd_split: column-sum workspace too small");
+    return MVAE_EWORKSPACE;
+  }
+  return gn_bwd(x, dy, gamma, beta, mean, rstd, dx, dx_add, dgamma, dbeta, nb, hw, c, groups, silu, drop_p, seed,
+                workspace, workspace_bytes, dx_split, dbias, bias_beta, cs_workspace, stream, 1);
+}
+
 static int gn_bwd(const float* x, const float* dy, const float* gamma, const float* beta, const float* mean,
                   const float* rstd, float* dx, const float* dx_add, float* dgamma, float* dbeta, int nb, int hw, int c,
                   int groups, int silu, float drop_p, unsigned long long seed, void* workspace, size_t workspace_bytes,
-                  void* dxp, float* dbias, float bias_beta, void* cs_ws, void* stream) {
+                  void* dxp, float* dbias, float bias_beta, void* cs_ws, void* stream, int dxp_split) {
   if (nb <= 0 || hw <= 0 || c <= 0 || (c & 3) || groups <= 0 || c % groups) {
     set_error("group_norm_bwd: bad geometry");
     return MVAE_EINVAL;
@@ -1251,6 +1283,7 @@ static int gn_bwd(const float* x, const float* dy, const float* gamma, const flo
   a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
   a.ws = (double*)workspace;
   a.dxp = (uint2*)dxp;
+  a.dxp_split = dxp_split;
   a.csp = dbias ? (double*)cs_ws : nullptr;
   int it = 0;
   static const int bwd_max_it = [] {

@@ -765,9 +765,10 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
     ws = ARENA.get("ws", nbytes, dy.device)
     mode = (1 if g.upsample else 0) | (MVAE_CONV_XSPLIT if x_split else 0)
     dya = dy
-    if dys is not None and co % 4 == 0:
+    if dys is not None and co % 4 == 0:  # (a pre-split dy carries no in-kernel bias sum: the caller sums it)
         mode |= MVAE_CONV_DYSPLIT
         dya = dys
+        db = None
     _lib.call("mvae_conv2d_wgrad_nhwc", dya.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db), float(beta), n, h, wd,
               c, co, g.kh, g.kw, g.stride, g.pad_t, g.pad_l, ho, wo, mode, ws.data_ptr(), ws.numel(), st)
     return db is not None
@@ -812,13 +813,23 @@ class GradSink:
 # (mvae_group_norm_bwd_pack_nhwc), and the conv backward takes both from it instead of a pack_bf16_colsum pass over dy.
 DYPACK_ATTR = "_mvae_dypack"
 DYPACK = os.environ.get("MVAE_NO_DYPACK") is None
+# fp32-class (3xBF16) mode: the same request with the output gradient written as split4_bf16 groups
+# (mvae_group_norm_bwd_split_nhwc) -- the pre-split dY operand of both backward GEMMs (input gradient: the gathered A
+# operand, MVAE_CONV_XSPLIT; weight gradient: dY^T, MVAE_CONV_DYSPLIT), so neither splits dy in its K loop, and the
+# conv bias gradient summed in the same pass. MVAE_NO_DYSPLIT=1: the conv backward splits dy in registers as before.
+DYSPLIT = os.environ.get("MVAE_NO_DYSPLIT") is None
+# only for convs of at least this many MACs (the c4 levels): measured same box, interleaved (profiles/r05_dysplit_ab.txt),
+# c4 +0.9 % (dgrad 442 -> 459, wgrad 414 -> 426 TF/s against +4.3 ms of GroupNorm backward for the extra 4 B per
+# element), while c2 (-0.6 %) and c3 (-3.6 %) lose: their GEMMs gain less than the wider GroupNorm pass costs
+DYSPLIT_MIN_MACS = 1e11
 
 
 class DyPack:
-    __slots__ = ("bias_ref", "packed", "dx_ptr", "dx_version", "dx_shape", "bias_done", "db")
+    __slots__ = ("bias_ref", "packed", "dx_ptr", "dx_version", "dx_shape", "bias_done", "db", "split")
 
-    def __init__(self, bias_ref):
+    def __init__(self, bias_ref, split: bool = False):
         self.bias_ref = bias_ref
+        self.split = split  # False: packed bf16 (bf16-mixed); True: split4_bf16 (3xBF16)
         self.packed = self.dx_ptr = self.dx_version = self.dx_shape = self.db = None
         self.bias_done = False
 
@@ -910,7 +921,17 @@ class Conv2dFn(torch.autograd.Function):
         bias_done = False
         dyb = None
         got = ctx.dypack.take(dy) if ctx.dypack is not None else None
-        if got is not None:  # packed dy (and the bias gradient) from the GroupNorm backward that produced dy
+        dys = None
+        if got is not None and ctx.dypack.split:  # dy pre-split (and the bias gradient) by the GroupNorm backward
+            dys, bias_done, db_ret = got
+            if not want_b:
+                db_ret = None
+            elif bias_done:
+                bt = _main_grad(ctx.bias_ref)
+                if bt is not None:  # into the flat slot now that dy is known to be the GroupNorm's dx
+                    bt.add_(db_ret)
+                    db_ret = None
+        elif got is not None:  # packed dy (and the bias gradient) from the GroupNorm backward that produced dy
             dyb, bias_done, db_ret = got
             if not want_b:
                 db_ret = None
@@ -927,7 +948,8 @@ class Conv2dFn(torch.autograd.Function):
             dyb, bias_done = pack_dy(dy, g, w.shape[1], bt if bt is not None else db_ret, 1.0 if bt is not None else 0.0)
             if not bias_done:
                 db_ret = None
-        dys = split_dy(dy) if not g.pointwise and not _subpixel_upsample(g) and dyb is None else None
+        if dys is None and not g.pointwise and not _subpixel_upsample(g) and dyb is None:
+            dys = split_dy(dy)
 
         def wgrad():
             nonlocal dw_ret, bias_done
@@ -989,6 +1011,12 @@ GN_PART_ATTR = "_mvae_gn_part"
 GN_FUSED_STATS = os.environ.get("MVAE_NO_GN_FUSED") is None and os.environ.get("MVAE_NO_VEC_EPI") is None
 
 
+def _conv_macs(x, weight, geom: ConvGeom) -> float:
+    n, c, h, w = x.shape
+    ho, wo = geom.out_hw(h, w)
+    return float(n) * ho * wo * weight.shape[0] * c * geom.kh * geom.kw
+
+
 def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink=None, gn_stats: bool = False):
     """gn_stats=True: the output feeds a Normalize (encoder_decoder.py:28-33) -- emit its statistics from the
     conv's epilogue so the GroupNorm skips its statistics pass (plain implicit-GEMM convs only)."""
@@ -1007,6 +1035,10 @@ def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink
     if gn_stats and DYPACK and _dma_fmt() == 2 and not geom.pointwise and weight.shape[0] % 8 == 0 and \
             geom.kh * geom.kw <= 32 and torch.is_grad_enabled():
         dyp = DyPack(bias)
+    elif gn_stats and DYSPLIT and _dma_fmt() == 0 and _MATH[0] == 0 and not geom.pointwise and \
+            not _subpixel_upsample(geom) and weight.shape[0] % 4 == 0 and geom.kh * geom.kw <= 32 and \
+            torch.is_grad_enabled() and _conv_macs(x, weight, geom) >= DYSPLIT_MIN_MACS:
+        dyp = DyPack(bias, split=True)
     y = Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink, part, link, dyp)
     if part is not None:
         setattr(y, GN_PART_ATTR, (part, y._version))
@@ -1120,7 +1152,9 @@ class GroupNormFn(torch.autograd.Function):
             elif ctx.dypack is not None and _al16(dy, dx) and (add is None or _al16(add)):
                 # also dx as packed bf16 and the producing conv's bias gradient (DyPack)
                 req = ctx.dypack
-                packed = torch.empty(x.numel() * 2, device=x.device, dtype=torch.uint8)
+                # packed bf16: 2 B per element; split4_bf16: 4 B per element, dx's layout (an fp32-sized buffer)
+                packed = (torch.empty_like(x, memory_format=CL) if req.split else
+                          torch.empty(x.numel() * 2, device=x.device, dtype=torch.uint8))
                 bref = req.bias_ref
                 tgt, bbeta = None, 0.0
                 if bref is not None and bref.requires_grad:
@@ -1130,7 +1164,8 @@ class GroupNormFn(torch.autograd.Function):
                     tgt = req.db = torch.empty(c, device=x.device, dtype=torch.float32)
                 csb = _lib.query("mvae_group_norm_colsum_workspace_bytes", n, h * w, c)
                 cs = ARENA.get("gncs", csb, x.device) if tgt is not None else None
-                _lib.call("mvae_group_norm_bwd_pack_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(),
+                _lib.call("mvae_group_norm_bwd_split_nhwc" if req.split else "mvae_group_norm_bwd_pack_nhwc",
+                          x.data_ptr(), dy.data_ptr(), gamma.data_ptr(),
                           beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(add), _ptr(dg),
                           _ptr(db), n, h * w, c, groups, silu, drop_p, seed, ws.data_ptr(), ws.numel(),
                           packed.data_ptr(), _ptr(tgt), float(bbeta), _ptr(cs), cs.numel() if cs is not None else 0,

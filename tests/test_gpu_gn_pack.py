@@ -21,9 +21,11 @@ def dev():
 SHAPES = [(4, 64, 64, 128, 32), (8, 8, 8, 512, 32), (6, 7, 7, 256, 32)]
 
 
+@pytest.mark.parametrize("fmt", ["pack", "split"])
 @pytest.mark.parametrize("add", [False, True])
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
-def test_gn_bwd_pack_matches_plain_backward(dev, shape, add):
+def test_gn_bwd_pack_matches_plain_backward(dev, shape, add, fmt):
+    """fmt pack: dx also as packed bf16 (bf16-mixed); split: as split4_bf16 groups (3xBF16, the pre-split dY operand)"""
     from medvae_disentangled_multimodal_amd._lib import call, query
     nb, h, w, c, g = shape
     gen = torch.Generator(device=dev).manual_seed(nb * c + h)
@@ -44,15 +46,16 @@ def test_gn_bwd_pack_matches_plain_backward(dev, shape, add):
          ws.data_ptr(), ws.numel(), st)
     dx1 = torch.empty_like(x)
     dg1, db1 = torch.zeros(c, device=dev), torch.zeros(c, device=dev)
-    packed = torch.empty(x.numel() * 2, dtype=torch.uint8, device=dev)
+    packed = torch.empty(x.numel() * (4 if fmt == "split" else 2), dtype=torch.uint8, device=dev)
     bias = torch.randn(c, device=dev, generator=gen)
     bias0 = bias.clone()
     cs = torch.empty(query("mvae_group_norm_colsum_workspace_bytes", nb, h * w, c), dtype=torch.uint8, device=dev)
-    call("mvae_group_norm_bwd_pack_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+    call("mvae_group_norm_bwd_split_nhwc" if fmt == "split" else "mvae_group_norm_bwd_pack_nhwc",
+         x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
          mean.data_ptr(), rstd.data_ptr(), dx1.data_ptr(), ptr(dadd), dg1.data_ptr(), db1.data_ptr(), nb, h * w, c, g,
          1, 0.0, 0, ws.data_ptr(), ws.numel(), packed.data_ptr(), bias.data_ptr(), 1.0, cs.data_ptr(), cs.numel(), st)
     ref_packed = torch.empty_like(packed)
-    call("mvae_pack_bf16", dx0.data_ptr(), ref_packed.data_ptr(), x.numel(), st)
+    call("mvae_split_bf16" if fmt == "split" else "mvae_pack_bf16", dx0.data_ptr(), ref_packed.data_ptr(), x.numel(), st)
     torch.cuda.synchronize()
     assert torch.equal(dx1, dx0)
     assert torch.equal(dg1, dg0) and torch.equal(db1, db0)
@@ -159,3 +162,49 @@ def test_dypack_rejected_dy_leaves_no_partial_bias_grad(dev):
     for name in g_off:
         rel = float((g_on[name] - g_off[name]).norm() / g_off[name].norm())
         assert rel < 1e-6, (name, rel)
+
+
+def _model_grads_3x(dev, dysplit: bool, calls):
+    import medvae_disentangled_multimodal_amd as M
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    kw = dict(input_channels=3, latent_dim=8, hidden_channels=64, ch_mult=(1, 2), num_res_blocks=1,
+              attn_resolutions=[], dropout=0.0, resolution=32)
+    torch.manual_seed(0)
+    model = M.BaseVAE(**kw).to(dev)
+    mod = M.VAELightningModule(model, {"type": "adam", "lr": 1e-4}, {"type": "none"}, {"type": "vae"},
+                               gradient_clip_val=None)
+    mod.configure_optimizers()
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(4, 3, 32, 32, generator=g) * 2 - 1).to(dev)
+    eps = torch.randn(4, 8, 16, 16, generator=g).to(dev)
+    saved, real_call, mn = ops.DYSPLIT, _lib.call, ops.DYSPLIT_MIN_MACS
+
+    def counting(name, *args):
+        calls[name] = calls.get(name, 0) + 1
+        return real_call(name, *args)
+    ops.DYSPLIT, _lib.call, ops.DYSPLIT_MIN_MACS = dysplit, counting, 0.0  # (every conv of the small model)
+    try:
+        mod.optimizer.zero_grad()
+        ops.prep_flat_weights(mod.flat.data)
+        loss = mod.training_step((x, torch.zeros(4, 1, dtype=torch.long, device=dev)), 0, eps=eps)
+        loss.backward()
+        ops.flat_weights_stale()
+        torch.cuda.synchronize()
+    finally:
+        ops.DYSPLIT, _lib.call, ops.DYSPLIT_MIN_MACS = saved, real_call, mn
+    return mod.flat.grad.detach().double().cpu(), mod.flat
+
+
+def test_3xbf16_step_with_gn_split_dy_matches_register_split(dev):
+    """the fp32-class (3xBF16) step with each conv's output gradient pre-split by the GroupNorm backward that produces
+    it (mvae_group_norm_bwd_split_nhwc -> MVAE_CONV_XSPLIT / MVAE_CONV_DYSPLIT GEMM operands) against the step whose
+    GEMMs split dy in registers: identical operand bits, so only the bias gradients' summation order differs."""
+    c_on, c_off = {}, {}
+    g_on, flat = _model_grads_3x(dev, True, c_on)
+    g_off, _ = _model_grads_3x(dev, False, c_off)
+    assert c_on.get("mvae_group_norm_bwd_split_nhwc", 0) >= 3 and "mvae_group_norm_bwd_split_nhwc" not in c_off
+    rel = float((g_on - g_off).norm() / g_off.norm())
+    assert rel < 1e-5, rel
+    for p, off, name in zip(flat.params, flat.offsets, flat.names):
+        a, b = g_on[off:off + p.numel()], g_off[off:off + p.numel()]
+        assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max())), name
