@@ -39,7 +39,7 @@ namespace mvae {
 // operand kinds
 // *_SPLIT kinds read operands already split into 3xBF16 hi/lo groups in HBM (split4_bf16 layout)
 enum { A_ROWK = 0, A_COLM = 1, A_CONV_FWD = 2, A_CONV_UPS = 3, A_CONV_DGRAD = 4, A_CONV_SUBPIX = 5, A_COLM_PIX = 6,
-       A_CONV_FWD_SPLIT = 7, A_CONV_DGRAD_SPLIT = 8, A_COLM_SPLIT = 9 };
+       A_CONV_FWD_SPLIT = 7, A_CONV_DGRAD_SPLIT = 8, A_COLM_SPLIT = 9, A_ROWK_SPLIT = 10 };
 enum { B_ROWK = 0, B_COLN = 1, B_WGRAD_FWD = 2, B_WGRAD_UPS = 3, B_WGRAD_SUBPIX = 4, B_ROWK_SPLIT = 5,
        B_WGRAD_FWD_SPLIT = 6, B_WGRAD_P2 = 7, B_WGRAD_P2_SPLIT = 8 };
 // B_WGRAD_P2(_SPLIT): the weight gradient's im2col gather of a stride-1 conv whose output is the input's size and whose
@@ -1264,6 +1264,8 @@ struct Loader<8, ROWS, VEC, NT, true, PREC> : LoadConvA<ROWS, VEC, NT, MODE_DGRA
 template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<9, ROWS, VEC, NT, true, PREC> : LoadColK<ROWS, VEC, NT, true, PREC, true> {};
 template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<A_ROWK_SPLIT, ROWS, VEC, NT, true, PREC> : LoadRowK<ROWS, VEC, NT, true, PREC, true> {};
+template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<B_WGRAD_P2, ROWS, VEC, NT, false, PREC> : LoadWgradXP2<ROWS, NT, PREC, false> {};
 template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<B_WGRAD_P2_SPLIT, ROWS, VEC, NT, false, PREC> : LoadWgradXP2<ROWS, NT, PREC, true> {};
@@ -1271,7 +1273,11 @@ struct Loader<B_WGRAD_P2_SPLIT, ROWS, VEC, NT, false, PREC> : LoadWgradXP2<ROWS,
 template <int BM, int BN, int WGM, int WGN, int AK, int VA, int BKIND, int VB, int PREC>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
   constexpr int NT = 64 * WGM * WGN;
-  constexpr int MF = mf_of(AK), KS = ks_of<MF>(), NR = nr_of<MF>();
+#ifndef MVAE_COL_MF16  // COL-image (weight-gradient) register-staged loops on 16x16x32 MFMAs (-DMVAE_COL_MF16=0: 32x32x16)
+#define MVAE_COL_MF16 1
+#endif
+  constexpr int MF = (MVAE_COL_MF16 && PREC < 4 && mf_of(AK) == 32) ? 16 : mf_of(AK);
+  constexpr int KS = ks_of<MF>(), NR = nr_of<MF>();
   using acc_t = acc_of<MF>;
   constexpr int LP = PREC == 4 ? 1 : PREC == 5 ? 3 : PREC;  // arithmetic of the register-staged loaders
   using LA = Loader<AK, BM, VA, NT, true, LP>;
@@ -2013,7 +2019,7 @@ void launch_cfg(GemmArgs& a, hipStream_t st) {
               (!a.res || ((a.ldr & 3) == 0 && (a.sR & 3) == 0 && al16(a.res))) && (!a.bias || al16(a.bias)) &&
               !vec_epi_disabled();
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splits);
-  constexpr bool presplit = AK == A_CONV_FWD_SPLIT || AK == A_CONV_DGRAD_SPLIT || AK == A_COLM_SPLIT ||
+  constexpr bool presplit = AK == A_CONV_FWD_SPLIT || AK == A_CONV_DGRAD_SPLIT || AK == A_COLM_SPLIT || AK == A_ROWK_SPLIT ||
                             BKIND == B_ROWK_SPLIT || BKIND == B_WGRAD_FWD_SPLIT || BKIND == B_WGRAD_P2_SPLIT;
   const int mm = math_mode();
   if constexpr (PO >= 0)

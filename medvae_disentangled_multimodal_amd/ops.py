@@ -216,6 +216,34 @@ def _al16(*ts) -> bool:
     return all(t.data_ptr() % 16 == 0 for t in ts)
 
 
+# Winograd F(2x2, 3x3) for the 3x3 / stride-1 / pad-1 convs of the wide, low-resolution levels (c4 / c5's 8x8 x 2048 and
+# 16x16 x 1024; csrc/winograd.hip): 4/9 of the GEMM MACs for the input / output transform traffic (4x the input and 4x
+# the output in fp32-class words), forward and input gradient, 3xBF16 mode. MVAE_NO_WINOGRAD=1 keeps the implicit GEMM;
+# MVAE_WINOGRAD_MIN_C sets the smallest channel count (both sides) it is used for.
+WINOGRAD = os.environ.get("MVAE_NO_WINOGRAD") is None
+WINOGRAD_MIN_C = int(os.environ.get("MVAE_WINOGRAD_MIN_C", "512"))
+
+
+def _wino_ok(g, h: int, wd: int, cin: int, cout: int) -> bool:
+    return (WINOGRAD and _MATH[0] == 0 and _dma_fmt() == 0 and g.kh == 3 and g.kw == 3 and g.stride == 1 and
+            not g.upsample and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and wd in (8, 16) and h % 2 == 0 and
+            (h * wd) % 32 == 0 and cin % 4 == 0 and cout % 4 == 0 and min(cin, cout) >= WINOGRAD_MIN_C)
+
+
+def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split: bool, dgrad: bool, st):
+    """U (filters), V (input tiles) and the 16 position GEMMs M = V U^T; returns M (arena) for an output transform."""
+    t = n * (h // 2) * (wd // 2)
+    dev = src.device
+    u = ARENA.get("wino_u", 64 * k_in * n_out, dev)
+    v = ARENA.get("wino_v", 64 * t * k_in, dev)
+    m = ARENA.get("wino_m", 64 * t * n_out, dev)
+    cin, cout = (n_out, k_in) if dgrad else (k_in, n_out)
+    _lib.call("mvae_winograd_weight_transform", w.data_ptr(), u.data_ptr(), cin, cout, int(dgrad), st)
+    _lib.call("mvae_winograd_input_transform", src.data_ptr(), v.data_ptr(), n, h, wd, k_in, int(src_split), st)
+    _lib.call("mvae_winograd_gemm", v.data_ptr(), u.data_ptr(), m.data_ptr(), t, k_in, n_out, st)
+    return m
+
+
 # Convolutions on DMA-staged operands: the GEMM stages them into LDS by DMA (no staging registers, conversion or
 # split). bf16-mixed: packed bf16 (MVAE_CONV_BF16, 64-deep K-tiles; default, MVAE_NO_BF16_DMA=1 keeps the
 # register-staged bf16 loop on fp32 operands). fp32-class 3xBF16: planar hi / lo bf16 planes (MVAE_CONV_PLANAR,
@@ -517,6 +545,12 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
         return _conv_fwd_bf16(x, w, b, res, g, y, n, c, h, wd, co, ho, wo, sub, alg, ref, gn_part, st, x_bf16)
     if x_bf16:
         raise RuntimeError("conv2d: a packed bf16 input needs the bf16-mixed LDS-DMA conv path")
+    if _wino_ok(g, h, wd, c, co) and _al16(x, w) and (b is None or _al16(b)) and (res is None or _al16(res)):
+        with _timed("conv_fwd", ref * 4 / 9, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
+            m = _winograd(x, w, n, h, wd, c, co, x_split, False, st)
+            _lib.call("mvae_winograd_output_transform", m.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), _ptr(gn_part),
+                      n, h, wd, co, st)
+        return y
     wg = w
     if sub:  # tap-summed per-class weights (prepared outside the timed GEMM launch)
         wg = ARENA.get("w4", 16 * co * c * 4, x.device)
@@ -620,6 +654,21 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
     if dys is not None and (g.pointwise or co % 4):
         dys = None
     dya = dy if dys is None else dys
+    if _wino_ok(g, h, wd, co, c) and _al16(dya, w) and dy.is_contiguous(memory_format=CL):
+        # the input gradient is the 3x3 / pad-1 conv of dy with the flipped, transposed filters
+        link = gn_link if gn_link is not None and gn_link.usable(dx) else None
+        part = torch.empty(n * h * wd // 32 * c * 2, device=dy.device, dtype=torch.float64) if link else None
+        with _timed("conv_dgrad", flops * 4 / 9, shp, flops):
+            m = _winograd(dya, w, n, h, wd, co, c, dys is not None, True, st)
+            if link is None:
+                _lib.call("mvae_winograd_output_transform", m.data_ptr(), None, None, dx.data_ptr(), None, n, h, wd, c,
+                          st)
+            else:  # with the GroupNorm backward partials (mvae_conv2d_dgrad_gnbwd_nhwc's epilogue sums)
+                _lib.call("mvae_winograd_output_gnbwd", m.data_ptr(), dx.data_ptr(), link.x.data_ptr(),
+                          link.mean.data_ptr(), link.rstd.data_ptr(), link.gamma.data_ptr(), link.beta.data_ptr(),
+                          link.groups, link.silu, part.data_ptr(), n, h, wd, c, st)
+                link.part, link.dx = part, dx
+        return dx
     if gn_link is not None and gn_link.usable(dx) and not g.pointwise and not g.upsample and g.stride == 1 and \
             co % 4 == 0 and _al16(dy, dx):
         split = WEIGHT_SPLIT and _splits_ok()

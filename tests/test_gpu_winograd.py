@@ -1,0 +1,167 @@
+"""Winograd F(2x2, 3x3) convolution (csrc/winograd.hip) against float64 references: forward with bias, residual and the
+fused GroupNorm statistics, input gradient with and without the GroupNorm backward partials, pre-split (3xBF16) inputs,
+both supported widths (8, 16) and non-square heights; and through ops.conv2d's dispatcher against the implicit-GEMM
+path of the same layer.
+
+Tolerance: 3xBF16 GEMM arithmetic on fp32 transforms, <= 2e-4 norm-wise relative error (the conv bar of
+test_gpu_kernels.py); the fp64 statistics to 1e-5 relative."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CONV_TOL = 2e-4
+
+# n, cin, cout, h, w
+CASES = [
+    (2, 64, 64, 8, 8),
+    (3, 128, 64, 16, 16),
+    (2, 32, 96, 12, 8),    # non-square, cin != cout
+    (1, 256, 128, 4, 16),  # one tile row pair per image
+    (4, 512, 512, 8, 8),   # c4-like channel count, 256-wide GEMM tiles
+]
+
+
+def rel(a, b):
+    a = a.detach().double().cpu().flatten()
+    b = b.detach().double().cpu().flatten()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def cl(t, dev):
+    return t.to(dev).contiguous(memory_format=torch.channels_last)
+
+
+def _split(t):
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    s = torch.empty_like(t)
+    _lib.call("mvae_split_bf16", t.data_ptr(), s.data_ptr(), t.numel(), ops._stream(t))
+    return s
+
+
+def _stats64(y, groups_of=4):
+    """{sum, sum of squares} per 32-pixel block and 4-channel group of an NHWC float64 tensor."""
+    n, c, h, w = y.shape
+    t = y.permute(0, 2, 3, 1).reshape(n * h * w // 32, 32, c // groups_of, groups_of)
+    return torch.stack([t.sum((1, 3)), (t * t).sum((1, 3))], -1).flatten()
+
+
+@pytest.fixture(autouse=True)
+def _wino_on(monkeypatch):
+    from medvae_disentangled_multimodal_amd import ops
+    monkeypatch.setattr(ops, "WINOGRAD", True)
+    monkeypatch.setattr(ops, "WINOGRAD_MIN_C", 1)
+
+
+@pytest.mark.parametrize("n,ci,co,h,w", CASES)
+@pytest.mark.parametrize("x_split", [False, True])
+def test_winograd_forward(dev, n, ci, co, h, w, x_split):
+    from medvae_disentangled_multimodal_amd import ops
+    g = torch.Generator().manual_seed(n * ci + co + h * w)
+    x = torch.randn(n, ci, h, w, generator=g)
+    wt = torch.randn(co, ci, 3, 3, generator=g) / (3 * ci ** 0.5)
+    b = torch.randn(co, generator=g)
+    r = torch.randn(n, co, h, w, generator=g)
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
+    assert ops._wino_ok(geom, h, w, ci, co)
+    xd = cl(x, dev)
+    if x_split:
+        xd = _split(xd)
+    part = torch.empty(n * h * w // 32 * (co // 4) * 2, device=dev, dtype=torch.float64)
+    y = ops.conv2d_forward_raw(xd, cl(wt, dev), b.to(dev), cl(r, dev), geom, x_split=x_split, gn_part=part)
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.conv2d(x.double(), wt.double(), b.double(), padding=1) + r.double()
+    assert rel(y, ref) < CONV_TOL
+    assert rel(part, _stats64(y.double().cpu())) < 1e-9  # the statistics are of the stored y
+    assert rel(part, _stats64(ref)) < CONV_TOL
+
+
+@pytest.mark.parametrize("n,ci,co,h,w", CASES)
+@pytest.mark.parametrize("dy_split", [False, True])
+def test_winograd_input_gradient(dev, n, ci, co, h, w, dy_split):
+    from medvae_disentangled_multimodal_amd import ops
+    g = torch.Generator().manual_seed(7 * n + ci + co + h)
+    dy = torch.randn(n, co, h, w, generator=g)
+    wt = torch.randn(co, ci, 3, 3, generator=g) / (3 * co ** 0.5)
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
+    dyd = cl(dy, dev)
+    dys = _split(dyd) if dy_split else None
+    dx = ops.conv2d_dgrad_raw(dyd, cl(wt, dev), (n, ci, h, w), geom, dys=dys)
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_input((n, ci, h, w), wt.double(), dy.double(), padding=1)
+    assert rel(dx, ref) < CONV_TOL
+
+
+@pytest.mark.parametrize("silu", [False, True])
+def test_winograd_input_gradient_gn_partials(dev, silu):
+    """The GroupNorm-backward partials of the dgrad output transform: per channel and 32-pixel block
+    {sum dyn, sum dyn * xhat}, dyn = dx * silu'(.) (mvae_conv2d_dgrad_gnbwd_nhwc's contract)."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    n, ci, co, h, w, groups = 2, 128, 64, 8, 16, 32
+    g = torch.Generator().manual_seed(11 + silu)
+    dy = torch.randn(n, co, h, w, generator=g)
+    wt = torch.randn(co, ci, 3, 3, generator=g) / (3 * co ** 0.5)
+    xg = torch.randn(n, ci, h, w, generator=g) * 1.5 + 0.3
+    gamma, beta = torch.randn(ci, generator=g), torch.randn(ci, generator=g)
+    xs = xg.double().reshape(n, groups, -1)
+    mean = xs.mean(-1)
+    rstd = (xs.var(-1, unbiased=False) + 1e-6).rsqrt()
+    link = ops.GnBwdLink(groups, silu)
+    link.x, link.gamma, link.beta = cl(xg, dev), gamma.to(dev), beta.to(dev)
+    link.mean, link.rstd = mean.float().flatten().to(dev), rstd.float().flatten().to(dev)
+    dx = ops.conv2d_dgrad_raw(cl(dy, dev), cl(wt, dev), (n, ci, h, w), ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False),
+                              gn_link=link)
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_input((n, ci, h, w), wt.double(), dy.double(), padding=1)
+    assert rel(dx, ref) < CONV_TOL
+    assert link.part is not None and link.dx is dx
+    xh = ((xg.double().reshape(n, groups, -1) - mean[..., None]) * rstd[..., None]).reshape(n, ci, h, w)
+    d = dx.double().cpu()
+    if silu:
+        yn = xh * gamma.double()[None, :, None, None] + beta.double()[None, :, None, None]
+        sg = torch.sigmoid(yn)
+        d = d * sg * (1 + yn * (1 - sg))
+    blk = lambda t: t.permute(0, 2, 3, 1).reshape(n * h * w // 32, 32, ci).sum(1)  # noqa: E731
+    want = torch.stack([blk(d), blk(d * xh)], -1).flatten()
+    assert rel(link.part, want) < 1e-5
+
+
+def test_winograd_through_conv2d_matches_implicit_gemm(dev, monkeypatch):
+    """ops.conv2d forward + backward (dx, dW, db) on the Winograd path against the same layer on the implicit GEMM."""
+    from medvae_disentangled_multimodal_amd import ops
+    n, c, h, w = 4, 256, 16, 16
+    g = torch.Generator().manual_seed(5)
+    x0 = torch.randn(n, c, h, w, generator=g)
+    w0 = torch.randn(c, c, 3, 3, generator=g) / (3 * c ** 0.5)
+    b0 = torch.randn(c, generator=g)
+    dy0 = torch.randn(n, c, h, w, generator=g)
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
+
+    def run(wino):
+        monkeypatch.setattr(ops, "WINOGRAD", wino)
+        x = cl(x0, dev).requires_grad_(True)
+        wt = w0.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        b = b0.to(dev).requires_grad_(True)
+        y = ops.conv2d(x, wt, b, geom)
+        y.backward(cl(dy0, dev))
+        torch.cuda.synchronize()
+        return y.detach().cpu(), x.grad.cpu(), wt.grad.cpu(), b.grad.cpu()
+
+    a, r = run(True), run(False)
+    for u, v in zip(a, r):
+        assert rel(u, v) < CONV_TOL
+
+
+def test_winograd_rejects_unsupported_geometry(dev):
+    from medvae_disentangled_multimodal_amd import _lib
+    x = torch.zeros(1, 12, 12, 64, device=dev)
+    v = torch.zeros(16 * 36 * 64, device=dev)
+    with pytest.raises(RuntimeError):
+        _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), 1, 12, 12, 64, 0, 0)
