@@ -183,6 +183,17 @@ int mvae_winograd_output_gnbwd(const float* m, float* dx, const float* x, const 
                                const float* gamma, const float* beta, int groups, int silu, double* part, int nb, int h,
                                int w, int n, void* stream);
 size_t mvae_winograd_workspace_bytes(int nb, int h, int w, int cin, int cout);
+/* Weight gradient of the same convs, F(3x3, 2x2) on the same tiles: dw = beta*dw + G^T M G with
+ * M_xi = sum_tiles D'_xi (x) V_xi, D' = A D A^T of the 2x2 output-gradient tiles, V the forward's input transform.
+ *   dy_transform:  dy [nb][h][w][k] (fp32, or split4_bf16 groups when dy_split) -> d [16][T][k] split4_bf16
+ *   wgrad_gemm:    m [16][cout][cin] = sum over tiles d^T v (split over the tiles within workspace:
+ *                  mvae_gemm_workspace_bytes(cout, cin, tiles, 16))
+ *   wgrad_output:  dw [cout][3][3][cin] = beta*dw + G^T m G
+ * The conv bias gradient is not produced here (mvae_bias_grad, or the GroupNorm backward that split dy). */
+int mvae_winograd_dy_transform(const float* dy, void* d, int nb, int h, int w, int k, int dy_split, void* stream);
+int mvae_winograd_wgrad_gemm(const void* d, const void* v, float* m, long long tiles, int cout, int cin, float* workspace,
+                             size_t workspace_bytes, void* stream);
+int mvae_winograd_wgrad_output(const float* m, float* dw, float beta, int cout, int cin, void* stream);
 
 /* 3xBF16 operand pre-split (same bytes as the fp32 tensor): per 4 values hi0..hi3 lo0..lo3 bf16,
  * hi = bf16(x) (round to nearest even), lo = bf16(x - hi). The weight-prep entry points below take

@@ -39,6 +39,9 @@ SIGNATURES = {
     "mvae_winograd_output_transform": (I, [P, P, P, P, P, I, I, I, I, P]),
     "mvae_winograd_output_gnbwd": (I, [P, P, P, P, P, P, P, I, I, P, I, I, I, I, P]),
     "mvae_winograd_workspace_bytes": (Z, [I, I, I, I, I]),
+    "mvae_winograd_dy_transform": (I, [P, P, I, I, I, I, I, P]),
+    "mvae_winograd_wgrad_gemm": (I, [P, P, P, L, I, I, P, Z, P]),
+    "mvae_winograd_wgrad_output": (I, [P, P, F, I, I, P]),
     "mvae_conv2d_wgrad_workspace_bytes": (Z, [I, I, I, I, I, I, I]),
     "mvae_conv2d_wgrad_small_cout_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, I, P, Z, P]),
     "mvae_conv2d_wgrad_small_cout_workspace_bytes": (Z, [I, I]),

@@ -41,7 +41,7 @@ namespace mvae {
 enum { A_ROWK = 0, A_COLM = 1, A_CONV_FWD = 2, A_CONV_UPS = 3, A_CONV_DGRAD = 4, A_CONV_SUBPIX = 5, A_COLM_PIX = 6,
        A_CONV_FWD_SPLIT = 7, A_CONV_DGRAD_SPLIT = 8, A_COLM_SPLIT = 9, A_ROWK_SPLIT = 10 };
 enum { B_ROWK = 0, B_COLN = 1, B_WGRAD_FWD = 2, B_WGRAD_UPS = 3, B_WGRAD_SUBPIX = 4, B_ROWK_SPLIT = 5,
-       B_WGRAD_FWD_SPLIT = 6, B_WGRAD_P2 = 7, B_WGRAD_P2_SPLIT = 8 };
+       B_WGRAD_FWD_SPLIT = 6, B_WGRAD_P2 = 7, B_WGRAD_P2_SPLIT = 8, B_COLN_SPLIT = 9 };
 // B_WGRAD_P2(_SPLIT): the weight gradient's im2col gather of a stride-1 conv whose output is the input's size and whose
 // H and W are powers of two (the c4 / c5 levels 64, 32, 16, 8): the source pixel of output pixel p through tap (r, s) is
 // p + (r - pad_t) W + (s - pad_l), valid where h + r - pad_t and w + s - pad_l stay inside the image, and h, w come from p
@@ -1266,6 +1266,8 @@ struct Loader<9, ROWS, VEC, NT, true, PREC> : LoadColK<ROWS, VEC, NT, true, PREC
 template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<A_ROWK_SPLIT, ROWS, VEC, NT, true, PREC> : LoadRowK<ROWS, VEC, NT, true, PREC, true> {};
 template <int ROWS, int VEC, int NT, int PREC>
+struct Loader<B_COLN_SPLIT, ROWS, VEC, NT, false, PREC> : LoadColK<ROWS, VEC, NT, false, PREC, true> {};
+template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<B_WGRAD_P2, ROWS, VEC, NT, false, PREC> : LoadWgradXP2<ROWS, NT, PREC, false> {};
 template <int ROWS, int VEC, int NT, int PREC>
 struct Loader<B_WGRAD_P2_SPLIT, ROWS, VEC, NT, false, PREC> : LoadWgradXP2<ROWS, NT, PREC, true> {};
@@ -2020,7 +2022,8 @@ void launch_cfg(GemmArgs& a, hipStream_t st) {
               !vec_epi_disabled();
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splits);
   constexpr bool presplit = AK == A_CONV_FWD_SPLIT || AK == A_CONV_DGRAD_SPLIT || AK == A_COLM_SPLIT || AK == A_ROWK_SPLIT ||
-                            BKIND == B_ROWK_SPLIT || BKIND == B_WGRAD_FWD_SPLIT || BKIND == B_WGRAD_P2_SPLIT;
+                            BKIND == B_ROWK_SPLIT || BKIND == B_WGRAD_FWD_SPLIT || BKIND == B_WGRAD_P2_SPLIT ||
+                            BKIND == B_COLN_SPLIT;
   const int mm = math_mode();
   if constexpr (PO >= 0)
     hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, PO>), grid, dim3(64 * WGM * WGN), 0, st, a);

@@ -1,6 +1,6 @@
 // Winograd F(2x2, 3x3) convolution for the 3x3 / stride-1 / pad-1 convs of the low-resolution, wide levels (c4 / c5's
 // 8x8 x 2048 and 16x16 x 1024: ResnetBlock conv1 / conv2, the mid blocks -- src/models/encoder_decoder.py:123-170) in the
-// fp32-class (3xBF16) arithmetic, forward and input gradient.
+// fp32-class (3xBF16) arithmetic: forward, input gradient and weight gradient (F(3x3, 2x2), below).
 //
 // Per 2x2 output tile t and channel c the 4x4 input patch d is transformed to V = B^T d B, the 3x3 filter g of (k, c) to
 // U = G g G^T, the 16 transformed positions xi are independent GEMMs M_xi[t][k] = sum_c V_xi[t][c] U_xi[k][c], and the
@@ -80,6 +80,90 @@ __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ 
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[((long long)(i * 4 + j) * T + t) * C4 + c4] = split4_bf16(d[i][j]);
+}
+
+// Weight gradient (F(3x3, 2x2) on the same tiles): with D_t the 2x2 output-gradient tile and X_t the input patch of
+// tile t, dW[r][s] = sum_t sum_{a,e} D_t[a][e] X_t[a+r][e+s] = G^T [ sum_t (A D_t A^T) (.) (B^T X_t B) ] G -- the bilinear
+// form of the forward identity differentiated by the filter. So dW = G^T M G with M_xi[k][c] = sum_t D'_xi[t][k]
+// V_xi[t][c]: 16 GEMMs over the tiles (K = T) of the transformed output gradient D' = A D A^T (A = (A^T)^T, rows
+// [1 0; 1 1; 1 -1; 0 -1]) and the forward's V.
+
+// dy [nb][H][W][K] (fp32, or split4_bf16 groups when XS) -> D' [16][T][K] split4_bf16: one thread per (tile, 4-group)
+template <bool XS>
+__global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ dy, uint4* __restrict__ d, int nb, int H,
+                                                      int W, int K) {
+  const int K4 = K >> 2, th = H >> 1, tw = W >> 1;
+  const long long T = (long long)nb * th * tw;
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= T * K4) return;
+  const long long t = idx / K4;
+  const int k4 = (int)(idx - t * K4);
+  const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
+  float4 v[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float4 r = *(const float4*)(dy + (((long long)b * H + 2 * ti + a) * W + 2 * tj + e) * K + k4 * 4);
+      if constexpr (XS) {
+        const unsigned h01 = __float_as_uint(r.x), h23 = __float_as_uint(r.y);
+        const unsigned l01 = __float_as_uint(r.z), l23 = __float_as_uint(r.w);
+        v[a][e] = float4{__uint_as_float(h01 << 16) + __uint_as_float(l01 << 16),
+                         __uint_as_float(h01 & 0xFFFF0000u) + __uint_as_float(l01 & 0xFFFF0000u),
+                         __uint_as_float(h23 << 16) + __uint_as_float(l23 << 16),
+                         __uint_as_float(h23 & 0xFFFF0000u) + __uint_as_float(l23 & 0xFFFF0000u)};
+      } else {
+        v[a][e] = r;
+      }
+    }
+  float4 c[4][2];  // A D: rows
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    c[0][e] = v[0][e];
+    c[1][e] = f4add(v[0][e], v[1][e]);
+    c[2][e] = f4sub(v[0][e], v[1][e]);
+    c[3][e] = f4scale(v[1][e], -1.f);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float4 o[4] = {c[i][0], f4add(c[i][0], c[i][1]), f4sub(c[i][0], c[i][1]), f4scale(c[i][1], -1.f)};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[((long long)(i * 4 + j) * T + t) * K4 + k4] = split4_bf16(o[j]);
+  }
+}
+
+// dw [cout][3][3][cin] = beta * dw + G^T M G, M [16][cout][cin] fp32: one thread per (k, 4-group of c)
+__global__ void __launch_bounds__(256) wino_wout_kernel(const float* __restrict__ m, float* __restrict__ dw, float beta,
+                                                        int cout, int cin) {
+  const int C4 = cin >> 2;
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)cout * C4) return;
+  const long long mn = (long long)cout * cin;
+  float4 mv[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mv[i][j] = *(const float4*)(m + (i * 4 + j) * mn + idx * 4);
+  float4 r[3][4];  // G^T M
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[0][j] = f4add(mv[0][j], f4scale(f4add(mv[1][j], mv[2][j]), 0.5f));
+    r[1][j] = f4scale(f4sub(mv[1][j], mv[2][j]), 0.5f);
+    r[2][j] = f4add(f4scale(f4add(mv[1][j], mv[2][j]), 0.5f), mv[3][j]);
+  }
+  const int k = (int)(idx / C4), c4 = (int)(idx - (long long)k * C4);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float4 o[3] = {f4add(r[i][0], f4scale(f4add(r[i][1], r[i][2]), 0.5f)), f4scale(f4sub(r[i][1], r[i][2]), 0.5f),
+                         f4add(f4scale(f4add(r[i][1], r[i][2]), 0.5f), r[i][3])};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float4* p = (float4*)(dw + (((long long)k * 3 + i) * 3 + j) * cin + c4 * 4);
+      float4 v = o[j];
+      if (beta != 0.f) v = f4add(v, f4scale(*p, beta));
+      *p = v;
+    }
+  }
 }
 
 // G g G^T of a 3x3 filter of float4 groups
@@ -369,6 +453,60 @@ int mvae_winograd_output_gnbwd(const float* m, float* dx, const float* x, const 
   p.groups = groups; p.silu = silu; p.nb = nb; p.H = h; p.W = w; p.N = n;
   const long long nblk = wino_tiles(nb, h, w) / 8;
   hipLaunchKernelGGL(wino_out_kernel<true>, dim3(egrid256(nblk * (n / 4))), dim3(256), 0, (hipStream_t)stream, p);
+  return launch_status();
+}
+
+// D' [16][T][k] split4_bf16 of the output gradient dy [nb][h][w][k] (fp32, or split4_bf16 groups when dy_split)
+int mvae_winograd_dy_transform(const float* dy, void* d, int nb, int h, int w, int k, int dy_split, void* stream) {
+  if (!dy || !d || !wino_geom_ok(nb, h, w, k, k) || !al16(dy) || !al16(d)) {
+    set_error("winograd_dy_transform: even h, w in {8, 16}, h w %% 32 == 0, k %% 4 == 0, 16-B aligned");
+    return MVAE_EINVAL;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const long long n = wino_tiles(nb, h, w) * (k / 4);
+  if (dy_split)
+    hipLaunchKernelGGL(wino_dy_kernel<true>, dim3(egrid256(n)), dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
+  else
+    hipLaunchKernelGGL(wino_dy_kernel<false>, dim3(egrid256(n)), dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
+  return launch_status();
+}
+
+// M [16][cout][cin] fp32 = sum over the tiles of D'_xi [T][cout] (x) V_xi [T][cin]: one batched launch (COL x COL
+// images of pre-split operands), split over the tiles when the 16 products leave the chip under-filled and the
+// workspace (mvae_gemm_workspace_bytes(cout, cin, tiles, 16)) allows
+int mvae_winograd_wgrad_gemm(const void* d, const void* v, float* m, long long tiles, int cout, int cin, float* workspace,
+                             size_t workspace_bytes, void* stream) {
+  if (!d || !v || !m || tiles <= 0 || cout <= 0 || cin <= 0 || cout % 4 || cin % 4 || !al16(d) || !al16(v) || !al16(m) ||
+      tiles * std::max(cout, cin) * 4 > MAX_DESC_BYTES || tiles > (1LL << 30)) {
+    set_error("winograd_wgrad_gemm: cout, cin multiples of 4, 16-B aligned, one position < 4 GiB");
+    return MVAE_EINVAL;
+  }
+  if (math_mode() != MATH_3XBF16) {
+    set_error("winograd: the 3xBF16 (fp32-class) arithmetic only");
+    return MVAE_EINVAL;
+  }
+  GemmArgs a{};
+  a.M = cout; a.N = cin; a.K = (int)tiles; a.batch = 16;
+  a.A = (const float*)d; a.lda = cout; a.sA = tiles * cout;
+  a.B = (const float*)v; a.ldb = cin; a.sB = tiles * cin;
+  a.C = m; a.ldc = cin; a.sC = (long long)cout * cin;
+  a.alpha = 1.f; a.beta = 0.f;
+  a.a_bytes = (unsigned)(tiles * cout * 4); a.b_bytes = (unsigned)(tiles * cin * 4);
+  a.c_bytes = (unsigned)((long long)cout * cin * 4);
+  const int cfg = choose_tile(a, true, workspace != nullptr);
+  plan_splits(a, cfg, workspace, workspace_bytes);
+  launch_big<A_COLM_SPLIT, 4, B_COLN_SPLIT, 4>(a, (hipStream_t)stream, cfg);
+  return gemm_finish(a, (hipStream_t)stream);
+}
+
+// dw [cout][3][3][cin] = beta * dw + G^T M G
+int mvae_winograd_wgrad_output(const float* m, float* dw, float beta, int cout, int cin, void* stream) {
+  if (!m || !dw || cout <= 0 || cin <= 0 || cin % 4 || !al16(m) || !al16(dw)) {
+    set_error("winograd_wgrad_output: cin %% 4 == 0, 16-B aligned");
+    return MVAE_EINVAL;
+  }
+  hipLaunchKernelGGL(wino_wout_kernel, dim3(egrid256((long long)cout * (cin / 4))), dim3(256), 0, (hipStream_t)stream, m,
+                     dw, beta, cout, cin);
   return launch_status();
 }
 

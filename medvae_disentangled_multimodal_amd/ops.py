@@ -230,6 +230,16 @@ def _wino_ok(g, h: int, wd: int, cin: int, cout: int) -> bool:
             (h * wd) % 32 == 0 and cin % 4 == 0 and cout % 4 == 0 and min(cin, cout) >= WINOGRAD_MIN_C)
 
 
+WINOGRAD_WGRAD = os.environ.get("MVAE_NO_WINOGRAD_WGRAD") is None
+
+
+def _wino_wgrad_ok(g, x, dy, dw, dys) -> bool:
+    n, c, h, wd = x.shape
+    co = dy.shape[1]
+    return (WINOGRAD_WGRAD and _wino_ok(g, h, wd, c, co) and _al16(x, dy, dw) and (dys is None or _al16(dys)) and
+            dy.is_contiguous(memory_format=CL) and dw.is_contiguous(memory_format=CL))
+
+
 def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split: bool, dgrad: bool, st):
     """U (filters), V (input tiles) and the 16 position GEMMs M = V U^T; returns M (arena) for an output transform."""
     t = n * (h // 2) * (wd // 2)
@@ -755,7 +765,7 @@ def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool
     co = dy.shape[1]
     _, _, ho, wo = dy.shape
     ref = 2.0 * n * ho * wo * co * c * g.kh * g.kw
-    alg = ref * 4 / 9 if _subpixel_upsample(g) else ref
+    alg = ref * 4 / 9 if _subpixel_upsample(g) or (dyb is None and _wino_wgrad_ok(g, x, dy, dw, dys)) else ref
     if dyb is not None and not x_split and not g.upsample and c % 8 == 0 and co % 8 == 0 and _al16(x):
         # bf16-mixed weight gradient on packed bf16 dy and x (LDS-DMA main loop); the bias gradient is summed from the
         # fp32 dy by the caller
@@ -810,6 +820,23 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         _lib.call("mvae_conv2d_wgrad_upsample_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db),
                   float(beta), n, h, wd, c, co, ws.data_ptr(), ws.numel(), st)
         return db is not None
+    if _wino_wgrad_ok(g, x, dy, dw, dys):
+        # Winograd F(3x3, 2x2): dW = G^T [sum_tiles (A D A^T) (.) (B^T X B)] G (csrc/winograd.hip); the bias gradient is
+        # left to the caller
+        t = n * (h // 2) * (wd // 2)
+        dev = dy.device
+        dt = ARENA.get("wino_d", 64 * t * co, dev)
+        v = ARENA.get("wino_v", 64 * t * c, dev)
+        m = ARENA.get("wino_mw", 64 * co * c, dev)
+        nbytes = _lib.query("mvae_gemm_workspace_bytes", co, c, t, 16)
+        ws = ARENA.get("ws", nbytes, dev)
+        dya = dys if dys is not None else dy
+        _lib.call("mvae_winograd_dy_transform", dya.data_ptr(), dt.data_ptr(), n, h, wd, co, int(dys is not None), st)
+        _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), n, h, wd, c, int(x_split), st)
+        _lib.call("mvae_winograd_wgrad_gemm", dt.data_ptr(), v.data_ptr(), m.data_ptr(), t, co, c, ws.data_ptr(),
+                  ws.numel(), st)
+        _lib.call("mvae_winograd_wgrad_output", m.data_ptr(), dw.data_ptr(), float(beta), co, c, st)
+        return False
     nbytes = _lib.query("mvae_conv2d_wgrad_workspace_bytes", n, c, co, g.kh, g.kw, ho, wo)
     ws = ARENA.get("ws", nbytes, dy.device)
     mode = (1 if g.upsample else 0) | (MVAE_CONV_XSPLIT if x_split else 0)

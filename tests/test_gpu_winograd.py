@@ -99,6 +99,27 @@ def test_winograd_input_gradient(dev, n, ci, co, h, w, dy_split):
     assert rel(dx, ref) < CONV_TOL
 
 
+@pytest.mark.parametrize("n,ci,co,h,w", CASES)
+@pytest.mark.parametrize("split", [False, True])
+def test_winograd_weight_gradient(dev, n, ci, co, h, w, split):
+    """F(3x3, 2x2) weight gradient accumulating into dW (beta = 1) on plain and pre-split x / dy."""
+    from medvae_disentangled_multimodal_amd import ops
+    g = torch.Generator().manual_seed(3 * n + ci + 2 * co + w)
+    x = torch.randn(n, ci, h, w, generator=g)
+    dy = torch.randn(n, co, h, w, generator=g)
+    dw0 = torch.randn(co, ci, 3, 3, generator=g)
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
+    xd, dyd = cl(x, dev), cl(dy, dev)
+    dw = cl(dw0, dev)
+    assert ops._wino_wgrad_ok(geom, xd, dyd, dw, None)
+    fused = ops.conv2d_wgrad_raw(dyd, _split(xd) if split else xd, dw, 1.0, geom, x_split=split,
+                                 dys=_split(dyd) if split else None)
+    torch.cuda.synchronize()
+    assert fused is False  # (the bias gradient is the caller's)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (co, ci, 3, 3), dy.double(), padding=1)
+    assert rel(dw.double().cpu() - dw0.double(), ref) < CONV_TOL
+
+
 @pytest.mark.parametrize("silu", [False, True])
 def test_winograd_input_gradient_gn_partials(dev, silu):
     """The GroupNorm-backward partials of the dgrad output transform: per channel and 32-pixel block
