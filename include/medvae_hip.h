@@ -161,39 +161,42 @@ int mvae_conv2d_wgrad_upsample_nhwc(const float* dy, const float* x, float* dw, 
                                     void* stream);
 size_t mvae_conv2d_wgrad_upsample_workspace_bytes(int nb, int h, int w_, int cin, int cout);
 
-/* Winograd F(2x2, 3x3) form of a 3x3 / stride-1 / pad-1 conv (ResnetBlock conv1 / conv2 and the mid blocks at the
- * 8x8 / 16x16 levels, encoder_decoder.py:123-170; forward and input gradient), 3xBF16 math mode only. Four stages
- * on the stream: U = G g G^T of the filters, V = B^T d B of the input's 4x4 patches (2x2 output tiles, T = nb h/2 w/2
- * tiles), M_xi = V_xi U_xi^T for the 16 positions xi (one batched MFMA GEMM: 4/9 of the direct conv's MACs), output
- * A^T M A (+ bias, + residual, + the following GroupNorm's statistics). The input gradient is the same conv of dy
- * with the flipped, transposed filters (weight_transform dgrad = 1) and may emit the GroupNorm backward partials of
+/* Winograd F(m x m, 3x3) form of a 3x3 / stride-1 / pad-1 conv, m = `tile` in {2, 4} (ResnetBlock conv1 / conv2 and
+ * the mid blocks at the 8x8 / 16x16 levels, encoder_decoder.py:123-170; forward, input gradient, weight gradient),
+ * 3xBF16 math mode only; a = m + 2, P = a^2 transformed positions, T = nb (h/m) (w/m) output tiles. Stages on the
+ * stream: U = G g G^T of the filters, V = B^T d B of the input's a x a patches, M_xi = V_xi U_xi^T for the P positions
+ * (one batched MFMA GEMM: P / (9 m^2) of the direct conv's MACs -- 4/9 at m = 2, 1/4 at m = 4), output A^T M A
+ * (+ bias, + residual, + the following GroupNorm's statistics). The input gradient is the same conv of dy with the
+ * flipped, transposed filters (weight_transform dgrad = 1) and may emit the GroupNorm backward partials of
  * mvae_conv2d_dgrad_gnbwd_nhwc (output_gnbwd). V, U: split4_bf16 (16 B per 4 values), M: fp32. Conditions: w in
- * {8, 16}, h even, h w % 32 == 0, channel counts % 4 == 0, 16-B aligned operands.
- *   weight_transform: w [cout][3][3][cin] -> u [16][cout][cin] (dgrad 0) or [16][cin][cout] (dgrad 1)
- *   input_transform:  x [nb][h][w][c] (fp32, or split4_bf16 groups when x_split) -> v [16][T][c]
- *   gemm:             m [16][tiles][n_out] = v . u^T over k_in
+ * {8, 16}, h % 4 == 0, channel counts % 4 == 0, 16-B aligned operands.
+ *   weight_transform: w [cout][3][3][cin] -> u [P][cout][cin] (dgrad 0) or [P][cin][cout] (dgrad 1)
+ *   input_transform:  x [nb][h][w][c] (fp32, or split4_bf16 groups when x_split) -> v [P][T][c]
+ *   gemm:             m [P][tiles][n_out] = v . u^T over k_in
  *   output_transform: m -> y [nb][h][w][n] (+ bias[n]) (+ residual [nb][h][w][n]); gn_part as mvae_conv2d_gnstats_nhwc
- *   output_gnbwd:     m -> dx, part as mvae_conv2d_dgrad_gnbwd_nhwc (x, mean, rstd, gamma, beta: that GroupNorm's) */
-int mvae_winograd_weight_transform(const float* w, void* u, int cin, int cout, int dgrad, void* stream);
-int mvae_winograd_input_transform(const float* x, void* v, int nb, int h, int w, int c, int x_split, void* stream);
-int mvae_winograd_gemm(const void* v, const void* u, float* m, long long tiles, int k_in, int n_out, void* stream);
-int mvae_winograd_output_transform(const float* m, const float* bias, const float* residual, float* y, double* gn_part,
-                                   int nb, int h, int w, int n, void* stream);
-int mvae_winograd_output_gnbwd(const float* m, float* dx, const float* x, const float* mean, const float* rstd,
-                               const float* gamma, const float* beta, int groups, int silu, double* part, int nb, int h,
-                               int w, int n, void* stream);
-size_t mvae_winograd_workspace_bytes(int nb, int h, int w, int cin, int cout);
-/* Weight gradient of the same convs, F(3x3, 2x2) on the same tiles: dw = beta*dw + G^T M G with
- * M_xi = sum_tiles D'_xi (x) V_xi, D' = A D A^T of the 2x2 output-gradient tiles, V the forward's input transform.
- *   dy_transform:  dy [nb][h][w][k] (fp32, or split4_bf16 groups when dy_split) -> d [16][T][k] split4_bf16
- *   wgrad_gemm:    m [16][cout][cin] = sum over tiles d^T v (split over the tiles within workspace:
- *                  mvae_gemm_workspace_bytes(cout, cin, tiles, 16))
+ *   output_gnbwd:     m -> dx, part as mvae_conv2d_dgrad_gnbwd_nhwc (x, mean, rstd, gamma, beta: that GroupNorm's)
+ * Weight gradient, F(3x3, m x m) on the same tiles: dw = beta*dw + G^T M G with M_xi = sum_tiles D'_xi (x) V_xi,
+ * D' = A D A^T of the m x m output-gradient tiles, V the forward's input transform:
+ *   dy_transform:  dy [nb][h][w][k] (fp32, or split4_bf16 groups when dy_split) -> d [P][T][k] split4_bf16
+ *   wgrad_gemm:    m [P][cout][cin] = sum over tiles d^T v (split over the tiles within workspace:
+ *                  mvae_gemm_workspace_bytes(cout, cin, tiles, P))
  *   wgrad_output:  dw [cout][3][3][cin] = beta*dw + G^T m G
  * The conv bias gradient is not produced here (mvae_bias_grad, or the GroupNorm backward that split dy). */
-int mvae_winograd_dy_transform(const float* dy, void* d, int nb, int h, int w, int k, int dy_split, void* stream);
-int mvae_winograd_wgrad_gemm(const void* d, const void* v, float* m, long long tiles, int cout, int cin, float* workspace,
-                             size_t workspace_bytes, void* stream);
-int mvae_winograd_wgrad_output(const float* m, float* dw, float beta, int cout, int cin, void* stream);
+int mvae_winograd_weight_transform(const float* w, void* u, int cin, int cout, int dgrad, int tile, void* stream);
+int mvae_winograd_input_transform(const float* x, void* v, int nb, int h, int w, int c, int x_split, int tile,
+                                  void* stream);
+int mvae_winograd_gemm(const void* v, const void* u, float* m, long long tiles, int k_in, int n_out, int tile,
+                       void* stream);
+int mvae_winograd_output_transform(const float* m, const float* bias, const float* residual, float* y, double* gn_part,
+                                   int nb, int h, int w, int n, int tile, void* stream);
+int mvae_winograd_output_gnbwd(const float* m, float* dx, const float* x, const float* mean, const float* rstd,
+                               const float* gamma, const float* beta, int groups, int silu, double* part, int nb, int h,
+                               int w, int n, int tile, void* stream);
+int mvae_winograd_dy_transform(const float* dy, void* d, int nb, int h, int w, int k, int dy_split, int tile,
+                               void* stream);
+int mvae_winograd_wgrad_gemm(const void* d, const void* v, float* m, long long tiles, int cout, int cin, int tile,
+                             float* workspace, size_t workspace_bytes, void* stream);
+int mvae_winograd_wgrad_output(const float* m, float* dw, float beta, int cout, int cin, int tile, void* stream);
 
 /* 3xBF16 operand pre-split (same bytes as the fp32 tensor): per 4 values hi0..hi3 lo0..lo3 bf16,
  * hi = bf16(x) (round to nearest even), lo = bf16(x - hi). The weight-prep entry points below take

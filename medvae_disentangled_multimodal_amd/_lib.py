@@ -33,15 +33,14 @@ SIGNATURES = {
     "mvae_conv2d_gnstats_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P]),
     "mvae_conv2d_dgrad_gnbwd_nhwc": (I, [P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P, P, I, I, P, P]),
     "mvae_conv2d_wgrad_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),
-    "mvae_winograd_weight_transform": (I, [P, P, I, I, I, P]),
-    "mvae_winograd_input_transform": (I, [P, P, I, I, I, I, I, P]),
-    "mvae_winograd_gemm": (I, [P, P, P, L, I, I, P]),
-    "mvae_winograd_output_transform": (I, [P, P, P, P, P, I, I, I, I, P]),
-    "mvae_winograd_output_gnbwd": (I, [P, P, P, P, P, P, P, I, I, P, I, I, I, I, P]),
-    "mvae_winograd_workspace_bytes": (Z, [I, I, I, I, I]),
-    "mvae_winograd_dy_transform": (I, [P, P, I, I, I, I, I, P]),
-    "mvae_winograd_wgrad_gemm": (I, [P, P, P, L, I, I, P, Z, P]),
-    "mvae_winograd_wgrad_output": (I, [P, P, F, I, I, P]),
+    "mvae_winograd_weight_transform": (I, [P, P, I, I, I, I, P]),
+    "mvae_winograd_input_transform": (I, [P, P, I, I, I, I, I, I, P]),
+    "mvae_winograd_gemm": (I, [P, P, P, L, I, I, I, P]),
+    "mvae_winograd_output_transform": (I, [P, P, P, P, P, I, I, I, I, I, P]),
+    "mvae_winograd_output_gnbwd": (I, [P, P, P, P, P, P, P, I, I, P, I, I, I, I, I, P]),
+    "mvae_winograd_dy_transform": (I, [P, P, I, I, I, I, I, I, P]),
+    "mvae_winograd_wgrad_gemm": (I, [P, P, P, L, I, I, I, P, Z, P]),
+    "mvae_winograd_wgrad_output": (I, [P, P, F, I, I, I, P]),
     "mvae_conv2d_wgrad_workspace_bytes": (Z, [I, I, I, I, I, I, I]),
     "mvae_conv2d_wgrad_small_cout_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, I, P, Z, P]),
     "mvae_conv2d_wgrad_small_cout_workspace_bytes": (Z, [I, I]),

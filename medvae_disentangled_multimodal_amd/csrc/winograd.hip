@@ -1,223 +1,205 @@
-// Winograd F(2x2, 3x3) convolution for the 3x3 / stride-1 / pad-1 convs of the low-resolution, wide levels (c4 / c5's
-// 8x8 x 2048 and 16x16 x 1024: ResnetBlock conv1 / conv2, the mid blocks -- src/models/encoder_decoder.py:123-170) in the
-// fp32-class (3xBF16) arithmetic: forward, input gradient and weight gradient (F(3x3, 2x2), below).
+// Winograd convolution F(m x m, 3x3), m = 2 or 4, for the 3x3 / stride-1 / pad-1 convs of the low-resolution, wide levels
+// (c4 / c5's 8x8 x 2048 and 16x16 x 1024: ResnetBlock conv1 / conv2, the mid blocks -- src/models/encoder_decoder.py:
+// 123-170) in the fp32-class (3xBF16) arithmetic: forward, input gradient and weight gradient.
 //
-// Per 2x2 output tile t and channel c the 4x4 input patch d is transformed to V = B^T d B, the 3x3 filter g of (k, c) to
-// U = G g G^T, the 16 transformed positions xi are independent GEMMs M_xi[t][k] = sum_c V_xi[t][c] U_xi[k][c], and the
-// tile's outputs are A^T M A:
-//   B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1],  G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1],
-//   A^T = [1 1 1 0; 0 1 -1 -1]
-// 16 multiplies per output tile instead of 36: the GEMM work is 4/9 of the direct conv's. The transforms are additions
-// (and halvings) of fp32 values; V and U are written in the 3xBF16 pre-split layout (split4_bf16) so the batched GEMM
-// (gemm3x_kernel, A_ROWK_SPLIT x B_ROWK_SPLIT, 16 batch entries) stages them without split arithmetic. Its cost against
-// the direct conv is the traffic of V (16 / 4 = 4x the input) and M (4x the output) -- small next to the GEMM when the
-// channel count is large and the image small, which is where the dispatcher (ops.py) uses it.
+// Per m x m output tile t and channel c the a x a input patch d (a = m + 2) is transformed to V = B^T d B, the 3x3 filter
+// g of (k, c) to U = G g G^T, the a^2 transformed positions xi are independent GEMMs M_xi[t][k] = sum_c V_xi[t][c]
+// U_xi[k][c], and the tile's outputs are A^T M A. a^2 multiplies per output tile instead of 9 m^2: the GEMM work is
+// 16/36 = 4/9 (m = 2) or 36/144 = 1/4 (m = 4) of the direct conv's.
+//   m = 2: B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1], G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1],
+//          A^T = [1 1 1 0; 0 1 -1 -1]
+//   m = 4: points 0, +-1, +-2, inf (wino_bt / wino_g / wino_at below)
+// The transforms run in fp32; V and U are written in the 3xBF16 pre-split layout (split4_bf16) so the batched GEMM
+// (gemm3x_kernel, A_ROWK_SPLIT x B_ROWK_SPLIT, a^2 batch entries) stages them without split arithmetic. Error against
+// float64 (tests/test_gpu_winograd.py): m = 2 ~1e-5, m = 4 ~5e-5 norm-wise relative (the larger m = 4 coefficients
+// amplify the 3xBF16 operand rounding; the north_star bar is 1e-3). The cost against the direct conv is the transform
+// traffic -- V is a^2 / m^2 times the input (4x for m = 2, 2.25x for m = 4), M as much of the output -- small next to
+// the GEMM when the channel count is large and the image small, which is where the dispatcher (ops.py) uses it.
 //
-// The input gradient of the same conv is a 3x3 / stride-1 / pad-1 conv of dy with the flipped, transposed filters
-// g'(c, k)[r][s] = g(k, c)[2-r][2-s]: the same four stages with U' (mvae_winograd_weight_transform's dgrad form).
-// The output transform can add the conv bias and the ResnetBlock residual and emits the following GroupNorm's
-// statistics in the GEMM epilogue's layout (per 32-pixel block and 4-channel group, fp64 {sum y, sum y^2}).
+// The input gradient is a 3x3 / stride-1 / pad-1 conv of dy with the flipped, transposed filters g'(c, k)[r][s] =
+// g(k, c)[2-r][2-s]: the same stages with U' (mvae_winograd_weight_transform's dgrad form). The output transform can add
+// the conv bias and the ResnetBlock residual and emits the following GroupNorm's statistics in the GEMM epilogue's
+// layout (per 32-pixel block and 4-channel group, fp64 {sum y, sum y^2}), or, for an input gradient, the GroupNorm
+// backward partials of mvae_conv2d_dgrad_gnbwd_nhwc.
+//
+// Weight gradient: with D_t the m x m output-gradient tile and X_t the input patch of tile t, dW[r][s] =
+// sum_t sum_{u,e} D_t[u][e] X_t[u+r][e+s] = G^T [ sum_t (A D_t A^T) (.) (B^T X_t B) ] G -- the bilinear form of the
+// forward identity differentiated by the filter. So dW = G^T M G with M_xi[k][c] = sum_t D'_xi[t][k] V_xi[t][c]: a^2
+// GEMMs over the tiles (K = T) of the transformed output gradient D' = A D A^T and the forward's V.
 #include "gemm_core.h"
 
 namespace mvae {
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) { return float4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
-__device__ __forceinline__ float4 f4sub(float4 a, float4 b) { return float4{a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w}; }
-__device__ __forceinline__ float4 f4scale(float4 a, float s) { return float4{a.x * s, a.y * s, a.z * s, a.w * s}; }
 
-// B^T d B of a 4x4 patch of float4 channel groups, in place: rows, then columns
-__device__ __forceinline__ void wino_bt(float4 (&d)[4][4]) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float4 r0 = f4sub(d[0][j], d[2][j]), r1 = f4add(d[1][j], d[2][j]);
-    const float4 r2 = f4sub(d[2][j], d[1][j]), r3 = f4sub(d[1][j], d[3][j]);
-    d[0][j] = r0; d[1][j] = r1; d[2][j] = r2; d[3][j] = r3;
+// transform coefficients (compile-time after unrolling: zero terms vanish, +-1 terms are adds / subtracts)
+template <int MT>
+__host__ __device__ constexpr float wino_bt(int i, int j) {  // B^T [a][a]
+  if constexpr (MT == 2) {
+    constexpr float m[4][4] = {{1, 0, -1, 0}, {0, 1, 1, 0}, {0, -1, 1, 0}, {0, 1, 0, -1}};
+    return m[i][j];
+  } else {
+    constexpr float m[6][6] = {{4, 0, -5, 0, 1, 0},  {0, -4, -4, 1, 1, 0}, {0, 4, -4, -1, 1, 0},
+                               {0, -2, -1, 2, 1, 0}, {0, 2, -1, -2, 1, 0}, {0, 4, 0, -5, 0, 1}};
+    return m[i][j];
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float4 c0 = f4sub(d[i][0], d[i][2]), c1 = f4add(d[i][1], d[i][2]);
-    const float4 c2 = f4sub(d[i][2], d[i][1]), c3 = f4sub(d[i][1], d[i][3]);
-    d[i][0] = c0; d[i][1] = c1; d[i][2] = c2; d[i][3] = c3;
+}
+template <int MT>
+__host__ __device__ constexpr float wino_g(int i, int j) {  // G [a][3]
+  if constexpr (MT == 2) {
+    constexpr float m[4][3] = {{1, 0, 0}, {0.5f, 0.5f, 0.5f}, {0.5f, -0.5f, 0.5f}, {0, 0, 1}};
+    return m[i][j];
+  } else {
+    constexpr float m[6][3] = {{0.25f, 0, 0},
+                               {-1.f / 6, -1.f / 6, -1.f / 6},
+                               {-1.f / 6, 1.f / 6, -1.f / 6},
+                               {1.f / 24, 1.f / 12, 1.f / 6},
+                               {1.f / 24, -1.f / 12, 1.f / 6},
+                               {0, 0, 1}};
+    return m[i][j];
+  }
+}
+template <int MT>
+__host__ __device__ constexpr float wino_at(int i, int j) {  // A^T [m][a]
+  if constexpr (MT == 2) {
+    constexpr float m[2][4] = {{1, 1, 1, 0}, {0, 1, -1, -1}};
+    return m[i][j];
+  } else {
+    constexpr float m[4][6] = {{1, 1, 1, 1, 1, 0}, {0, 1, -1, 2, -2, 0}, {0, 1, 1, 4, 4, 0}, {0, 1, -1, 8, -8, 1}};
+    return m[i][j];
   }
 }
 
-// x [nb][H][W][C] (fp32, or split4_bf16 groups when XS) -> V [16][T][C] split4_bf16, T = nb (H/2) (W/2)
-// one thread per (tile, 4-channel group): 16 coalesced 16-B loads (zeros outside the image), 16 16-B stores
-template <bool XS>
+// acc (+)= c * v, with `first` a compile-time flag after unrolling
+__device__ __forceinline__ void wmadd(float4& acc, bool& first, float c, float4 v) {
+  if (c == 0.f) return;
+  float4 t;
+  if (c == 1.f) t = v;
+  else if (c == -1.f) t = float4{-v.x, -v.y, -v.z, -v.w};
+  else t = float4{c * v.x, c * v.y, c * v.z, c * v.w};
+  if (first) {
+    acc = t;
+    first = false;
+  } else if (c == -1.f) {
+    acc = float4{acc.x - v.x, acc.y - v.y, acc.z - v.z, acc.w - v.w};
+  } else {
+    acc = f4add(acc, t);
+  }
+}
+
+// y[i] = sum_k C(i, k) x[k] for i < RO, k < RI, over float4 vectors with strides (x, y may alias only if RO == RI and
+// the caller copies); COEF(i, k) is a constexpr coefficient function
+template <int RO, int RI, typename F>
+__device__ __forceinline__ void wlin(float4* y, int ys, const float4* x, int xs, F coef) {
+  float4 t[RO];
+#pragma unroll
+  for (int i = 0; i < RO; ++i) {
+    bool first = true;
+    t[i] = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < RI; ++k) wmadd(t[i], first, coef(i, k), x[k * xs]);
+  }
+#pragma unroll
+  for (int i = 0; i < RO; ++i) y[i * ys] = t[i];
+}
+
+__device__ __forceinline__ float4 split4_to_f32(float4 r) {  // split4_bf16 group (hi0..hi3 lo0..lo3) -> hi + lo
+  const unsigned h01 = __float_as_uint(r.x), h23 = __float_as_uint(r.y);
+  const unsigned l01 = __float_as_uint(r.z), l23 = __float_as_uint(r.w);
+  return float4{__uint_as_float(h01 << 16) + __uint_as_float(l01 << 16),
+                __uint_as_float(h01 & 0xFFFF0000u) + __uint_as_float(l01 & 0xFFFF0000u),
+                __uint_as_float(h23 << 16) + __uint_as_float(l23 << 16),
+                __uint_as_float(h23 & 0xFFFF0000u) + __uint_as_float(l23 & 0xFFFF0000u)};
+}
+
+// x [nb][H][W][C] (fp32, or split4_bf16 groups when XS) -> V [a^2][T][C] split4_bf16, T = nb (H/m) (W/m)
+// one thread per (tile, 4-channel group): a^2 coalesced 16-B loads (zeros outside the image), a^2 16-B stores
+template <int MT, bool XS>
 __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ x, uint4* __restrict__ v, int nb, int H,
                                                       int W, int C) {
-  const int C4 = C >> 2, th = H >> 1, tw = W >> 1;
+  constexpr int AL = MT + 2;
+  const int C4 = C >> 2, th = H / MT, tw = W / MT;
   const long long T = (long long)nb * th * tw;
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= T * C4) return;
   const long long t = idx / C4;
   const int c4 = (int)(idx - t * C4);
   const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
-  float4 d[4][4];
+  float4 d[AL][AL];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int h = 2 * ti - 1 + i, w = 2 * tj - 1 + j;
+    for (int j = 0; j < AL; ++j) {
+      const int h = MT * ti - 1 + i, w = MT * tj - 1 + j;
       float4 val{0.f, 0.f, 0.f, 0.f};
       if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
         const float4 r = *(const float4*)(x + (((long long)b * H + h) * W + w) * C + c4 * 4);
-        if constexpr (XS) {  // split4: hi0..hi3 then lo0..lo3 as bf16 -> fp32 hi + lo
-          const unsigned h01 = __float_as_uint(r.x), h23 = __float_as_uint(r.y);
-          const unsigned l01 = __float_as_uint(r.z), l23 = __float_as_uint(r.w);
-          val = float4{__uint_as_float(h01 << 16) + __uint_as_float(l01 << 16),
-                       __uint_as_float(h01 & 0xFFFF0000u) + __uint_as_float(l01 & 0xFFFF0000u),
-                       __uint_as_float(h23 << 16) + __uint_as_float(l23 << 16),
-                       __uint_as_float(h23 & 0xFFFF0000u) + __uint_as_float(l23 & 0xFFFF0000u)};
-        } else {
-          val = r;
-        }
+        val = XS ? split4_to_f32(r) : r;
       }
       d[i][j] = val;
     }
-  wino_bt(d);
+  constexpr auto bt = [](int i, int k) { return wino_bt<MT>(i, k); };
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int j = 0; j < AL; ++j) wlin<AL, AL>(&d[0][j], AL, &d[0][j], AL, bt);  // columns: B^T d
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[((long long)(i * 4 + j) * T + t) * C4 + c4] = split4_bf16(d[i][j]);
-}
-
-// Weight gradient (F(3x3, 2x2) on the same tiles): with D_t the 2x2 output-gradient tile and X_t the input patch of
-// tile t, dW[r][s] = sum_t sum_{a,e} D_t[a][e] X_t[a+r][e+s] = G^T [ sum_t (A D_t A^T) (.) (B^T X_t B) ] G -- the bilinear
-// form of the forward identity differentiated by the filter. So dW = G^T M G with M_xi[k][c] = sum_t D'_xi[t][k]
-// V_xi[t][c]: 16 GEMMs over the tiles (K = T) of the transformed output gradient D' = A D A^T (A = (A^T)^T, rows
-// [1 0; 1 1; 1 -1; 0 -1]) and the forward's V.
-
-// dy [nb][H][W][K] (fp32, or split4_bf16 groups when XS) -> D' [16][T][K] split4_bf16: one thread per (tile, 4-group)
-template <bool XS>
-__global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ dy, uint4* __restrict__ d, int nb, int H,
-                                                      int W, int K) {
-  const int K4 = K >> 2, th = H >> 1, tw = W >> 1;
-  const long long T = (long long)nb * th * tw;
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= T * K4) return;
-  const long long t = idx / K4;
-  const int k4 = (int)(idx - t * K4);
-  const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
-  float4 v[2][2];
+  for (int i = 0; i < AL; ++i) wlin<AL, AL>(&d[i][0], 1, &d[i][0], 1, bt);    // rows: (B^T d) B
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const float4 r = *(const float4*)(dy + (((long long)b * H + 2 * ti + a) * W + 2 * tj + e) * K + k4 * 4);
-      if constexpr (XS) {
-        const unsigned h01 = __float_as_uint(r.x), h23 = __float_as_uint(r.y);
-        const unsigned l01 = __float_as_uint(r.z), l23 = __float_as_uint(r.w);
-        v[a][e] = float4{__uint_as_float(h01 << 16) + __uint_as_float(l01 << 16),
-                         __uint_as_float(h01 & 0xFFFF0000u) + __uint_as_float(l01 & 0xFFFF0000u),
-                         __uint_as_float(h23 << 16) + __uint_as_float(l23 << 16),
-                         __uint_as_float(h23 & 0xFFFF0000u) + __uint_as_float(l23 & 0xFFFF0000u)};
-      } else {
-        v[a][e] = r;
-      }
-    }
-  float4 c[4][2];  // A D: rows
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    c[0][e] = v[0][e];
-    c[1][e] = f4add(v[0][e], v[1][e]);
-    c[2][e] = f4sub(v[0][e], v[1][e]);
-    c[3][e] = f4scale(v[1][e], -1.f);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float4 o[4] = {c[i][0], f4add(c[i][0], c[i][1]), f4sub(c[i][0], c[i][1]), f4scale(c[i][1], -1.f)};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) d[((long long)(i * 4 + j) * T + t) * K4 + k4] = split4_bf16(o[j]);
-  }
-}
-
-// dw [cout][3][3][cin] = beta * dw + G^T M G, M [16][cout][cin] fp32: one thread per (k, 4-group of c)
-__global__ void __launch_bounds__(256) wino_wout_kernel(const float* __restrict__ m, float* __restrict__ dw, float beta,
-                                                        int cout, int cin) {
-  const int C4 = cin >> 2;
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long long)cout * C4) return;
-  const long long mn = (long long)cout * cin;
-  float4 mv[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) mv[i][j] = *(const float4*)(m + (i * 4 + j) * mn + idx * 4);
-  float4 r[3][4];  // G^T M
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    r[0][j] = f4add(mv[0][j], f4scale(f4add(mv[1][j], mv[2][j]), 0.5f));
-    r[1][j] = f4scale(f4sub(mv[1][j], mv[2][j]), 0.5f);
-    r[2][j] = f4add(f4scale(f4add(mv[1][j], mv[2][j]), 0.5f), mv[3][j]);
-  }
-  const int k = (int)(idx / C4), c4 = (int)(idx - (long long)k * C4);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const float4 o[3] = {f4add(r[i][0], f4scale(f4add(r[i][1], r[i][2]), 0.5f)), f4scale(f4sub(r[i][1], r[i][2]), 0.5f),
-                         f4add(f4scale(f4add(r[i][1], r[i][2]), 0.5f), r[i][3])};
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float4* p = (float4*)(dw + (((long long)k * 3 + i) * 3 + j) * cin + c4 * 4);
-      float4 v = o[j];
-      if (beta != 0.f) v = f4add(v, f4scale(*p, beta));
-      *p = v;
-    }
-  }
+    for (int j = 0; j < AL; ++j) v[((long long)(i * AL + j) * T + t) * C4 + c4] = split4_bf16(d[i][j]);
 }
 
 // G g G^T of a 3x3 filter of float4 groups
-__device__ __forceinline__ void wino_g(const float4 (&g)[3][3], float4 (&o)[4][4]) {
-  float4 t[4][3];
+template <int MT>
+__device__ __forceinline__ void wino_filter(const float4 (&g)[3][3], float4 (&o)[MT + 2][MT + 2]) {
+  constexpr int AL = MT + 2;
+  constexpr auto gc = [](int i, int k) { return wino_g<MT>(i, k); };
+  float4 t[AL][3];
 #pragma unroll
-  for (int s = 0; s < 3; ++s) {
-    t[0][s] = g[0][s];
-    t[1][s] = f4scale(f4add(f4add(g[0][s], g[1][s]), g[2][s]), 0.5f);
-    t[2][s] = f4scale(f4add(f4sub(g[0][s], g[1][s]), g[2][s]), 0.5f);
-    t[3][s] = g[2][s];
-  }
+  for (int s = 0; s < 3; ++s) wlin<AL, 3>(&t[0][s], 3, &g[0][s], 3, gc);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    o[i][0] = t[i][0];
-    o[i][1] = f4scale(f4add(f4add(t[i][0], t[i][1]), t[i][2]), 0.5f);
-    o[i][2] = f4scale(f4add(f4sub(t[i][0], t[i][1]), t[i][2]), 0.5f);
-    o[i][3] = t[i][2];
-  }
+  for (int i = 0; i < AL; ++i) wlin<AL, 3>(&o[i][0], 1, &t[i][0], 1, gc);
 }
 
-// forward filters U[16][cout][cin] split4_bf16 from KRSC weights w [cout][3][3][cin], g(n, k) = w[n][.][.][k]:
-// one thread per (cout n, 4-group of cin k), 9 coalesced 16-B loads, 16 coalesced 16-B stores
+// forward filters U[a^2][cout][cin] split4_bf16 from KRSC weights w [cout][3][3][cin], g(n, k) = w[n][.][.][k]:
+// one thread per (cout n, 4-group of cin k), 9 coalesced 16-B loads, a^2 coalesced 16-B stores
+template <int MT>
 __global__ void __launch_bounds__(256) wino_wt_fwd_kernel(const float* __restrict__ w, uint4* __restrict__ u, int cout,
                                                           int cin) {
+  constexpr int AL = MT + 2;
   const int K4 = cin >> 2;
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long long)cout * K4) return;
   const int n = (int)(idx / K4), k4 = (int)(idx - (long long)n * K4);
-  float4 g[3][3], o[4][4];
+  float4 g[3][3], o[AL][AL];
 #pragma unroll
   for (int r = 0; r < 3; ++r)
 #pragma unroll
     for (int s = 0; s < 3; ++s) g[r][s] = *(const float4*)(w + (((long long)n * 3 + r) * 3 + s) * cin + k4 * 4);
-  wino_g(g, o);
+  wino_filter<MT>(g, o);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) u[((long long)(i * 4 + j) * cout + n) * K4 + k4] = split4_bf16(o[i][j]);
+    for (int j = 0; j < AL; ++j) u[((long long)(i * AL + j) * cout + n) * K4 + k4] = split4_bf16(o[i][j]);
 }
 
-// input-gradient filters U'[16][cin][cout] split4_bf16, g'(n = cin, k = cout)[r][s] = w[k][2-r][2-s][n]: the source
-// is contiguous along n and the destination along k, so a workgroup transposes a 32 (n) x 8 (k groups of 4) block
-// through LDS: loads coalesced over n (32 lanes), stores in 128-B runs over k
-constexpr int WDG_N = 32, WDG_K4 = 8;
+// input-gradient filters U'[a^2][cin][cout] split4_bf16, g'(n = cin, k = cout)[r][s] = w[k][2-r][2-s][n]: the source is
+// contiguous along n and the destination along k, so a workgroup transposes a 32 (n) x KQ (k groups of 4) block through
+// LDS: loads coalesced over n (32 lanes), stores in KQ * 16-B runs over k
+constexpr int WDG_N = 32;
+template <int MT>
+constexpr int wdg_kq() { return MT == 2 ? 8 : 4; }
+template <int MT>
 __global__ void __launch_bounds__(256) wino_wt_dgrad_kernel(const float* __restrict__ w, uint4* __restrict__ u,
                                                             int cout, int cin) {
-  __shared__ uint4 lds[16][WDG_N][WDG_K4];  // 64 KB
+  constexpr int AL = MT + 2, KQ = wdg_kq<MT>(), NT = WDG_N * KQ;
+  __shared__ uint4 lds[AL * AL][WDG_N][KQ];  // 64 KB (m = 2), 72 KB (m = 4)
   const int K4 = cout >> 2;
-  const int n0 = blockIdx.x * WDG_N, kb = blockIdx.y * WDG_K4;
-  const int nl = threadIdx.x & (WDG_N - 1), kq = threadIdx.x / WDG_N;
+  const int n0 = blockIdx.x * WDG_N, kb = blockIdx.y * KQ;
+  const int nl = threadIdx.x % WDG_N, kq = threadIdx.x / WDG_N;
   const int n = n0 + nl, k4 = kb + kq;
   if (n < cin && k4 < K4) {
-    float4 g[3][3], o[4][4];
+    float4 g[3][3], o[AL][AL];
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -227,25 +209,23 @@ __global__ void __launch_bounds__(256) wino_wt_dgrad_kernel(const float* __restr
         for (int q = 0; q < 4; ++q) e[q] = w[(((long long)(k4 * 4 + q) * 3 + (2 - r)) * 3 + (2 - s)) * cin + n];
         g[r][s] = float4{e[0], e[1], e[2], e[3]};
       }
-    wino_g(g, o);
+    wino_filter<MT>(g, o);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < AL; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) lds[i * 4 + j][nl][kq] = split4_bf16(o[i][j]);
+      for (int j = 0; j < AL; ++j) lds[i * AL + j][nl][kq] = split4_bf16(o[i][j]);
   }
   __syncthreads();
-#pragma unroll
-  for (int it = 0; it < 16 * WDG_N * WDG_K4 / 256; ++it) {
-    const int e = it * 256 + threadIdx.x;
-    const int xi = e / (WDG_N * WDG_K4), rem = e % (WDG_N * WDG_K4);
-    const int nn = n0 + rem / WDG_K4, kk = kb + rem % WDG_K4;
-    if (nn < cin && kk < K4) u[((long long)xi * cin + nn) * K4 + kk] = lds[xi][rem / WDG_K4][rem % WDG_K4];
+  for (int e = threadIdx.x; e < AL * AL * WDG_N * KQ; e += NT) {
+    const int xi = e / (WDG_N * KQ), rem = e % (WDG_N * KQ);
+    const int nn = n0 + rem / KQ, kk = kb + rem % KQ;
+    if (nn < cin && kk < K4) u[((long long)xi * cin + nn) * K4 + kk] = lds[xi][rem / KQ][rem % KQ];
   }
 }
 
 // output transform operands
 struct WinoOut {
-  const float* m;      // [16][T][N] fp32 GEMM results
+  const float* m;      // [a^2][T][N] fp32 GEMM results
   const float* bias;   // [N] or null
   const float* res;    // residual [nb][H][W][N] or null
   float* y;            // [nb][H][W][N]
@@ -260,21 +240,42 @@ struct WinoOut {
   int nb, H, W, N;
 };
 
-// M -> y = A^T M A (+ bias) (+ residual) for W in {8, 16}: 8 consecutive tiles are one 32-pixel block of the row-major
-// pixel order (2 tile rows of an 8-wide image, 1 of a 16-wide one). One thread per (block of 8 tiles, 4-channel group);
-// the channel groups of a block are consecutive threads (coalesced 16-B loads / stores).
-template <bool GNB>
+// M -> y = A^T M A (+ bias) (+ residual). A thread covers whole 32-pixel blocks of the statistics layouts: TR tile rows
+// x CT tiles of one image, i.e. an (TR m) x WSEG pixel window with WSEG = min(W, 32) (W in {8, 16}: the full width, TR
+// = 32 / (m W) tile rows when that is > 1; W a multiple of 32: one tile row of a 32-pixel column segment) -- NBK = TR m
+// WSEG / 32 blocks, each block's sums in registers (compile-time index). Threads of a group are consecutive 4-channel
+// groups (coalesced 16-B loads / stores).
+template <int MT, int WSEG>
+struct WinoOutGeo {
+  static constexpr int TR = MT * WSEG >= 32 ? 1 : 32 / (MT * WSEG);
+  static constexpr int CT = WSEG / MT;
+  static constexpr int NBK = TR * MT * WSEG / 32;
+};
+
+template <int MT, int WSEG, bool GNB>
 __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
-  const int N = p.N, N4 = N >> 2, th = p.H >> 1, tw = p.W >> 1;
-  const long long T = (long long)p.nb * th * tw, nblk = T / 8;
+  constexpr int AL = MT + 2;
+  using Geo = WinoOutGeo<MT, WSEG>;
+  constexpr int TR = Geo::TR, CT = Geo::CT, NBK = Geo::NBK;
+  const int N = p.N, N4 = N >> 2, th = p.H / MT, tw = p.W / MT, nseg = p.W / WSEG;
+  const long long T = (long long)p.nb * th * tw;
+  const long long ngrp = (long long)p.nb * (th / TR) * nseg;
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= nblk * N4) return;
-  const long long blk = idx / N4;
-  const int c4 = (int)(idx - blk * N4);
+  if (idx >= ngrp * N4) return;
+  const long long grp = idx / N4;
+  const int c4 = (int)(idx - grp * N4);
+  const int seg = (int)(grp % nseg);
+  const long long rg = grp / nseg;
+  const int b = (int)(rg / (th / TR)), ti0 = (int)(rg % (th / TR)) * TR, tj0 = seg * CT;
   const float4 bv = p.bias ? *(const float4*)(p.bias + c4 * 4) : float4{0.f, 0.f, 0.f, 0.f};
-  double s0 = 0.0, s1 = 0.0;
-  double g0[4] = {0.0, 0.0, 0.0, 0.0}, g1[4] = {0.0, 0.0, 0.0, 0.0};
-  float ggm[4], gbt[4];
+  double s0[NBK], s1[NBK], g0[GNB ? NBK : 1][4], g1[GNB ? NBK : 1][4];
+#pragma unroll
+  for (int q = 0; q < NBK; ++q) s0[q] = s1[q] = 0.0;
+#pragma unroll
+  for (int q = 0; q < (GNB ? NBK : 1); ++q)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) g0[q][u] = g1[q][u] = 0.0;
+  float ggm[4] = {0.f, 0.f, 0.f, 0.f}, gbt[4] = {0.f, 0.f, 0.f, 0.f};
   if constexpr (GNB) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -283,73 +284,183 @@ __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
     }
   }
   const int cpg = GNB ? N / p.groups : 1;
-  for (int q = 0; q < 8; ++q) {
-    const long long t = blk * 8 + q;
-    const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
-    float4 mv[4][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int tr = 0; tr < TR; ++tr)
+#pragma unroll 1
+    for (int tq = 0; tq < CT; ++tq) {
+      const int ti = ti0 + tr, tj = tj0 + tq;
+      const long long t = ((long long)b * th + ti) * tw + tj;
+      float4 mv[AL][AL];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) mv[i][j] = *(const float4*)(p.m + ((long long)(i * 4 + j) * T + t) * N + c4 * 4);
-    float4 r[2][4];  // A^T M: rows
+      for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      r[0][j] = f4add(f4add(mv[0][j], mv[1][j]), mv[2][j]);
-      r[1][j] = f4sub(f4sub(mv[1][j], mv[2][j]), mv[3][j]);
-    }
+        for (int j = 0; j < AL; ++j) mv[i][j] = *(const float4*)(p.m + ((long long)(i * AL + j) * T + t) * N + c4 * 4);
+      constexpr auto at = [](int i, int k) { return wino_at<MT>(i, k); };
+      float4 r[MT][AL];
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      const float4 o0 = f4add(f4add(r[a][0], r[a][1]), r[a][2]);
-      const float4 o1 = f4sub(f4sub(r[a][1], r[a][2]), r[a][3]);
+      for (int j = 0; j < AL; ++j) wlin<MT, AL>(&r[0][j], AL, &mv[0][j], AL, at);  // A^T M
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const long long pix = ((long long)b * p.H + 2 * ti + a) * p.W + 2 * tj + e;
-        const long long off = pix * N + c4 * 4;
-        float4 o = f4add(e == 0 ? o0 : o1, bv);
-        if (p.res) o = f4add(o, *(const float4*)(p.res + off));
-        *(float4*)(p.y + off) = o;
-        if (p.gn_part) {
-          s0 += ((double)o.x + (double)o.y) + ((double)o.z + (double)o.w);
-          s1 += ((double)o.x * o.x + (double)o.y * o.y) + ((double)o.z * o.z + (double)o.w * o.w);
-        }
-        if constexpr (GNB) {
-          const float4 x4 = *(const float4*)(p.gx + off);
-          const int bg = b * p.groups + (c4 * 4) / cpg;  // (a 4-channel group never straddles a GroupNorm group)
-          const float mu = p.mean[bg], rs = p.rstd[bg];
-          const float xs[4] = {x4.x, x4.y, x4.z, x4.w}, vs[4] = {o.x, o.y, o.z, o.w};
+      for (int a = 0; a < MT; ++a) {
+        float4 o[MT];
+        wlin<MT, AL>(o, 1, &r[a][0], 1, at);  // (A^T M) A
+        const int row = ti * MT + a;
+        const int q = ((tr * MT + a) * WSEG) / 32;  // block within the group (compile-time: tr, a unrolled)
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            float d = vs[u];
-            const float xh = (xs[u] - mu) * rs;
-            if (p.silu) {
-              const float yn = xh * ggm[u] + gbt[u];
-              const float sg = sigmoid_f(yn);
-              d = d * sg * (1.f + yn * (1.f - sg));
+        for (int e = 0; e < MT; ++e) {
+          const long long off = (((long long)b * p.H + row) * p.W + tj * MT + e) * N + c4 * 4;
+          float4 val = f4add(o[e], bv);
+          if (p.res) val = f4add(val, *(const float4*)(p.res + off));
+          *(float4*)(p.y + off) = val;
+          if (p.gn_part) {
+            s0[q] += ((double)val.x + (double)val.y) + ((double)val.z + (double)val.w);
+            s1[q] += ((double)val.x * val.x + (double)val.y * val.y) + ((double)val.z * val.z + (double)val.w * val.w);
+          }
+          if constexpr (GNB) {
+            const float4 x4 = *(const float4*)(p.gx + off);
+            const int bg = b * p.groups + (c4 * 4) / cpg;  // (a 4-channel group never straddles a GroupNorm group)
+            const float mu = p.mean[bg], rs = p.rstd[bg];
+            const float xs[4] = {x4.x, x4.y, x4.z, x4.w}, vs[4] = {val.x, val.y, val.z, val.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              float d = vs[u];
+              const float xh = (xs[u] - mu) * rs;
+              if (p.silu) {
+                const float yn = xh * ggm[u] + gbt[u];
+                const float sg = sigmoid_f(yn);
+                d = d * sg * (1.f + yn * (1.f - sg));
+              }
+              g0[q][u] += d;
+              g1[q][u] += (double)d * xh;
             }
-            g0[u] += d;
-            g1[u] += (double)d * xh;
           }
         }
       }
     }
-  }
-  if (p.gn_part) *(double2*)(p.gn_part + (blk * N4 + c4) * 2) = double2{s0, s1};
-  if constexpr (GNB) {
-    double* gp = p.gnb_part + (blk * N + c4 * 4) * 2;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) *(double2*)(gp + 2 * u) = double2{g0[u], g1[u]};
+  for (int q = 0; q < NBK; ++q) {
+    // first pixel of local block q: (q 32 / WSEG) rows down, at the group's column segment
+    const long long blk = (((long long)b * p.H + ti0 * MT + (q * 32) / WSEG) * p.W + seg * WSEG) >> 5;
+    if (p.gn_part) *(double2*)(p.gn_part + (blk * N4 + c4) * 2) = double2{s0[q], s1[q]};
+    if constexpr (GNB) {
+      double* gp = p.gnb_part + (blk * N + c4 * 4) * 2;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) *(double2*)(gp + 2 * u) = double2{g0[q][u], g1[q][u]};
+    }
   }
 }
 
-static long long wino_tiles(int nb, int h, int w) { return (long long)nb * (h / 2) * (w / 2); }
+// dy [nb][H][W][K] (fp32, or split4_bf16 groups when XS) -> D' = A D A^T [a^2][T][K] split4_bf16: one thread per
+// (tile, 4-group)
+template <int MT, bool XS>
+__global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ dy, uint4* __restrict__ d, int nb, int H,
+                                                      int W, int K) {
+  constexpr int AL = MT + 2;
+  const int K4 = K >> 2, th = H / MT, tw = W / MT;
+  const long long T = (long long)nb * th * tw;
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= T * K4) return;
+  const long long t = idx / K4;
+  const int k4 = (int)(idx - t * K4);
+  const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
+  float4 v[MT][MT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int e = 0; e < MT; ++e) {
+      const float4 r = *(const float4*)(dy + (((long long)b * H + MT * ti + a) * W + MT * tj + e) * K + k4 * 4);
+      v[a][e] = XS ? split4_to_f32(r) : r;
+    }
+  constexpr auto ac = [](int i, int k) { return wino_at<MT>(k, i); };  // A = (A^T)^T
+  float4 c[AL][MT], o[AL][AL];
+#pragma unroll
+  for (int e = 0; e < MT; ++e) wlin<AL, MT>(&c[0][e], MT, &v[0][e], MT, ac);
+#pragma unroll
+  for (int i = 0; i < AL; ++i) wlin<AL, MT>(&o[i][0], 1, &c[i][0], 1, ac);
+#pragma unroll
+  for (int i = 0; i < AL; ++i)
+#pragma unroll
+    for (int j = 0; j < AL; ++j) d[((long long)(i * AL + j) * T + t) * K4 + k4] = split4_bf16(o[i][j]);
+}
 
-static bool wino_geom_ok(int nb, int h, int w, int cin, int cout) {
-  // (h w % 32 == 0: the output transform's 8-tile blocks are the 32-pixel blocks of the statistics layouts)
-  return nb > 0 && h >= 2 && (h % 2) == 0 && (w == 8 || w == 16) && (h * w) % 32 == 0 && cin > 0 && cout > 0 &&
-         cin % 4 == 0 && cout % 4 == 0 && wino_tiles(nb, h, w) * std::max(cin, cout) * 4 <= MAX_DESC_BYTES;
+// dw [cout][3][3][cin] = beta * dw + G^T M G, M [a^2][cout][cin] fp32: one thread per (k, 4-group of c)
+template <int MT>
+__global__ void __launch_bounds__(256) wino_wout_kernel(const float* __restrict__ m, float* __restrict__ dw, float beta,
+                                                        int cout, int cin) {
+  constexpr int AL = MT + 2;
+  const int C4 = cin >> 2;
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)cout * C4) return;
+  const long long mn = (long long)cout * cin;
+  float4 mv[AL][AL];
+#pragma unroll
+  for (int i = 0; i < AL; ++i)
+#pragma unroll
+    for (int j = 0; j < AL; ++j) mv[i][j] = *(const float4*)(m + (i * AL + j) * mn + idx * 4);
+  constexpr auto gt = [](int r, int i) { return wino_g<MT>(i, r); };  // G^T
+  float4 r[3][AL], o[3][3];
+#pragma unroll
+  for (int j = 0; j < AL; ++j) wlin<3, AL>(&r[0][j], AL, &mv[0][j], AL, gt);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) wlin<3, AL>(&o[i][0], 1, &r[i][0], 1, gt);
+  const int k = (int)(idx / C4), c4 = (int)(idx - (long long)k * C4);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float4* q = (float4*)(dw + (((long long)k * 3 + i) * 3 + j) * cin + c4 * 4);
+      float4 val = o[i][j];
+      if (beta != 0.f) {
+        const float4 old = *q;
+        val = float4{fmaf(beta, old.x, val.x), fmaf(beta, old.y, val.y), fmaf(beta, old.z, val.z),
+                     fmaf(beta, old.w, val.w)};
+      }
+      *q = val;
+    }
+}
+
+static long long wino_tiles(int nb, int h, int w, int mt) { return (long long)nb * (h / mt) * (w / mt); }
+
+static bool wino_geom_ok(int mt, int nb, int h, int w, int cin, int cout) {
+  // (the output transform's thread groups are whole 32-pixel blocks of the statistics layouts: h % 4 == 0 covers
+  // every (m, w) pair: m = 2 at w = 8 takes 2 tile rows per group)
+  const long long pos = (long long)(mt + 2) * (mt + 2);
+  return (mt == 2 || mt == 4) && nb > 0 && h >= 4 && h % 4 == 0 && (w == 8 || w == 16 || (w >= 32 && w % 32 == 0)) &&
+         cin > 0 && cout > 0 && cin % 4 == 0 && cout % 4 == 0 &&
+         (long long)nb * h * w * std::max(cin, cout) * 4 <= MAX_DESC_BYTES &&
+         wino_tiles(nb, h, w, mt) * std::max(cin, cout) * 4 <= MAX_DESC_BYTES && pos > 0;
 }
 
 static int egrid256(long long n) { return (int)std::min<long long>((n + 255) / 256, 1LL << 30); }
+
+static bool wino_math_ok() {
+  if (math_mode() == MATH_3XBF16) return true;
+  set_error("winograd: the 3xBF16 (fp32-class) arithmetic only");
+  return false;
+}
+
+template <int MT, int WSEG>
+static void wino_out_go(WinoOut& p, bool gnb, hipStream_t st) {
+  using Geo = WinoOutGeo<MT, WSEG>;
+  const long long groups = (long long)p.nb * (p.H / MT / Geo::TR) * (p.W / WSEG);
+  const dim3 g(egrid256(groups * (p.N / 4)));
+  if (gnb) hipLaunchKernelGGL((wino_out_kernel<MT, WSEG, true>), g, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((wino_out_kernel<MT, WSEG, false>), g, dim3(256), 0, st, p);
+}
+
+static int wino_out_launch(WinoOut& p, int tile, bool gnb, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int wseg = std::min(p.W, 32);
+  if (tile == 2) {
+    if (wseg == 8) wino_out_go<2, 8>(p, gnb, st);
+    else if (wseg == 16) wino_out_go<2, 16>(p, gnb, st);
+    else wino_out_go<2, 32>(p, gnb, st);
+  } else {
+    if (wseg == 8) wino_out_go<4, 8>(p, gnb, st);
+    else if (wseg == 16) wino_out_go<4, 16>(p, gnb, st);
+    else wino_out_go<4, 32>(p, gnb, st);
+  }
+  return launch_status();
+}
 
 }  // namespace mvae
 
@@ -357,56 +468,63 @@ using namespace mvae;
 
 extern "C" {
 
-// U = the 16 transformed filters in split4_bf16 ([16][cout][cin] forward, [16][cin][cout] for the input gradient when
-// dgrad != 0) of KRSC 3x3 weights w [cout][3][3][cin]
-int mvae_winograd_weight_transform(const float* w, void* u, int cin, int cout, int dgrad, void* stream) {
-  if (!w || !u || cin <= 0 || cout <= 0 || cin % 4 || cout % 4 || !al16(w) || !al16(u)) {
-    set_error("winograd_weight_transform: cin, cout multiples of 4, 16-B aligned w / u");
+// U = the a^2 transformed filters in split4_bf16 ([a^2][cout][cin] forward, [a^2][cin][cout] for the input gradient
+// when dgrad != 0) of KRSC 3x3 weights w [cout][3][3][cin]; tile = m (2 or 4)
+int mvae_winograd_weight_transform(const float* w, void* u, int cin, int cout, int dgrad, int tile, void* stream) {
+  if (!w || !u || cin <= 0 || cout <= 0 || cin % 4 || cout % 4 || !al16(w) || !al16(u) || (tile != 2 && tile != 4)) {
+    set_error("winograd_weight_transform: cin, cout multiples of 4, 16-B aligned w / u, tile 2 or 4");
     return MVAE_EINVAL;
   }
-  if (math_mode() != MATH_3XBF16) {
-    set_error("winograd: the 3xBF16 (fp32-class) arithmetic only");
-    return MVAE_EINVAL;
-  }
+  if (!wino_math_ok()) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  if (dgrad)
-    hipLaunchKernelGGL(wino_wt_dgrad_kernel, dim3(cdiv(cin, WDG_N), cdiv(cout / 4, WDG_K4)), dim3(256), 0, st, w,
-                       (uint4*)u, cout, cin);
-  else
-    hipLaunchKernelGGL(wino_wt_fwd_kernel, dim3(egrid256((long long)cout * (cin / 4))), dim3(256), 0, st, w, (uint4*)u,
-                       cout, cin);
+  if (dgrad) {
+    if (tile == 2)
+      hipLaunchKernelGGL(wino_wt_dgrad_kernel<2>, dim3(cdiv(cin, WDG_N), cdiv(cout / 4, wdg_kq<2>())),
+                         dim3(WDG_N * wdg_kq<2>()), 0, st, w, (uint4*)u, cout, cin);
+    else
+      hipLaunchKernelGGL(wino_wt_dgrad_kernel<4>, dim3(cdiv(cin, WDG_N), cdiv(cout / 4, wdg_kq<4>())),
+                         dim3(WDG_N * wdg_kq<4>()), 0, st, w, (uint4*)u, cout, cin);
+  } else {
+    const dim3 g(egrid256((long long)cout * (cin / 4)));
+    if (tile == 2) hipLaunchKernelGGL(wino_wt_fwd_kernel<2>, g, dim3(256), 0, st, w, (uint4*)u, cout, cin);
+    else hipLaunchKernelGGL(wino_wt_fwd_kernel<4>, g, dim3(256), 0, st, w, (uint4*)u, cout, cin);
+  }
   return launch_status();
 }
 
-// V [16][T][c] split4_bf16 of x [nb][h][w][c] (fp32, or split4_bf16 groups when x_split), T = nb (h/2) (w/2)
-int mvae_winograd_input_transform(const float* x, void* v, int nb, int h, int w, int c, int x_split, void* stream) {
-  if (!x || !v || !wino_geom_ok(nb, h, w, c, c) || !al16(x) || !al16(v)) {
-    set_error("winograd_input_transform: even h, w in {8, 16}, h w %% 32 == 0, c %% 4 == 0, 16-B aligned");
+// V [a^2][T][c] split4_bf16 of x [nb][h][w][c] (fp32, or split4_bf16 groups when x_split), T = nb (h/m) (w/m)
+int mvae_winograd_input_transform(const float* x, void* v, int nb, int h, int w, int c, int x_split, int tile,
+                                  void* stream) {
+  if (!x || !v || !wino_geom_ok(tile, nb, h, w, c, c) || !al16(x) || !al16(v)) {
+    set_error("winograd_input_transform: tile 2 or 4, h %% 4 == 0, w in {8, 16} or a multiple of 32, c %% 4 == 0, "
+              "16-B aligned");
     return MVAE_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;
-  const long long n = wino_tiles(nb, h, w) * (c / 4);
-  if (x_split)
-    hipLaunchKernelGGL(wino_in_kernel<true>, dim3(egrid256(n)), dim3(256), 0, st, x, (uint4*)v, nb, h, w, c);
-  else
-    hipLaunchKernelGGL(wino_in_kernel<false>, dim3(egrid256(n)), dim3(256), 0, st, x, (uint4*)v, nb, h, w, c);
+  const dim3 g(egrid256(wino_tiles(nb, h, w, tile) * (c / 4)));
+  if (tile == 2) {
+    if (x_split) hipLaunchKernelGGL((wino_in_kernel<2, true>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c);
+    else hipLaunchKernelGGL((wino_in_kernel<2, false>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c);
+  } else {
+    if (x_split) hipLaunchKernelGGL((wino_in_kernel<4, true>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c);
+    else hipLaunchKernelGGL((wino_in_kernel<4, false>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c);
+  }
   return launch_status();
 }
 
-// M [16][T][n_out] fp32 = V_xi [T][k_in] . U_xi [n_out][k_in]^T for the 16 positions xi: one batched launch of the
+// M [a^2][T][n_out] fp32 = V_xi [T][k_in] . U_xi [n_out][k_in]^T for the a^2 positions xi: one batched launch of the
 // implicit-GEMM core on pre-split operands
-int mvae_winograd_gemm(const void* v, const void* u, float* m, long long tiles, int k_in, int n_out, void* stream) {
+int mvae_winograd_gemm(const void* v, const void* u, float* m, long long tiles, int k_in, int n_out, int tile,
+                       void* stream) {
   if (!v || !u || !m || tiles <= 0 || k_in <= 0 || n_out <= 0 || k_in % 4 || n_out % 4 || !al16(v) || !al16(u) ||
-      !al16(m) || tiles * std::max(k_in, n_out) * 4 > MAX_DESC_BYTES || tiles > (1LL << 30)) {
-    set_error("winograd_gemm: k_in, n_out multiples of 4, 16-B aligned, one position < 4 GiB");
+      !al16(m) || tiles * std::max(k_in, n_out) * 4 > MAX_DESC_BYTES || tiles > (1LL << 30) ||
+      (tile != 2 && tile != 4)) {
+    set_error("winograd_gemm: k_in, n_out multiples of 4, 16-B aligned, one position < 4 GiB, tile 2 or 4");
     return MVAE_EINVAL;
   }
-  if (math_mode() != MATH_3XBF16) {
-    set_error("winograd: the 3xBF16 (fp32-class) arithmetic only");
-    return MVAE_EINVAL;
-  }
+  if (!wino_math_ok()) return MVAE_EINVAL;
   GemmArgs a{};
-  a.M = (int)tiles; a.N = n_out; a.K = k_in; a.batch = 16;
+  a.M = (int)tiles; a.N = n_out; a.K = k_in; a.batch = (tile + 2) * (tile + 2);
   a.A = (const float*)v; a.lda = k_in; a.sA = tiles * k_in;
   a.B = (const float*)u; a.ldb = k_in; a.sB = (long long)n_out * k_in;
   a.C = m; a.ldc = n_out; a.sC = tiles * n_out;
@@ -422,18 +540,17 @@ int mvae_winograd_gemm(const void* v, const void* u, float* m, long long tiles, 
 // y [nb][h][w][n] = A^T M A (+ bias[n]) (+ residual, same layout as y); gn_part (nullable): the GroupNorm statistics of
 // y per 32-pixel block and 4-channel group (fp64 pairs, [nb*h*w/32][n/4][2], the mvae_conv2d_gnstats_nhwc layout)
 int mvae_winograd_output_transform(const float* m, const float* bias, const float* residual, float* y, double* gn_part,
-                                   int nb, int h, int w, int n, void* stream) {
-  if (!m || !y || !wino_geom_ok(nb, h, w, n, n) || !al16(m) || !al16(y) || (bias && !al16(bias)) ||
+                                   int nb, int h, int w, int n, int tile, void* stream) {
+  if (!m || !y || !wino_geom_ok(tile, nb, h, w, n, n) || !al16(m) || !al16(y) || (bias && !al16(bias)) ||
       (residual && !al16(residual))) {
-    set_error("winograd_output_transform: even h, w in {8, 16}, h w %% 32 == 0, n %% 4 == 0, 16-B aligned");
+    set_error("winograd_output_transform: tile 2 or 4, h %% 4 == 0, w in {8, 16} or a multiple of 32, n %% 4 == 0, "
+              "16-B aligned");
     return MVAE_EINVAL;
   }
   WinoOut p{};
   p.m = m; p.bias = bias; p.res = residual; p.y = y; p.gn_part = gn_part;
   p.groups = 1; p.nb = nb; p.H = h; p.W = w; p.N = n;
-  const long long nblk = wino_tiles(nb, h, w) / 8;
-  hipLaunchKernelGGL(wino_out_kernel<false>, dim3(egrid256(nblk * (n / 4))), dim3(256), 0, (hipStream_t)stream, p);
-  return launch_status();
+  return wino_out_launch(p, tile, false, stream);
 }
 
 // Input-gradient output transform dx = A^T M A that also emits the backward partials of the GroupNorm whose
@@ -442,51 +559,52 @@ int mvae_winograd_output_transform(const float* m, const float* bias, const floa
 // GroupNorm's input and statistics ([nb][h][w][n], [nb * groups] x 2, [n] x 2)
 int mvae_winograd_output_gnbwd(const float* m, float* dx, const float* x, const float* mean, const float* rstd,
                                const float* gamma, const float* beta, int groups, int silu, double* part, int nb, int h,
-                               int w, int n, void* stream) {
+                               int w, int n, int tile, void* stream) {
   if (!m || !dx || !x || !mean || !rstd || !gamma || !beta || !part || groups <= 0 || n % groups ||
-      (n / groups) % 4 || !wino_geom_ok(nb, h, w, n, n) || !al16(m) || !al16(dx) || !al16(x)) {
-    set_error("winograd_output_gnbwd: even h, w in {8, 16}, h w %% 32 == 0, channels per group %% 4 == 0, 16-B aligned");
+      (n / groups) % 4 || !wino_geom_ok(tile, nb, h, w, n, n) || !al16(m) || !al16(dx) || !al16(x)) {
+    set_error("winograd_output_gnbwd: tile 2 or 4, h %% 4 == 0, w in {8, 16} or a multiple of 32, channels per "
+              "group %% 4 == 0, 16-B aligned");
     return MVAE_EINVAL;
   }
   WinoOut p{};
   p.m = m; p.y = dx; p.gnb_part = part; p.gx = x; p.mean = mean; p.rstd = rstd; p.gamma = gamma; p.beta = beta;
   p.groups = groups; p.silu = silu; p.nb = nb; p.H = h; p.W = w; p.N = n;
-  const long long nblk = wino_tiles(nb, h, w) / 8;
-  hipLaunchKernelGGL(wino_out_kernel<true>, dim3(egrid256(nblk * (n / 4))), dim3(256), 0, (hipStream_t)stream, p);
-  return launch_status();
+  return wino_out_launch(p, tile, true, stream);
 }
 
-// D' [16][T][k] split4_bf16 of the output gradient dy [nb][h][w][k] (fp32, or split4_bf16 groups when dy_split)
-int mvae_winograd_dy_transform(const float* dy, void* d, int nb, int h, int w, int k, int dy_split, void* stream) {
-  if (!dy || !d || !wino_geom_ok(nb, h, w, k, k) || !al16(dy) || !al16(d)) {
-    set_error("winograd_dy_transform: even h, w in {8, 16}, h w %% 32 == 0, k %% 4 == 0, 16-B aligned");
+// D' [a^2][T][k] split4_bf16 of the output gradient dy [nb][h][w][k] (fp32, or split4_bf16 groups when dy_split)
+int mvae_winograd_dy_transform(const float* dy, void* d, int nb, int h, int w, int k, int dy_split, int tile,
+                               void* stream) {
+  if (!dy || !d || !wino_geom_ok(tile, nb, h, w, k, k) || !al16(dy) || !al16(d)) {
+    set_error("winograd_dy_transform: tile 2 or 4, h %% 4 == 0, w in {8, 16} or a multiple of 32, k %% 4 == 0, "
+              "16-B aligned");
     return MVAE_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;
-  const long long n = wino_tiles(nb, h, w) * (k / 4);
-  if (dy_split)
-    hipLaunchKernelGGL(wino_dy_kernel<true>, dim3(egrid256(n)), dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
-  else
-    hipLaunchKernelGGL(wino_dy_kernel<false>, dim3(egrid256(n)), dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
+  const dim3 g(egrid256(wino_tiles(nb, h, w, tile) * (k / 4)));
+  if (tile == 2) {
+    if (dy_split) hipLaunchKernelGGL((wino_dy_kernel<2, true>), g, dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
+    else hipLaunchKernelGGL((wino_dy_kernel<2, false>), g, dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
+  } else {
+    if (dy_split) hipLaunchKernelGGL((wino_dy_kernel<4, true>), g, dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
+    else hipLaunchKernelGGL((wino_dy_kernel<4, false>), g, dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
+  }
   return launch_status();
 }
 
-// M [16][cout][cin] fp32 = sum over the tiles of D'_xi [T][cout] (x) V_xi [T][cin]: one batched launch (COL x COL
-// images of pre-split operands), split over the tiles when the 16 products leave the chip under-filled and the
-// workspace (mvae_gemm_workspace_bytes(cout, cin, tiles, 16)) allows
-int mvae_winograd_wgrad_gemm(const void* d, const void* v, float* m, long long tiles, int cout, int cin, float* workspace,
-                             size_t workspace_bytes, void* stream) {
+// M [a^2][cout][cin] fp32 = sum over the tiles of D'_xi [T][cout] (x) V_xi [T][cin]: one batched launch (COL x COL
+// images of pre-split operands), split over the tiles when the a^2 products leave the chip under-filled and the
+// workspace (mvae_gemm_workspace_bytes(cout, cin, tiles, a^2)) allows
+int mvae_winograd_wgrad_gemm(const void* d, const void* v, float* m, long long tiles, int cout, int cin, int tile,
+                             float* workspace, size_t workspace_bytes, void* stream) {
   if (!d || !v || !m || tiles <= 0 || cout <= 0 || cin <= 0 || cout % 4 || cin % 4 || !al16(d) || !al16(v) || !al16(m) ||
-      tiles * std::max(cout, cin) * 4 > MAX_DESC_BYTES || tiles > (1LL << 30)) {
-    set_error("winograd_wgrad_gemm: cout, cin multiples of 4, 16-B aligned, one position < 4 GiB");
+      tiles * std::max(cout, cin) * 4 > MAX_DESC_BYTES || tiles > (1LL << 30) || (tile != 2 && tile != 4)) {
+    set_error("winograd_wgrad_gemm: cout, cin multiples of 4, 16-B aligned, one position < 4 GiB, tile 2 or 4");
     return MVAE_EINVAL;
   }
-  if (math_mode() != MATH_3XBF16) {
-    set_error("winograd: the 3xBF16 (fp32-class) arithmetic only");
-    return MVAE_EINVAL;
-  }
+  if (!wino_math_ok()) return MVAE_EINVAL;
   GemmArgs a{};
-  a.M = cout; a.N = cin; a.K = (int)tiles; a.batch = 16;
+  a.M = cout; a.N = cin; a.K = (int)tiles; a.batch = (tile + 2) * (tile + 2);
   a.A = (const float*)d; a.lda = cout; a.sA = tiles * cout;
   a.B = (const float*)v; a.ldb = cin; a.sB = tiles * cin;
   a.C = m; a.ldc = cin; a.sC = (long long)cout * cin;
@@ -500,21 +618,17 @@ int mvae_winograd_wgrad_gemm(const void* d, const void* v, float* m, long long t
 }
 
 // dw [cout][3][3][cin] = beta * dw + G^T M G
-int mvae_winograd_wgrad_output(const float* m, float* dw, float beta, int cout, int cin, void* stream) {
-  if (!m || !dw || cout <= 0 || cin <= 0 || cin % 4 || !al16(m) || !al16(dw)) {
-    set_error("winograd_wgrad_output: cin %% 4 == 0, 16-B aligned");
+int mvae_winograd_wgrad_output(const float* m, float* dw, float beta, int cout, int cin, int tile, void* stream) {
+  if (!m || !dw || cout <= 0 || cin <= 0 || cin % 4 || !al16(m) || !al16(dw) || (tile != 2 && tile != 4)) {
+    set_error("winograd_wgrad_output: cin %% 4 == 0, 16-B aligned, tile 2 or 4");
     return MVAE_EINVAL;
   }
-  hipLaunchKernelGGL(wino_wout_kernel, dim3(egrid256((long long)cout * (cin / 4))), dim3(256), 0, (hipStream_t)stream, m,
-                     dw, beta, cout, cin);
+  const dim3 g(egrid256((long long)cout * (cin / 4)));
+  if (tile == 2)
+    hipLaunchKernelGGL(wino_wout_kernel<2>, g, dim3(256), 0, (hipStream_t)stream, m, dw, beta, cout, cin);
+  else
+    hipLaunchKernelGGL(wino_wout_kernel<4>, g, dim3(256), 0, (hipStream_t)stream, m, dw, beta, cout, cin);
   return launch_status();
-}
-
-// workspace of the Winograd form of a conv: V (16 T cin), M (16 T cout) and U (16 cin cout), 4 B each, 256-B aligned
-size_t mvae_winograd_workspace_bytes(int nb, int h, int w, int cin, int cout) {
-  const long long t = wino_tiles(nb, h, w);
-  auto al = [](long long b) { return (size_t)((b + 255) / 256 * 256); };
-  return al(64LL * t * cin) + al(64LL * t * cout) + al(64LL * cin * cout);
 }
 
 }  // extern "C"

@@ -222,12 +222,28 @@ def _al16(*ts) -> bool:
 # MVAE_WINOGRAD_MIN_C sets the smallest channel count (both sides) it is used for.
 WINOGRAD = os.environ.get("MVAE_NO_WINOGRAD") is None
 WINOGRAD_MIN_C = int(os.environ.get("MVAE_WINOGRAD_MIN_C", "512"))
+# output tile m of F(m x m, 3x3): 4 (default; 1/4 of the direct MACs, V / M 2.25x the input / output) or 2 (4/9 of the
+# MACs, 4x the traffic, ~7x smaller transform error)
+WINOGRAD_TILE = int(os.environ.get("MVAE_WINOGRAD_TILE", "4"))
+if WINOGRAD_TILE not in (2, 4):
+    raise ValueError("MVAE_WINOGRAD_TILE must be 2 or 4")
+
+
+def _wino_alg(ref: float) -> float:
+    """GEMM FLOPs of the Winograd form of a conv whose direct form is `ref`: (m+2)^2 / (9 m^2)."""
+    m = WINOGRAD_TILE
+    return ref * (m + 2) ** 2 / (9.0 * m * m)
+
+
+# widest image it is used for (the library takes W in {8, 16} and multiples of 32)
+WINOGRAD_MAX_W = int(os.environ.get("MVAE_WINOGRAD_MAX_W", "32"))
 
 
 def _wino_ok(g, h: int, wd: int, cin: int, cout: int) -> bool:
     return (WINOGRAD and _MATH[0] == 0 and _dma_fmt() == 0 and g.kh == 3 and g.kw == 3 and g.stride == 1 and
-            not g.upsample and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and wd in (8, 16) and h % 2 == 0 and
-            (h * wd) % 32 == 0 and cin % 4 == 0 and cout % 4 == 0 and min(cin, cout) >= WINOGRAD_MIN_C)
+            not g.upsample and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and
+            (wd in (8, 16) or wd % 32 == 0) and wd <= WINOGRAD_MAX_W and h % 4 == 0 and cin % 4 == 0 and
+            cout % 4 == 0 and min(cin, cout) >= WINOGRAD_MIN_C)
 
 
 WINOGRAD_WGRAD = os.environ.get("MVAE_NO_WINOGRAD_WGRAD") is None
@@ -242,15 +258,17 @@ def _wino_wgrad_ok(g, x, dy, dw, dys) -> bool:
 
 def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split: bool, dgrad: bool, st):
     """U (filters), V (input tiles) and the 16 position GEMMs M = V U^T; returns M (arena) for an output transform."""
-    t = n * (h // 2) * (wd // 2)
+    mt = WINOGRAD_TILE
+    t = n * (h // mt) * (wd // mt)
+    pos = (mt + 2) ** 2
     dev = src.device
-    u = ARENA.get("wino_u", 64 * k_in * n_out, dev)
-    v = ARENA.get("wino_v", 64 * t * k_in, dev)
-    m = ARENA.get("wino_m", 64 * t * n_out, dev)
+    u = ARENA.get("wino_u", 4 * pos * k_in * n_out, dev)
+    v = ARENA.get("wino_v", 4 * pos * t * k_in, dev)
+    m = ARENA.get("wino_m", 4 * pos * t * n_out, dev)
     cin, cout = (n_out, k_in) if dgrad else (k_in, n_out)
-    _lib.call("mvae_winograd_weight_transform", w.data_ptr(), u.data_ptr(), cin, cout, int(dgrad), st)
-    _lib.call("mvae_winograd_input_transform", src.data_ptr(), v.data_ptr(), n, h, wd, k_in, int(src_split), st)
-    _lib.call("mvae_winograd_gemm", v.data_ptr(), u.data_ptr(), m.data_ptr(), t, k_in, n_out, st)
+    _lib.call("mvae_winograd_weight_transform", w.data_ptr(), u.data_ptr(), cin, cout, int(dgrad), mt, st)
+    _lib.call("mvae_winograd_input_transform", src.data_ptr(), v.data_ptr(), n, h, wd, k_in, int(src_split), mt, st)
+    _lib.call("mvae_winograd_gemm", v.data_ptr(), u.data_ptr(), m.data_ptr(), t, k_in, n_out, mt, st)
     return m
 
 
@@ -556,10 +574,10 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
     if x_bf16:
         raise RuntimeError("conv2d: a packed bf16 input needs the bf16-mixed LDS-DMA conv path")
     if _wino_ok(g, h, wd, c, co) and _al16(x, w) and (b is None or _al16(b)) and (res is None or _al16(res)):
-        with _timed("conv_fwd", ref * 4 / 9, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
+        with _timed("conv_fwd", _wino_alg(ref), (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
             m = _winograd(x, w, n, h, wd, c, co, x_split, False, st)
             _lib.call("mvae_winograd_output_transform", m.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), _ptr(gn_part),
-                      n, h, wd, co, st)
+                      n, h, wd, co, WINOGRAD_TILE, st)
         return y
     wg = w
     if sub:  # tap-summed per-class weights (prepared outside the timed GEMM launch)
@@ -668,15 +686,15 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
         # the input gradient is the 3x3 / pad-1 conv of dy with the flipped, transposed filters
         link = gn_link if gn_link is not None and gn_link.usable(dx) else None
         part = torch.empty(n * h * wd // 32 * c * 2, device=dy.device, dtype=torch.float64) if link else None
-        with _timed("conv_dgrad", flops * 4 / 9, shp, flops):
+        with _timed("conv_dgrad", _wino_alg(flops), shp, flops):
             m = _winograd(dya, w, n, h, wd, co, c, dys is not None, True, st)
             if link is None:
                 _lib.call("mvae_winograd_output_transform", m.data_ptr(), None, None, dx.data_ptr(), None, n, h, wd, c,
-                          st)
+                          WINOGRAD_TILE, st)
             else:  # with the GroupNorm backward partials (mvae_conv2d_dgrad_gnbwd_nhwc's epilogue sums)
                 _lib.call("mvae_winograd_output_gnbwd", m.data_ptr(), dx.data_ptr(), link.x.data_ptr(),
                           link.mean.data_ptr(), link.rstd.data_ptr(), link.gamma.data_ptr(), link.beta.data_ptr(),
-                          link.groups, link.silu, part.data_ptr(), n, h, wd, c, st)
+                          link.groups, link.silu, part.data_ptr(), n, h, wd, c, WINOGRAD_TILE, st)
                 link.part, link.dx = part, dx
         return dx
     if gn_link is not None and gn_link.usable(dx) and not g.pointwise and not g.upsample and g.stride == 1 and \
@@ -765,7 +783,9 @@ def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool
     co = dy.shape[1]
     _, _, ho, wo = dy.shape
     ref = 2.0 * n * ho * wo * co * c * g.kh * g.kw
-    alg = ref * 4 / 9 if _subpixel_upsample(g) or (dyb is None and _wino_wgrad_ok(g, x, dy, dw, dys)) else ref
+    alg = ref * 4 / 9 if _subpixel_upsample(g) else ref
+    if dyb is None and _wino_wgrad_ok(g, x, dy, dw, dys):
+        alg = _wino_alg(ref)
     if dyb is not None and not x_split and not g.upsample and c % 8 == 0 and co % 8 == 0 and _al16(x):
         # bf16-mixed weight gradient on packed bf16 dy and x (LDS-DMA main loop); the bias gradient is summed from the
         # fp32 dy by the caller
@@ -823,19 +843,22 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
     if _wino_wgrad_ok(g, x, dy, dw, dys):
         # Winograd F(3x3, 2x2): dW = G^T [sum_tiles (A D A^T) (.) (B^T X B)] G (csrc/winograd.hip); the bias gradient is
         # left to the caller
-        t = n * (h // 2) * (wd // 2)
+        mt = WINOGRAD_TILE
+        t = n * (h // mt) * (wd // mt)
+        pos = (mt + 2) ** 2
         dev = dy.device
-        dt = ARENA.get("wino_d", 64 * t * co, dev)
-        v = ARENA.get("wino_v", 64 * t * c, dev)
-        m = ARENA.get("wino_mw", 64 * co * c, dev)
-        nbytes = _lib.query("mvae_gemm_workspace_bytes", co, c, t, 16)
+        dt = ARENA.get("wino_d", 4 * pos * t * co, dev)
+        v = ARENA.get("wino_v", 4 * pos * t * c, dev)
+        m = ARENA.get("wino_mw", 4 * pos * co * c, dev)
+        nbytes = _lib.query("mvae_gemm_workspace_bytes", co, c, t, pos)
         ws = ARENA.get("ws", nbytes, dev)
         dya = dys if dys is not None else dy
-        _lib.call("mvae_winograd_dy_transform", dya.data_ptr(), dt.data_ptr(), n, h, wd, co, int(dys is not None), st)
-        _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), n, h, wd, c, int(x_split), st)
-        _lib.call("mvae_winograd_wgrad_gemm", dt.data_ptr(), v.data_ptr(), m.data_ptr(), t, co, c, ws.data_ptr(),
+        _lib.call("mvae_winograd_dy_transform", dya.data_ptr(), dt.data_ptr(), n, h, wd, co, int(dys is not None), mt,
+                  st)
+        _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), n, h, wd, c, int(x_split), mt, st)
+        _lib.call("mvae_winograd_wgrad_gemm", dt.data_ptr(), v.data_ptr(), m.data_ptr(), t, co, c, mt, ws.data_ptr(),
                   ws.numel(), st)
-        _lib.call("mvae_winograd_wgrad_output", m.data_ptr(), dw.data_ptr(), float(beta), co, c, st)
+        _lib.call("mvae_winograd_wgrad_output", m.data_ptr(), dw.data_ptr(), float(beta), co, c, mt, st)
         return False
     nbytes = _lib.query("mvae_conv2d_wgrad_workspace_bytes", n, c, co, g.kh, g.kw, ho, wo)
     ws = ARENA.get("ws", nbytes, dy.device)
