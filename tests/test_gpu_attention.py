@@ -127,9 +127,10 @@ def _run_tile(dev, q, k, v, go, prec, tile):
 
 @pytest.mark.parametrize("prec", sorted(TOL))
 @pytest.mark.parametrize("shape", TILE_SHAPES, ids=lambda s: "x".join(map(str, s)))
-def test_tile_attention_matches_float64(dev, shape, prec):
+def test_tile_attention_matches_float64(dev, shape, prec, monkeypatch):
     from medvae_disentangled_multimodal_amd import ops
     b, c, h, w = shape
+    monkeypatch.setattr(ops, "ATTN_TILE", True)  # (opt-in path: eligibility with the switch on)
     assert ops._attn_use_tile(torch.empty((b, 16), device=dev), h * w, c)
     g = torch.Generator().manual_seed(c + h * w + 1)
     q, k, v = (torch.randn(shape, generator=g) for _ in range(3))
