@@ -256,14 +256,25 @@ def _wino_wgrad_ok(g, x, dy, dw, dys) -> bool:
             dy.is_contiguous(memory_format=CL) and dw.is_contiguous(memory_format=CL))
 
 
-def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split: bool, dgrad: bool, st):
-    """U (filters), V (input tiles) and the 16 position GEMMs M = V U^T; returns M (arena) for an output transform."""
+# the forward's Winograd input transform V is kept for the weight gradient (which needs the same V of the same x)
+# instead of being recomputed there: one input transform per conv and step less, at (m+2)^2/m^2 x the input's bytes
+# of memory held from forward to backward (c4 ≈ 27 GB). MVAE_NO_WINOGRAD_KEEP_V=1 recomputes it.
+WINOGRAD_KEEP_V = os.environ.get("MVAE_NO_WINOGRAD_KEEP_V") is None
+
+
+def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split: bool, dgrad: bool, st, keep=None):
+    """U (filters), V (input tiles) and the (m+2)^2 position GEMMs M = V U^T; returns M (arena) for an output
+    transform. keep (a list): V is allocated outside the arena and appended to it (WINOGRAD_KEEP_V)."""
     mt = WINOGRAD_TILE
     t = n * (h // mt) * (wd // mt)
     pos = (mt + 2) ** 2
     dev = src.device
     u = ARENA.get("wino_u", 4 * pos * k_in * n_out, dev)
-    v = ARENA.get("wino_v", 4 * pos * t * k_in, dev)
+    if keep is not None:
+        v = torch.empty(4 * pos * t * k_in, dtype=torch.uint8, device=dev)
+        keep.append((v, mt, src.data_ptr(), src._version))
+    else:
+        v = ARENA.get("wino_v", 4 * pos * t * k_in, dev)
     m = ARENA.get("wino_m", 4 * pos * t * n_out, dev)
     cin, cout = (n_out, k_in) if dgrad else (k_in, n_out)
     _lib.call("mvae_winograd_weight_transform", w.data_ptr(), u.data_ptr(), cin, cout, int(dgrad), mt, st)
@@ -551,7 +562,8 @@ def _conv_call(x, w, b, res, y, n, h, wd, c, co, kh, kw, stride, pad_t, pad_l, h
                   mode, st)
 
 
-def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part=None, x_bf16: bool = False):
+def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part=None, x_bf16: bool = False,
+                       keep_v=None):
     """gn_part (fp64 [n*ho*wo/32 * cout/4 * 2]): also emit the GroupNorm statistics of y from the GEMM
     epilogue (mvae_conv2d_gnstats_nhwc; only on the plain implicit-GEMM path -- the caller checks).
     x_bf16: x holds packed bf16 (BF16_ATTR; bf16-mixed mode)."""
@@ -575,7 +587,7 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
         raise RuntimeError("conv2d: a packed bf16 input needs the bf16-mixed LDS-DMA conv path")
     if _wino_ok(g, h, wd, c, co) and _al16(x, w) and (b is None or _al16(b)) and (res is None or _al16(res)):
         with _timed("conv_fwd", _wino_alg(ref), (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
-            m = _winograd(x, w, n, h, wd, c, co, x_split, False, st)
+            m = _winograd(x, w, n, h, wd, c, co, x_split, False, st, keep_v)
             _lib.call("mvae_winograd_output_transform", m.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), _ptr(gn_part),
                       n, h, wd, co, WINOGRAD_TILE, st)
         return y
@@ -775,7 +787,7 @@ def _conv_dgrad_bf16(dyb, w, dx, g, n, c, h, wd, co, ho, wo, flops, shp, st):
 
 
 def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool = False, dys=None, dyb=None,
-                     x_bf16: bool = False):
+                     x_bf16: bool = False, wino_v=None):
     """dw (+ db when given and the conv is not pointwise) accumulate with `beta`. Returns True when
     the bias gradient was produced by the fused wgrad kernel. dys: dy pre-split by split_dy; dyb: dy as packed bf16
     (pack_dy, bf16-mixed mode)."""
@@ -801,10 +813,10 @@ def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool
     if x_bf16:
         raise RuntimeError("conv2d wgrad: a packed bf16 input needs the bf16-mixed LDS-DMA path (packed dy, cout % 8)")
     with _timed("conv_wgrad", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
-        return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db, x_split, dys)
+        return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db, x_split, dys, wino_v)
 
 
-def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_split=False, dys=None):
+def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_split=False, dys=None, wino_v=None):
     st = _stream(dy)
     if x_split and (g.pointwise or g.upsample):
         raise RuntimeError("conv2d wgrad: a pre-split input needs a non-pointwise, non-upsample conv")
@@ -848,14 +860,17 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         pos = (mt + 2) ** 2
         dev = dy.device
         dt = ARENA.get("wino_d", 4 * pos * t * co, dev)
-        v = ARENA.get("wino_v", 4 * pos * t * c, dev)
+        # the forward's V of this x when it was kept (same tile size, x unchanged since), else recomputed
+        kept = wino_v is not None and wino_v[1] == mt and wino_v[2] == x.data_ptr() and wino_v[3] == x._version
+        v = wino_v[0] if kept else ARENA.get("wino_v", 4 * pos * t * c, dev)
         m = ARENA.get("wino_mw", 4 * pos * co * c, dev)
         nbytes = _lib.query("mvae_gemm_workspace_bytes", co, c, t, pos)
         ws = ARENA.get("ws", nbytes, dev)
         dya = dys if dys is not None else dy
         _lib.call("mvae_winograd_dy_transform", dya.data_ptr(), dt.data_ptr(), n, h, wd, co, int(dys is not None), mt,
                   st)
-        _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), n, h, wd, c, int(x_split), mt, st)
+        if not kept:
+            _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), n, h, wd, c, int(x_split), mt, st)
         _lib.call("mvae_winograd_wgrad_gemm", dt.data_ptr(), v.data_ptr(), m.data_ptr(), t, co, c, mt, ws.data_ptr(),
                   ws.numel(), st)
         _lib.call("mvae_winograd_wgrad_output", m.data_ptr(), dw.data_ptr(), float(beta), co, c, mt, st)
@@ -987,7 +1002,9 @@ class Conv2dFn(torch.autograd.Function):
         x = nhwc(x)
         w = _krsc(weight)
         res = nhwc(residual) if residual is not None else None
-        y = conv2d_forward_raw(x, w, bias, res, geom, xs, gn_part, x_bf16=xb16)
+        keep = [] if WINOGRAD_KEEP_V and weight.requires_grad else None
+        y = conv2d_forward_raw(x, w, bias, res, geom, xs, gn_part, x_bf16=xb16, keep_v=keep)
+        ctx.wino_v = keep[0] if keep else None
         ctx.math = _MATH[0]  # the backward GEMMs run in the forward's arithmetic
         ctx.geom = geom
         ctx.x_split = xs
@@ -1057,13 +1074,15 @@ class Conv2dFn(torch.autograd.Function):
             want_b_w = want_b and not bias_done
             xs, xb16 = ctx.x_split, ctx.x_bf16
             if tgt is not None and (not want_b_w or btgt is not None):
-                fused = conv2d_wgrad_raw(dy, x, tgt, 1.0, g, btgt, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16)
+                fused = conv2d_wgrad_raw(dy, x, tgt, 1.0, g, btgt, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16,
+                                         wino_v=ctx.wino_v)
                 bias_done = bias_done or fused
             elif tgt is not None:
-                conv2d_wgrad_raw(dy, x, tgt, 1.0, g, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16)
+                conv2d_wgrad_raw(dy, x, tgt, 1.0, g, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16, wino_v=ctx.wino_v)
             else:
                 dw_ret = torch.empty_like(w, memory_format=CL)
-                conv2d_wgrad_raw(dy, x, dw_ret, 0.0, g, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16)
+                conv2d_wgrad_raw(dy, x, dw_ret, 0.0, g, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16,
+                                 wino_v=ctx.wino_v)
 
         side = _bwd_side(dy) if ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and \
             _main_grad(ctx.weight_ref) is not None and _overlap_ok(x, dy, g) else None
@@ -1085,6 +1104,7 @@ class Conv2dFn(torch.autograd.Function):
             main.wait_event(ev_join)
         elif ctx.needs_input_grad[1]:
             wgrad()
+        ctx.wino_v = None  # (released after the join: a later main-stream allocation is ordered after its last use)
         if ctx.has_bias and ctx.needs_input_grad[2] and not bias_done:
             tgt = _main_grad(ctx.bias_ref)
             n, co, ho, wo = dy.shape

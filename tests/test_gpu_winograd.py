@@ -193,3 +193,39 @@ def test_winograd_rejects_unsupported_geometry(dev):
     v = torch.zeros(16 * 36 * 64, device=dev)
     with pytest.raises(RuntimeError):
         _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), 1, 12, 12, 64, 0, 4, 0)
+
+
+def test_winograd_kept_input_transform_feeds_weight_gradient(dev, monkeypatch):
+    """The forward's V is kept for the weight gradient (WINOGRAD_KEEP_V): one input transform fewer per step, dW bitwise
+    equal to the recomputing path."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    n, c, h, w = 2, 128, 16, 16
+    g = torch.Generator().manual_seed(9)
+    x0 = torch.randn(n, c, h, w, generator=g)
+    w0 = torch.randn(c, c, 3, 3, generator=g) / (3 * c ** 0.5)
+    dy0 = torch.randn(n, c, h, w, generator=g)
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
+
+    def run(keep):
+        monkeypatch.setattr(ops, "WINOGRAD_KEEP_V", keep)
+        seen = []
+        orig = _lib.call
+
+        def spy(name, *args):
+            seen.append(name)
+            return orig(name, *args)
+        x = cl(x0, dev).requires_grad_(True)
+        wt = w0.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        y = ops.conv2d(x, wt, None, geom)
+        monkeypatch.setattr(_lib, "call", spy)
+        try:
+            y.backward(cl(dy0, dev))
+        finally:
+            monkeypatch.setattr(_lib, "call", orig)
+        torch.cuda.synchronize()
+        return x.grad.cpu(), wt.grad.cpu(), seen.count("mvae_winograd_input_transform")
+
+    dxk, dwk, nk = run(True)
+    dxr, dwr, nr = run(False)
+    assert (nk, nr) == (1, 2)  # backward: dy's transform only, vs dy's and x's
+    assert torch.equal(dwk, dwr) and torch.equal(dxk, dxr)
