@@ -118,7 +118,7 @@ template <int MT, bool XS>
 __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ x, uint4* __restrict__ v, int nb, int H,
                                                       int W, int C) {
   constexpr int AL = MT + 2;
-  const int C4 = C >> 2, th = H / MT, tw = W / MT;
+  const int C4 = C >> 2, th = (H + MT - 1) / MT, tw = (W + MT - 1) / MT;  // (edge tiles zero-filled)
   const long long T = (long long)nb * th * tw;
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= T * C4) return;
@@ -349,13 +349,53 @@ __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
   }
 }
 
+// M -> y = A^T M A (+ bias) (+ residual) for any H, W (edge tiles cut at the image border): one thread per (tile,
+// 4-channel group), no statistics (the GroupNorm after such a conv computes its own)
+template <int MT>
+__global__ void __launch_bounds__(256) wino_out_any_kernel(WinoOut p) {
+  constexpr int AL = MT + 2;
+  const int N = p.N, N4 = N >> 2, th = (p.H + MT - 1) / MT, tw = (p.W + MT - 1) / MT;
+  const long long T = (long long)p.nb * th * tw;
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= T * N4) return;
+  const long long t = idx / N4;
+  const int c4 = (int)(idx - t * N4);
+  const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
+  const float4 bv = p.bias ? *(const float4*)(p.bias + c4 * 4) : float4{0.f, 0.f, 0.f, 0.f};
+  float4 mv[AL][AL];
+#pragma unroll
+  for (int i = 0; i < AL; ++i)
+#pragma unroll
+    for (int j = 0; j < AL; ++j) mv[i][j] = *(const float4*)(p.m + ((long long)(i * AL + j) * T + t) * N + c4 * 4);
+  constexpr auto at = [](int i, int k) { return wino_at<MT>(i, k); };
+  float4 r[MT][AL];
+#pragma unroll
+  for (int j = 0; j < AL; ++j) wlin<MT, AL>(&r[0][j], AL, &mv[0][j], AL, at);
+#pragma unroll
+  for (int a = 0; a < MT; ++a) {
+    float4 o[MT];
+    wlin<MT, AL>(o, 1, &r[a][0], 1, at);
+    const int row = ti * MT + a;
+#pragma unroll
+    for (int e = 0; e < MT; ++e) {
+      const int col = tj * MT + e;
+      if (row < p.H && col < p.W) {
+        const long long off = (((long long)b * p.H + row) * p.W + col) * N + c4 * 4;
+        float4 val = f4add(o[e], bv);
+        if (p.res) val = f4add(val, *(const float4*)(p.res + off));
+        *(float4*)(p.y + off) = val;
+      }
+    }
+  }
+}
+
 // dy [nb][H][W][K] (fp32, or split4_bf16 groups when XS) -> D' = A D A^T [a^2][T][K] split4_bf16: one thread per
 // (tile, 4-group)
 template <int MT, bool XS>
 __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ dy, uint4* __restrict__ d, int nb, int H,
                                                       int W, int K) {
   constexpr int AL = MT + 2;
-  const int K4 = K >> 2, th = H / MT, tw = W / MT;
+  const int K4 = K >> 2, th = (H + MT - 1) / MT, tw = (W + MT - 1) / MT;
   const long long T = (long long)nb * th * tw;
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= T * K4) return;
@@ -367,8 +407,13 @@ __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ 
   for (int a = 0; a < MT; ++a)
 #pragma unroll
     for (int e = 0; e < MT; ++e) {
-      const float4 r = *(const float4*)(dy + (((long long)b * H + MT * ti + a) * W + MT * tj + e) * K + k4 * 4);
-      v[a][e] = XS ? split4_to_f32(r) : r;
+      const int h = MT * ti + a, w = MT * tj + e;
+      float4 val{0.f, 0.f, 0.f, 0.f};  // (pixels past the image edge carry no gradient)
+      if (h < H && w < W) {
+        const float4 r = *(const float4*)(dy + (((long long)b * H + h) * W + w) * K + k4 * 4);
+        val = XS ? split4_to_f32(r) : r;
+      }
+      v[a][e] = val;
     }
   constexpr auto ac = [](int i, int k) { return wino_at<MT>(k, i); };  // A = (A^T)^T
   float4 c[AL][MT], o[AL][AL];
@@ -418,17 +463,20 @@ __global__ void __launch_bounds__(256) wino_wout_kernel(const float* __restrict_
     }
 }
 
-static long long wino_tiles(int nb, int h, int w, int mt) { return (long long)nb * (h / mt) * (w / mt); }
-
-static bool wino_geom_ok(int mt, int nb, int h, int w, int cin, int cout) {
-  // (the output transform's thread groups are whole 32-pixel blocks of the statistics layouts: h % 4 == 0 covers
-  // every (m, w) pair: m = 2 at w = 8 takes 2 tile rows per group)
-  const long long pos = (long long)(mt + 2) * (mt + 2);
-  return (mt == 2 || mt == 4) && nb > 0 && h >= 4 && h % 4 == 0 && (w == 8 || w == 16 || (w >= 32 && w % 32 == 0)) &&
-         cin > 0 && cout > 0 && cin % 4 == 0 && cout % 4 == 0 &&
-         (long long)nb * h * w * std::max(cin, cout) * 4 <= MAX_DESC_BYTES &&
-         wino_tiles(nb, h, w, mt) * std::max(cin, cout) * 4 <= MAX_DESC_BYTES && pos > 0;
+static long long wino_tiles(int nb, int h, int w, int mt) {
+  return (long long)nb * ((h + mt - 1) / mt) * ((w + mt - 1) / mt);
 }
+
+// any image size (edge tiles zero-filled / cut), channel counts % 4, every operand < 4 GiB
+static bool wino_geom_ok(int mt, int nb, int h, int w, int cin, int cout) {
+  return (mt == 2 || mt == 4) && nb > 0 && h > 0 && w > 0 && cin > 0 && cout > 0 && cin % 4 == 0 && cout % 4 == 0 &&
+         (long long)nb * h * w * std::max(cin, cout) * 4 <= MAX_DESC_BYTES &&
+         wino_tiles(nb, h, w, mt) * std::max(cin, cout) * 4 <= MAX_DESC_BYTES;
+}
+
+// the blocked output transform (statistics in the 32-pixel-block layouts): whole tiles, and thread groups that are
+// whole 32-pixel blocks -- h % 4 == 0 covers every (m, w) pair (m = 2 at w = 8 takes 2 tile rows per group)
+static bool wino_blocks_ok(int h, int w) { return h % 4 == 0 && (w == 8 || w == 16 || (w >= 32 && w % 32 == 0)); }
 
 static int egrid256(long long n) { return (int)std::min<long long>((n + 255) / 256, 1LL << 30); }
 
@@ -449,6 +497,12 @@ static void wino_out_go(WinoOut& p, bool gnb, hipStream_t st) {
 
 static int wino_out_launch(WinoOut& p, int tile, bool gnb, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (!wino_blocks_ok(p.H, p.W)) {  // (callers reject statistics here)
+    const dim3 g(egrid256(wino_tiles(p.nb, p.H, p.W, tile) * (p.N / 4)));
+    if (tile == 2) hipLaunchKernelGGL(wino_out_any_kernel<2>, g, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL(wino_out_any_kernel<4>, g, dim3(256), 0, st, p);
+    return launch_status();
+  }
   const int wseg = std::min(p.W, 32);
   if (tile == 2) {
     if (wseg == 8) wino_out_go<2, 8>(p, gnb, st);
@@ -496,8 +550,7 @@ int mvae_winograd_weight_transform(const float* w, void* u, int cin, int cout, i
 int mvae_winograd_input_transform(const float* x, void* v, int nb, int h, int w, int c, int x_split, int tile,
                                   void* stream) {
   if (!x || !v || !wino_geom_ok(tile, nb, h, w, c, c) || !al16(x) || !al16(v)) {
-    set_error("winograd_input_transform: tile 2 or 4, h %% 4 == 0, w in {8, 16} or a multiple of 32, c %% 4 == 0, "
-              "16-B aligned");
+    set_error("winograd_input_transform: tile 2 or 4, c %% 4 == 0, 16-B aligned");
     return MVAE_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;
@@ -542,9 +595,9 @@ int mvae_winograd_gemm(const void* v, const void* u, float* m, long long tiles, 
 int mvae_winograd_output_transform(const float* m, const float* bias, const float* residual, float* y, double* gn_part,
                                    int nb, int h, int w, int n, int tile, void* stream) {
   if (!m || !y || !wino_geom_ok(tile, nb, h, w, n, n) || !al16(m) || !al16(y) || (bias && !al16(bias)) ||
-      (residual && !al16(residual))) {
-    set_error("winograd_output_transform: tile 2 or 4, h %% 4 == 0, w in {8, 16} or a multiple of 32, n %% 4 == 0, "
-              "16-B aligned");
+      (residual && !al16(residual)) || (gn_part && !wino_blocks_ok(h, w))) {
+    set_error("winograd_output_transform: tile 2 or 4, n %% 4 == 0, 16-B aligned; statistics need h %% 4 == 0 and w in "
+              "{8, 16} or a multiple of 32");
     return MVAE_EINVAL;
   }
   WinoOut p{};
@@ -561,7 +614,8 @@ int mvae_winograd_output_gnbwd(const float* m, float* dx, const float* x, const 
                                const float* gamma, const float* beta, int groups, int silu, double* part, int nb, int h,
                                int w, int n, int tile, void* stream) {
   if (!m || !dx || !x || !mean || !rstd || !gamma || !beta || !part || groups <= 0 || n % groups ||
-      (n / groups) % 4 || !wino_geom_ok(tile, nb, h, w, n, n) || !al16(m) || !al16(dx) || !al16(x)) {
+      (n / groups) % 4 || !wino_geom_ok(tile, nb, h, w, n, n) || !wino_blocks_ok(h, w) || !al16(m) || !al16(dx) ||
+      !al16(x)) {
     set_error("winograd_output_gnbwd: tile 2 or 4, h %% 4 == 0, w in {8, 16} or a multiple of 32, channels per "
               "group %% 4 == 0, 16-B aligned");
     return MVAE_EINVAL;
@@ -576,8 +630,7 @@ int mvae_winograd_output_gnbwd(const float* m, float* dx, const float* x, const 
 int mvae_winograd_dy_transform(const float* dy, void* d, int nb, int h, int w, int k, int dy_split, int tile,
                                void* stream) {
   if (!dy || !d || !wino_geom_ok(tile, nb, h, w, k, k) || !al16(dy) || !al16(d)) {
-    set_error("winograd_dy_transform: tile 2 or 4, h %% 4 == 0, w in {8, 16} or a multiple of 32, k %% 4 == 0, "
-              "16-B aligned");
+    set_error("winograd_dy_transform: tile 2 or 4, k %% 4 == 0, 16-B aligned");
     return MVAE_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;

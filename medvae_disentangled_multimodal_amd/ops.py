@@ -240,10 +240,21 @@ WINOGRAD_MAX_W = int(os.environ.get("MVAE_WINOGRAD_MAX_W", "32"))
 
 
 def _wino_ok(g, h: int, wd: int, cin: int, cout: int) -> bool:
+    """Any image size (edge tiles are zero-filled / cut: c2's 7x7 level in 2x2 tiles of 4x4); the fused GroupNorm
+    statistics / partials additionally need _wino_blocks."""
     return (WINOGRAD and _MATH[0] == 0 and _dma_fmt() == 0 and g.kh == 3 and g.kw == 3 and g.stride == 1 and
-            not g.upsample and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and
-            (wd in (8, 16) or wd % 32 == 0) and wd <= WINOGRAD_MAX_W and h % 4 == 0 and cin % 4 == 0 and
-            cout % 4 == 0 and min(cin, cout) >= WINOGRAD_MIN_C)
+            not g.upsample and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and wd <= WINOGRAD_MAX_W and
+            cin % 4 == 0 and cout % 4 == 0 and min(cin, cout) >= WINOGRAD_MIN_C)
+
+
+def _wino_blocks(h: int, wd: int) -> bool:
+    """The output transform's 32-pixel-block form (GroupNorm statistics / backward partials from it)."""
+    return h % 4 == 0 and (wd in (8, 16) or wd % 32 == 0)
+
+
+def _wino_tiles(n: int, h: int, wd: int) -> int:
+    mt = WINOGRAD_TILE
+    return n * (-(-h // mt)) * (-(-wd // mt))
 
 
 WINOGRAD_WGRAD = os.environ.get("MVAE_NO_WINOGRAD_WGRAD") is None
@@ -266,7 +277,7 @@ def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split:
     """U (filters), V (input tiles) and the (m+2)^2 position GEMMs M = V U^T; returns M (arena) for an output
     transform. keep (a list): V is allocated outside the arena and appended to it (WINOGRAD_KEEP_V)."""
     mt = WINOGRAD_TILE
-    t = n * (h // mt) * (wd // mt)
+    t = _wino_tiles(n, h, wd)
     pos = (mt + 2) ** 2
     dev = src.device
     u = ARENA.get("wino_u", 4 * pos * k_in * n_out, dev)
@@ -585,7 +596,8 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
         return _conv_fwd_bf16(x, w, b, res, g, y, n, c, h, wd, co, ho, wo, sub, alg, ref, gn_part, st, x_bf16)
     if x_bf16:
         raise RuntimeError("conv2d: a packed bf16 input needs the bf16-mixed LDS-DMA conv path")
-    if _wino_ok(g, h, wd, c, co) and _al16(x, w) and (b is None or _al16(b)) and (res is None or _al16(res)):
+    if _wino_ok(g, h, wd, c, co) and _al16(x, w) and (b is None or _al16(b)) and (res is None or _al16(res)) and \
+            (gn_part is None or _wino_blocks(h, wd)):
         with _timed("conv_fwd", _wino_alg(ref), (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
             m = _winograd(x, w, n, h, wd, c, co, x_split, False, st, keep_v)
             _lib.call("mvae_winograd_output_transform", m.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), _ptr(gn_part),
@@ -696,7 +708,7 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
     dya = dy if dys is None else dys
     if _wino_ok(g, h, wd, co, c) and _al16(dya, w) and dy.is_contiguous(memory_format=CL):
         # the input gradient is the 3x3 / pad-1 conv of dy with the flipped, transposed filters
-        link = gn_link if gn_link is not None and gn_link.usable(dx) else None
+        link = gn_link if gn_link is not None and gn_link.usable(dx) and _wino_blocks(h, wd) else None
         part = torch.empty(n * h * wd // 32 * c * 2, device=dy.device, dtype=torch.float64) if link else None
         with _timed("conv_dgrad", _wino_alg(flops), shp, flops):
             m = _winograd(dya, w, n, h, wd, co, c, dys is not None, True, st)
@@ -856,7 +868,7 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         # Winograd F(3x3, 2x2): dW = G^T [sum_tiles (A D A^T) (.) (B^T X B)] G (csrc/winograd.hip); the bias gradient is
         # left to the caller
         mt = WINOGRAD_TILE
-        t = n * (h // mt) * (wd // mt)
+        t = _wino_tiles(n, h, wd)
         pos = (mt + 2) ** 2
         dev = dy.device
         dt = ARENA.get("wino_d", 4 * pos * t * co, dev)

@@ -22,6 +22,8 @@ CASES = [
     (4, 512, 512, 8, 8),   # c4-like channel count, 256-wide GEMM tiles
     (2, 64, 32, 8, 32),    # W = 32: per-segment output groups
     (1, 32, 64, 12, 64),   # W = 64: two 32-pixel segments per row
+    (3, 64, 64, 7, 7),     # c2's 7x7 level: edge tiles cut (no fused statistics)
+    (2, 32, 48, 14, 10),   # ragged both ways
 ]
 
 
@@ -69,8 +71,8 @@ def _wino_on(monkeypatch, request):
 
 @pytest.mark.parametrize("n,ci,co,h,w", CASES)
 @pytest.mark.parametrize("x_split", [False, True])
-def test_winograd_forward(dev, n, ci, co, h, w, x_split):
-    from medvae_disentangled_multimodal_amd import ops
+def test_winograd_forward(dev, n, ci, co, h, w, x_split, monkeypatch):
+    from medvae_disentangled_multimodal_amd import _lib, ops
     g = torch.Generator().manual_seed(n * ci + co + h * w)
     x = torch.randn(n, ci, h, w, generator=g)
     wt = torch.randn(co, ci, 3, 3, generator=g) / (3 * ci ** 0.5)
@@ -81,13 +83,24 @@ def test_winograd_forward(dev, n, ci, co, h, w, x_split):
     xd = cl(x, dev)
     if x_split:
         xd = _split(xd)
-    part = torch.empty(n * h * w // 32 * (co // 4) * 2, device=dev, dtype=torch.float64)
+    blocks = ops._wino_blocks(h, w)
+    part = torch.empty(n * h * w // 32 * (co // 4) * 2, device=dev, dtype=torch.float64) if blocks else None
+    seen = []
+    orig = _lib.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return orig(name, *args)
+    monkeypatch.setattr(_lib, "call", spy)
     y = ops.conv2d_forward_raw(xd, cl(wt, dev), b.to(dev), cl(r, dev), geom, x_split=x_split, gn_part=part)
+    monkeypatch.setattr(_lib, "call", orig)
     torch.cuda.synchronize()
+    assert "mvae_winograd_output_transform" in seen
     ref = torch.nn.functional.conv2d(x.double(), wt.double(), b.double(), padding=1) + r.double()
     assert rel(y, ref) < CONV_TOL
-    assert rel(part, _stats64(y.double().cpu())) < 1e-9  # the statistics are of the stored y
-    assert rel(part, _stats64(ref)) < CONV_TOL
+    if blocks:
+        assert rel(part, _stats64(y.double().cpu())) < 1e-9  # the statistics are of the stored y
+        assert rel(part, _stats64(ref)) < CONV_TOL
 
 
 @pytest.mark.parametrize("n,ci,co,h,w", CASES)
@@ -188,11 +201,18 @@ def test_winograd_through_conv2d_matches_implicit_gemm(dev, monkeypatch):
 
 
 def test_winograd_rejects_unsupported_geometry(dev):
+    """Channel counts % 4, tile sizes 2 / 4, and fused statistics only on the 32-pixel-block geometries."""
     from medvae_disentangled_multimodal_amd import _lib
     x = torch.zeros(1, 12, 12, 64, device=dev)
     v = torch.zeros(16 * 36 * 64, device=dev)
     with pytest.raises(RuntimeError):
-        _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), 1, 12, 12, 64, 0, 4, 0)
+        _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), 1, 12, 12, 62, 0, 4, 0)
+    with pytest.raises(RuntimeError):
+        _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), 1, 12, 12, 64, 0, 3, 0)
+    part = torch.zeros(64, device=dev, dtype=torch.float64)
+    with pytest.raises(RuntimeError):  # 7x7: no 32-pixel blocks
+        _lib.call("mvae_winograd_output_transform", v.data_ptr(), None, None, x.data_ptr(), part.data_ptr(), 1, 7, 7,
+                  64, 4, 0)
 
 
 def test_winograd_kept_input_transform_feeds_weight_gradient(dev, monkeypatch):
