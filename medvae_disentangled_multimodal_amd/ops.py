@@ -239,12 +239,18 @@ def _wino_alg(ref: float) -> float:
 WINOGRAD_MAX_W = int(os.environ.get("MVAE_WINOGRAD_MAX_W", "32"))
 
 
-def _wino_ok(g, h: int, wd: int, cin: int, cout: int) -> bool:
+# smallest conv (direct MACs) it is used for: the four launches of the Winograd form lose to one implicit GEMM on small
+# batches (c1's 7x7x512 at B = 32, 3.7 GMAC: 3,607 -> 3,400 img/s; c2's at B = 256, 29.6 GMAC, gains 3.5 %)
+WINOGRAD_MIN_MACS = float(os.environ.get("MVAE_WINOGRAD_MIN_MACS", "1e10"))
+
+
+def _wino_ok(g, n: int, h: int, wd: int, cin: int, cout: int) -> bool:
     """Any image size (edge tiles are zero-filled / cut: c2's 7x7 level in 2x2 tiles of 4x4); the fused GroupNorm
     statistics / partials additionally need _wino_blocks."""
     return (WINOGRAD and _MATH[0] == 0 and _dma_fmt() == 0 and g.kh == 3 and g.kw == 3 and g.stride == 1 and
             not g.upsample and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and wd <= WINOGRAD_MAX_W and
-            cin % 4 == 0 and cout % 4 == 0 and min(cin, cout) >= WINOGRAD_MIN_C)
+            cin % 4 == 0 and cout % 4 == 0 and min(cin, cout) >= WINOGRAD_MIN_C and
+            9.0 * n * h * wd * cin * cout >= WINOGRAD_MIN_MACS)
 
 
 def _wino_blocks(h: int, wd: int) -> bool:
@@ -263,7 +269,7 @@ WINOGRAD_WGRAD = os.environ.get("MVAE_NO_WINOGRAD_WGRAD") is None
 def _wino_wgrad_ok(g, x, dy, dw, dys) -> bool:
     n, c, h, wd = x.shape
     co = dy.shape[1]
-    return (WINOGRAD_WGRAD and _wino_ok(g, h, wd, c, co) and _al16(x, dy, dw) and (dys is None or _al16(dys)) and
+    return (WINOGRAD_WGRAD and _wino_ok(g, n, h, wd, c, co) and _al16(x, dy, dw) and (dys is None or _al16(dys)) and
             dy.is_contiguous(memory_format=CL) and dw.is_contiguous(memory_format=CL))
 
 
@@ -596,7 +602,7 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
         return _conv_fwd_bf16(x, w, b, res, g, y, n, c, h, wd, co, ho, wo, sub, alg, ref, gn_part, st, x_bf16)
     if x_bf16:
         raise RuntimeError("conv2d: a packed bf16 input needs the bf16-mixed LDS-DMA conv path")
-    if _wino_ok(g, h, wd, c, co) and _al16(x, w) and (b is None or _al16(b)) and (res is None or _al16(res)) and \
+    if _wino_ok(g, n, h, wd, c, co) and _al16(x, w) and (b is None or _al16(b)) and (res is None or _al16(res)) and \
             (gn_part is None or _wino_blocks(h, wd)):
         with _timed("conv_fwd", _wino_alg(ref), (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
             m = _winograd(x, w, n, h, wd, c, co, x_split, False, st, keep_v)
@@ -706,7 +712,7 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
     if dys is not None and (g.pointwise or co % 4):
         dys = None
     dya = dy if dys is None else dys
-    if _wino_ok(g, h, wd, co, c) and _al16(dya, w) and dy.is_contiguous(memory_format=CL):
+    if _wino_ok(g, n, h, wd, co, c) and _al16(dya, w) and dy.is_contiguous(memory_format=CL):
         # the input gradient is the 3x3 / pad-1 conv of dy with the flipped, transposed filters
         link = gn_link if gn_link is not None and gn_link.usable(dx) and _wino_blocks(h, wd) else None
         part = torch.empty(n * h * wd // 32 * c * 2, device=dy.device, dtype=torch.float64) if link else None

@@ -634,7 +634,8 @@ def test_groupnorm_backward_partials_from_conv_dgrad(dev, n, c, co, h, silu, win
     Winograd F(4x4, 3x3) form, whose output transform emits the partials instead of the GEMM epilogue)."""
     from medvae_disentangled_multimodal_amd import ops
     monkeypatch.setattr(ops, "WINOGRAD", wino)
-    wino_used = wino and ops._wino_ok(ops.ConvGeom(3, 3, 1, 1, 1, 1, 1), h, h, co, c)
+    monkeypatch.setattr(ops, "WINOGRAD_MIN_MACS", 0.0)
+    wino_used = wino and ops._wino_ok(ops.ConvGeom(3, 3, 1, 1, 1, 1, 1), n, h, h, co, c)
     if wino and not wino_used:
         pytest.skip("not a Winograd geometry")
     producer = "mvae_winograd_output_gnbwd" if wino_used else "mvae_conv2d_dgrad_gnbwd_nhwc"

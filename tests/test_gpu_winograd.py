@@ -66,6 +66,7 @@ def _wino_on(monkeypatch, request):
     monkeypatch.setattr(ops, "WINOGRAD_MIN_C", 1)
     monkeypatch.setattr(ops, "WINOGRAD_TILE", request.param)
     monkeypatch.setattr(ops, "WINOGRAD_MAX_W", 64)
+    monkeypatch.setattr(ops, "WINOGRAD_MIN_MACS", 0.0)
     return request.param
 
 
@@ -79,7 +80,7 @@ def test_winograd_forward(dev, n, ci, co, h, w, x_split, monkeypatch):
     b = torch.randn(co, generator=g)
     r = torch.randn(n, co, h, w, generator=g)
     geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
-    assert ops._wino_ok(geom, h, w, ci, co)
+    assert ops._wino_ok(geom, n, h, w, ci, co)
     xd = cl(x, dev)
     if x_split:
         xd = _split(xd)
