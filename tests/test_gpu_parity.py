@@ -41,6 +41,29 @@ def _batch(case, data, dev):
 def test_training_step_matches_reference(name):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    _check_step(name)
+
+
+@pytest.mark.parametrize("name", ["cvae_c4_full", "beta_c2_full"])
+def test_training_step_winograd_matches_reference(name, monkeypatch):
+    """The same step with the Winograd F(4x4, 3x3) convs the bench runs at B = 256 forced on at the golden B = 2 (the
+    size rule would keep the implicit GEMM there): c4's 8x8 / 16x16 / 32x32 levels, c2's 7x7 level."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    monkeypatch.setattr(ops, "WINOGRAD_MIN_MACS", 0.0)
+    seen = set()
+    orig = _lib.call
+
+    def spy(fn, *args):
+        seen.add(fn)
+        return orig(fn, *args)
+    monkeypatch.setattr(_lib, "call", spy)
+    _check_step(name)
+    assert {"mvae_winograd_gemm", "mvae_winograd_wgrad_gemm"} <= seen
+
+
+def _check_step(name):
     import medvae_disentangled_multimodal_amd as M
     dev = torch.device("cuda:0")
     meta, data = load_case(name)
