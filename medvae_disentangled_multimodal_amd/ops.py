@@ -192,6 +192,8 @@ STRIDE2_CLASSES = os.environ.get("MVAE_NO_STRIDE2_CLASSES") is None
 WEIGHT_SPLIT = os.environ.get("MVAE_NO_WEIGHT_SPLIT") is None
 SMALL_COUT_WGRAD = os.environ.get("MVAE_NO_SMALL_COUT_WGRAD") is None
 DIRECT_WGRAD = os.environ.get("MVAE_NO_DIRECT_WGRAD") is None
+# output channel counts the direct weight gradient serves (the kernel takes 32 and 64; MVAE_DIRECT_WGRAD_C64=1 adds 64)
+DIRECT_WGRAD_COUT = (32, 64) if os.environ.get("MVAE_DIRECT_WGRAD_C64") is not None else (32,)
 MVAE_CONV_WSPLIT = 16
 MVAE_CONV_XSPLIT = 32
 MVAE_CONV_DYSPLIT = 64
@@ -854,8 +856,8 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         _lib.call("mvae_conv2d_wgrad_small_cout_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db),
                   float(beta), n, h, wd, c, co, int(x_split), ws.data_ptr(), ws.numel(), st)
         return db is not None
-    if (DIRECT_WGRAD and dys is None and c in (32, 64) and co == 32 and _MATH[0] != 2 and not g.upsample and
-            g.kh == 3 and g.kw == 3 and g.stride == 1 and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and
+    if (DIRECT_WGRAD and dys is None and c in (32, 64) and co in DIRECT_WGRAD_COUT and _MATH[0] != 2 and
+            not g.upsample and g.kh == 3 and g.kw == 3 and g.stride == 1 and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and
             _al16(x, dy)):
         # cout 32 (c3's 28x28 / 14x14 levels): per-tap MFMA products over LDS-resident row bands; 28x28x32 at bs 512
         # 128 -> 75 us, 28x28 64->32 185 -> 118 us (tools/wgrad_bench.py); cout 64 ties the GEMM and keeps it
