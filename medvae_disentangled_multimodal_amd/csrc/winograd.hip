@@ -103,6 +103,12 @@ __device__ __forceinline__ void wlin(float4* y, int ys, const float4* x, int xs,
   for (int i = 0; i < RO; ++i) y[i * ys] = t[i];
 }
 
+// 16-B buffer store of a split4_bf16 group: plane xi of a [P][rows][16 B] array is `base + xi * plane` bytes (the
+// whole array < 4 GiB, checked by the entry points): 32-bit offset adds instead of a 64-bit multiply per store
+__device__ __forceinline__ void wstore(__amdgpu_buffer_rsrc_t r, unsigned off, uint4 u) {
+  bstore4(r, off, float4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)});
+}
+
 __device__ __forceinline__ float4 split4_to_f32(float4 r) {  // split4_bf16 group (hi0..hi3 lo0..lo3) -> hi + lo
   const unsigned h01 = __float_as_uint(r.x), h23 = __float_as_uint(r.y);
   const unsigned l01 = __float_as_uint(r.z), l23 = __float_as_uint(r.w);
@@ -125,18 +131,21 @@ __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ 
   const long long t = idx / C4;
   const int c4 = (int)(idx - t * C4);
   const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
+  // buffer loads, zero beyond the image (the descriptor's range check): all 36 loads issue back to back instead of
+  // one exec-masked branch -- and one wait -- per patch element
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, (unsigned)((long long)nb * H * W * C * 4));
+  const unsigned cb = (unsigned)c4 * 16u;
+  const unsigned plane = (unsigned)(T * C4 * 16), base = (unsigned)(t * C4 + c4) * 16u;
+  const __amdgpu_buffer_rsrc_t vr = make_rsrc(v, plane * (unsigned)(AL * AL));
   float4 d[AL][AL];
 #pragma unroll
   for (int i = 0; i < AL; ++i)
 #pragma unroll
     for (int j = 0; j < AL; ++j) {
       const int h = MT * ti - 1 + i, w = MT * tj - 1 + j;
-      float4 val{0.f, 0.f, 0.f, 0.f};
-      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
-        const float4 r = *(const float4*)(x + (((long long)b * H + h) * W + w) * C + c4 * 4);
-        val = XS ? split4_to_f32(r) : r;
-      }
-      d[i][j] = val;
+      const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const float4 r = bload4(xr, ok ? ((unsigned)((b * H + h) * W + w) * (unsigned)C) * 4u + cb : OOB);
+      d[i][j] = XS ? split4_to_f32(r) : r;
     }
   constexpr auto bt = [](int i, int k) { return wino_bt<MT>(i, k); };
 #pragma unroll
@@ -146,7 +155,7 @@ __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ 
 #pragma unroll
   for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < AL; ++j) v[((long long)(i * AL + j) * T + t) * C4 + c4] = split4_bf16(d[i][j]);
+    for (int j = 0; j < AL; ++j) wstore(vr, base + (unsigned)(i * AL + j) * plane, split4_bf16(d[i][j]));
 }
 
 // G g G^T of a 3x3 filter of float4 groups
@@ -252,13 +261,15 @@ struct WinoOutGeo {
   static constexpr int NBK = TR * MT * WSEG / 32;
 };
 
-template <int MT, int WSEG, bool GNB>
+template <int MT, int WSEG, bool GNB, bool ST>
 __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
   constexpr int AL = MT + 2;
   using Geo = WinoOutGeo<MT, WSEG>;
   constexpr int TR = Geo::TR, CT = Geo::CT, NBK = Geo::NBK;
   const int N = p.N, N4 = N >> 2, th = p.H / MT, tw = p.W / MT, nseg = p.W / WSEG;
   const long long T = (long long)p.nb * th * tw;
+  const unsigned mplane = (unsigned)(T * N4 * 16);
+  const __amdgpu_buffer_rsrc_t mr = make_rsrc(p.m, mplane * (unsigned)(AL * AL));
   const long long ngrp = (long long)p.nb * (th / TR) * nseg;
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= ngrp * N4) return;
@@ -268,6 +279,12 @@ __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
   const long long rg = grp / nseg;
   const int b = (int)(rg / (th / TR)), ti0 = (int)(rg % (th / TR)) * TR, tj0 = seg * CT;
   const float4 bv = p.bias ? *(const float4*)(p.bias + c4 * 4) : float4{0.f, 0.f, 0.f, 0.f};
+  // y / residual / GroupNorm input through buffer descriptors (32-bit offsets; a null residual is an empty range,
+  // whose loads return zeros: no branch and no wait per pixel)
+  const unsigned ybytes = (unsigned)((long long)p.nb * p.H * p.W * N * 4);
+  const __amdgpu_buffer_rsrc_t yr = make_rsrc(p.y, ybytes);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res ? p.res : p.y, p.res ? ybytes : 0u);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(GNB ? p.gx : p.y, GNB ? ybytes : 0u);
   double s0[NBK], s1[NBK], g0[GNB ? NBK : 1][4], g1[GNB ? NBK : 1][4];
 #pragma unroll
   for (int q = 0; q < NBK; ++q) s0[q] = s1[q] = 0.0;
@@ -290,11 +307,12 @@ __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
     for (int tq = 0; tq < CT; ++tq) {
       const int ti = ti0 + tr, tj = tj0 + tq;
       const long long t = ((long long)b * th + ti) * tw + tj;
+      const unsigned mbase = (unsigned)(t * N4 + c4) * 16u;
       float4 mv[AL][AL];
 #pragma unroll
       for (int i = 0; i < AL; ++i)
 #pragma unroll
-        for (int j = 0; j < AL; ++j) mv[i][j] = *(const float4*)(p.m + ((long long)(i * AL + j) * T + t) * N + c4 * 4);
+        for (int j = 0; j < AL; ++j) mv[i][j] = bload4(mr, mbase + (unsigned)(i * AL + j) * mplane);
       constexpr auto at = [](int i, int k) { return wino_at<MT>(i, k); };
       float4 r[MT][AL];
 #pragma unroll
@@ -307,16 +325,15 @@ __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
         const int q = ((tr * MT + a) * WSEG) / 32;  // block within the group (compile-time: tr, a unrolled)
 #pragma unroll
         for (int e = 0; e < MT; ++e) {
-          const long long off = (((long long)b * p.H + row) * p.W + tj * MT + e) * N + c4 * 4;
-          float4 val = f4add(o[e], bv);
-          if (p.res) val = f4add(val, *(const float4*)(p.res + off));
-          *(float4*)(p.y + off) = val;
-          if (p.gn_part) {
+          const unsigned off = ((unsigned)((b * p.H + row) * p.W + tj * MT + e) * (unsigned)N + (unsigned)c4 * 4u) * 4u;
+          float4 val = f4add(f4add(o[e], bv), bload4(rr, off));
+          bstore4(yr, off, val);
+          if constexpr (ST) {
             s0[q] += ((double)val.x + (double)val.y) + ((double)val.z + (double)val.w);
             s1[q] += ((double)val.x * val.x + (double)val.y * val.y) + ((double)val.z * val.z + (double)val.w * val.w);
           }
           if constexpr (GNB) {
-            const float4 x4 = *(const float4*)(p.gx + off);
+            const float4 x4 = bload4(xr, off);
             const int bg = b * p.groups + (c4 * 4) / cpg;  // (a 4-channel group never straddles a GroupNorm group)
             const float mu = p.mean[bg], rs = p.rstd[bg];
             const float xs[4] = {x4.x, x4.y, x4.z, x4.w}, vs[4] = {val.x, val.y, val.z, val.w};
@@ -340,7 +357,7 @@ __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
   for (int q = 0; q < NBK; ++q) {
     // first pixel of local block q: (q 32 / WSEG) rows down, at the group's column segment
     const long long blk = (((long long)b * p.H + ti0 * MT + (q * 32) / WSEG) * p.W + seg * WSEG) >> 5;
-    if (p.gn_part) *(double2*)(p.gn_part + (blk * N4 + c4) * 2) = double2{s0[q], s1[q]};
+    if constexpr (ST) *(double2*)(p.gn_part + (blk * N4 + c4) * 2) = double2{s0[q], s1[q]};
     if constexpr (GNB) {
       double* gp = p.gnb_part + (blk * N + c4 * 4) * 2;
 #pragma unroll
@@ -356,6 +373,8 @@ __global__ void __launch_bounds__(256) wino_out_any_kernel(WinoOut p) {
   constexpr int AL = MT + 2;
   const int N = p.N, N4 = N >> 2, th = (p.H + MT - 1) / MT, tw = (p.W + MT - 1) / MT;
   const long long T = (long long)p.nb * th * tw;
+  const unsigned mplane = (unsigned)(T * N4 * 16);
+  const __amdgpu_buffer_rsrc_t mr = make_rsrc(p.m, mplane * (unsigned)(AL * AL));
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= T * N4) return;
   const long long t = idx / N4;
@@ -366,7 +385,7 @@ __global__ void __launch_bounds__(256) wino_out_any_kernel(WinoOut p) {
 #pragma unroll
   for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < AL; ++j) mv[i][j] = *(const float4*)(p.m + ((long long)(i * AL + j) * T + t) * N + c4 * 4);
+    for (int j = 0; j < AL; ++j) mv[i][j] = bload4(mr, (unsigned)(t * N4 + c4) * 16u + (unsigned)(i * AL + j) * mplane);
   constexpr auto at = [](int i, int k) { return wino_at<MT>(i, k); };
   float4 r[MT][AL];
 #pragma unroll
@@ -402,18 +421,18 @@ __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ 
   const long long t = idx / K4;
   const int k4 = (int)(idx - t * K4);
   const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
+  const __amdgpu_buffer_rsrc_t dr = make_rsrc(dy, (unsigned)((long long)nb * H * W * K * 4));
+  const unsigned plane = (unsigned)(T * K4 * 16), base = (unsigned)(t * K4 + k4) * 16u;
+  const __amdgpu_buffer_rsrc_t vr = make_rsrc(d, plane * (unsigned)(AL * AL));
   float4 v[MT][MT];
 #pragma unroll
   for (int a = 0; a < MT; ++a)
 #pragma unroll
     for (int e = 0; e < MT; ++e) {
-      const int h = MT * ti + a, w = MT * tj + e;
-      float4 val{0.f, 0.f, 0.f, 0.f};  // (pixels past the image edge carry no gradient)
-      if (h < H && w < W) {
-        const float4 r = *(const float4*)(dy + (((long long)b * H + h) * W + w) * K + k4 * 4);
-        val = XS ? split4_to_f32(r) : r;
-      }
-      v[a][e] = val;
+      const int h = MT * ti + a, w = MT * tj + e;  // (pixels past the image edge carry no gradient: zero)
+      const float4 r = bload4(dr, (h < H && w < W) ? ((unsigned)((b * H + h) * W + w) * (unsigned)K) * 4u +
+                                                         (unsigned)k4 * 16u : OOB);
+      v[a][e] = XS ? split4_to_f32(r) : r;
     }
   constexpr auto ac = [](int i, int k) { return wino_at<MT>(k, i); };  // A = (A^T)^T
   float4 c[AL][MT], o[AL][AL];
@@ -424,7 +443,7 @@ __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ 
 #pragma unroll
   for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < AL; ++j) d[((long long)(i * AL + j) * T + t) * K4 + k4] = split4_bf16(o[i][j]);
+    for (int j = 0; j < AL; ++j) wstore(vr, base + (unsigned)(i * AL + j) * plane, split4_bf16(o[i][j]));
 }
 
 // dw [cout][3][3][cin] = beta * dw + G^T M G, M [a^2][cout][cin] fp32: one thread per (k, 4-group of c)
@@ -469,9 +488,10 @@ static long long wino_tiles(int nb, int h, int w, int mt) {
 
 // any image size (edge tiles zero-filled / cut), channel counts % 4, every operand < 4 GiB
 static bool wino_geom_ok(int mt, int nb, int h, int w, int cin, int cout) {
+  // (the transforms address the whole [P][T][c] array through one buffer descriptor: < 4 GiB)
   return (mt == 2 || mt == 4) && nb > 0 && h > 0 && w > 0 && cin > 0 && cout > 0 && cin % 4 == 0 && cout % 4 == 0 &&
          (long long)nb * h * w * std::max(cin, cout) * 4 <= MAX_DESC_BYTES &&
-         wino_tiles(nb, h, w, mt) * std::max(cin, cout) * 4 <= MAX_DESC_BYTES;
+         (long long)(mt + 2) * (mt + 2) * wino_tiles(nb, h, w, mt) * std::max(cin, cout) * 4 <= MAX_DESC_BYTES;
 }
 
 // the blocked output transform (statistics in the 32-pixel-block layouts): whole tiles, and thread groups that are
@@ -491,8 +511,9 @@ static void wino_out_go(WinoOut& p, bool gnb, hipStream_t st) {
   using Geo = WinoOutGeo<MT, WSEG>;
   const long long groups = (long long)p.nb * (p.H / MT / Geo::TR) * (p.W / WSEG);
   const dim3 g(egrid256(groups * (p.N / 4)));
-  if (gnb) hipLaunchKernelGGL((wino_out_kernel<MT, WSEG, true>), g, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((wino_out_kernel<MT, WSEG, false>), g, dim3(256), 0, st, p);
+  if (gnb) hipLaunchKernelGGL((wino_out_kernel<MT, WSEG, true, false>), g, dim3(256), 0, st, p);
+  else if (p.gn_part) hipLaunchKernelGGL((wino_out_kernel<MT, WSEG, false, true>), g, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((wino_out_kernel<MT, WSEG, false, false>), g, dim3(256), 0, st, p);
 }
 
 static int wino_out_launch(WinoOut& p, int tile, bool gnb, void* stream) {
