@@ -262,7 +262,8 @@ def _roofline(rec_all, bf16, config, step_ms, detail, rank, exact=False):
     alg_bytes = sum(gemm_algorithmic_bytes(r[0], r[4]) for r in rec) / max(len(rec), 1)
     peak = BF16_DENSE_PEAK_TF if bf16 else FP32_MFMA_PEAK_TF if exact else PEAK_3XBF16_TF
     pmc = _pmc_traffic(config)
-    roofline = {"bound": "mfma", "kernel": "gemm3x_kernel (implicit-GEMM conv + attention bmm, all launches)",
+    roofline = {"bound": "mfma", "kernel": ("gemm3x_kernel (implicit-GEMM conv, Winograd position GEMMs with their "
+                                            "transforms, attention bmm; all launches)"),
                 "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(ach / peak, 4), "traffic": (pmc or {}).get("bytes_per_launch"),
                 "traffic_unit": "HBM bytes per launch (PMC)", "traffic_detail": pmc,
@@ -272,7 +273,8 @@ def _roofline(rec_all, bf16, config, step_ms, detail, rank, exact=False):
                               "3xBF16 fp32-emulation ceiling = bf16 dense MFMA 2.5 PF/s / 3; "
                               "native fp32 MFMA peak is 157.3 TF/s"),
                 "achieved_note": ("algorithmic FLOPs of the algorithms run (Upsample convs in sub-pixel form "
-                                  "count 4/9 of the reference conv's FLOPs)"),
+                                  "count 4/9 of the reference conv's FLOPs, Winograd F(4x4,3x3) convs 1/4) over the "
+                                  "time of all their launches, transforms included"),
                 "reference_equivalent_TFLOP/s": round(tot_ref / (tot_ms * 1e-3) / 1e12, 2),
                 "launches_per_step": len(rec), "avg_launch_us": round(tot_ms * 1e3 / max(len(rec), 1), 2),
                 "gemm_ms_per_step": round(tot_ms, 2), "instrumented_step_ms": round(step_ms, 2),
@@ -522,7 +524,8 @@ def _compact_roofline(r):
     if not r:
         return None
     out = {k: r[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "algorithmic_bytes_per_launch",
-                             "launches_per_step", "avg_launch_us", "gemm_ms_per_step", "instrumented_step_ms")
+                             "launches_per_step", "avg_launch_us", "gemm_ms_per_step", "instrumented_step_ms",
+                             "reference_equivalent_TFLOP/s")
            if k in r}
     out["kernel"] = "gemm3x_kernel"
     if r.get("by_pass"):  # per pass: [launches, ms per step, TFLOP/s]
