@@ -252,7 +252,12 @@ def _wino_ok(g, n: int, h: int, wd: int, cin: int, cout: int) -> bool:
     return (WINOGRAD and _MATH[0] == 0 and _dma_fmt() == 0 and g.kh == 3 and g.kw == 3 and g.stride == 1 and
             not g.upsample and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and wd <= WINOGRAD_MAX_W and
             cin % 4 == 0 and cout % 4 == 0 and min(cin, cout) >= WINOGRAD_MIN_C and
-            9.0 * n * h * wd * cin * cout >= WINOGRAD_MIN_MACS)
+            9.0 * n * h * wd * cin * cout >= WINOGRAD_MIN_MACS and
+            # (each transformed operand is addressed through one buffer descriptor: < 4 GiB)
+            (WINOGRAD_TILE + 2) ** 2 * _wino_tiles(n, h, wd) * max(cin, cout) * 4 <= _MAX_DESC_BYTES)
+
+
+_MAX_DESC_BYTES = 0xFFFFFF00  # csrc/gemm_core.h MAX_DESC_BYTES
 
 
 def _wino_blocks(h: int, wd: int) -> bool:
@@ -1003,9 +1008,16 @@ def _bwd_side(t: torch.Tensor):
     return side
 
 
+# experiment knob: also overlap the two backward passes of the Winograd convs (their memory-bound transforms against the
+# other pass's GEMM), whatever their size
+BWD_OVERLAP_WINO = os.environ.get("MVAE_BWD_OVERLAP_WINO") is not None
+
+
 def _overlap_ok(x, dy, g) -> bool:
-    n, c, _, _ = x.shape
+    n, c, h, w = x.shape
     _, co, ho, wo = dy.shape
+    if BWD_OVERLAP_WINO and _wino_ok(g, n, h, w, c, co):
+        return True
     # (image-side convs -- cout 3 / latent channels -- run memory-bound special kernels: c4 lost 0.35 % overlapping them)
     return not g.pointwise and min(c, co) >= 32 and 2.0 * n * ho * wo * co * c * g.kh * g.kw <= BWD_OVERLAP_MAX_FLOPS
 

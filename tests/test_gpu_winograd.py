@@ -250,3 +250,4 @@ def test_winograd_kept_input_transform_feeds_weight_gradient(dev, monkeypatch):
     dxr, dwr, nr = run(False)
     assert (nk, nr) == (1, 2)  # backward: dy's transform only, vs dy's and x's
     assert torch.equal(dwk, dwr) and torch.equal(dxk, dxr)
+
