@@ -404,6 +404,7 @@ def run_config(name, args, rank, world, dev, want_cpu=True, steps=None, warmup=N
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     loss_v = float(loss.detach())
+    peak_gb = torch.cuda.max_memory_allocated(dev) / 1e9  # HBM held by the step (caching allocator peak)
 
     roofline = None
     bf16 = cfg.get("precision", "32") == "bf16-mixed"
@@ -438,7 +439,7 @@ def run_config(name, args, rank, world, dev, want_cpu=True, steps=None, warmup=N
                        "model": cfg["cls"], "params": nparams, "global_batch": cfg["batch"] * world,
                        "per_gpu_batch": cfg["batch"], "resolution": cfg["res"], "parallelism": f"dp{world}",
                        "rccl_world_size": world, "backend": dist.get_backend() if world > 1 else None,
-                       "step_launch": launch},
+                       "step_launch": launch, "peak_hbm_GB": round(peak_gb, 1)},
             "loss": round(loss_v, 6), "roofline": roofline, "cpu_baseline": cpu}
 
 

@@ -224,6 +224,9 @@ def _al16(*ts) -> bool:
 # MVAE_WINOGRAD_MIN_C sets the smallest channel count (both sides) it is used for.
 WINOGRAD = os.environ.get("MVAE_NO_WINOGRAD") is None
 WINOGRAD_MIN_C = int(os.environ.get("MVAE_WINOGRAD_MIN_C", "512"))
+# ... and for images at least 32 wide (c4's 64x64x256 level: 665 -> 692 img/s same box; c2's 14x14x256 level lost 3 %
+# at 256 channels)
+WINOGRAD_MIN_C_WIDE = int(os.environ.get("MVAE_WINOGRAD_MIN_C_WIDE", "256"))
 # output tile m of F(m x m, 3x3): 4 (default; 1/4 of the direct MACs, V / M 2.25x the input / output) or 2 (4/9 of the
 # MACs, 4x the traffic, ~7x smaller transform error)
 WINOGRAD_TILE = int(os.environ.get("MVAE_WINOGRAD_TILE", "4"))
@@ -238,7 +241,7 @@ def _wino_alg(ref: float) -> float:
 
 
 # widest image it is used for (the library takes W in {8, 16} and multiples of 32)
-WINOGRAD_MAX_W = int(os.environ.get("MVAE_WINOGRAD_MAX_W", "32"))
+WINOGRAD_MAX_W = int(os.environ.get("MVAE_WINOGRAD_MAX_W", "64"))
 
 
 # smallest conv (direct MACs) it is used for: the four launches of the Winograd form lose to one implicit GEMM on small
@@ -251,7 +254,8 @@ def _wino_ok(g, n: int, h: int, wd: int, cin: int, cout: int) -> bool:
     statistics / partials additionally need _wino_blocks."""
     return (WINOGRAD and _MATH[0] == 0 and _dma_fmt() == 0 and g.kh == 3 and g.kw == 3 and g.stride == 1 and
             not g.upsample and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and wd <= WINOGRAD_MAX_W and
-            cin % 4 == 0 and cout % 4 == 0 and min(cin, cout) >= WINOGRAD_MIN_C and
+            cin % 4 == 0 and cout % 4 == 0 and
+            min(cin, cout) >= (WINOGRAD_MIN_C_WIDE if wd >= 32 else WINOGRAD_MIN_C) and
             9.0 * n * h * wd * cin * cout >= WINOGRAD_MIN_MACS and
             # (each transformed operand is addressed through one buffer descriptor: < 4 GiB)
             (WINOGRAD_TILE + 2) ** 2 * _wino_tiles(n, h, wd) * max(cin, cout) * 4 <= _MAX_DESC_BYTES)

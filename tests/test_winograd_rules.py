@@ -10,22 +10,27 @@ G3 = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
 def rules(monkeypatch):
     monkeypatch.setattr(ops, "WINOGRAD", True)
     monkeypatch.setattr(ops, "WINOGRAD_TILE", 4)
-    monkeypatch.setattr(ops, "WINOGRAD_MAX_W", 32)
+    monkeypatch.setattr(ops, "WINOGRAD_MAX_W", 64)
     monkeypatch.setattr(ops, "WINOGRAD_MIN_C", 512)
+    monkeypatch.setattr(ops, "WINOGRAD_MIN_C_WIDE", 256)
     monkeypatch.setattr(ops, "WINOGRAD_MIN_MACS", 1e10)
     monkeypatch.setattr(ops, "_MATH", [0])  # (a private list: the process-wide mode is untouched)
     return monkeypatch
 
 
 def test_c4_levels(rules):
-    """c4 at B = 256: the 8x8 / 16x16 / 32x32 levels run Winograd, the 64x64 level and every non-3x3 / strided /
-    upsample conv the implicit GEMM."""
+    """c4 at B = 256: every 3x3 / stride-1 level runs Winograd (the 64x64 level at 256 channels: images >= 32 wide take
+    >= 256 channels), except the 64x64 conv with a 512-channel side (operand over 4 GiB); non-3x3 / strided /
+    upsample convs the implicit GEMM."""
     assert ops._wino_ok(G3, 256, 8, 8, 2048, 2048)
     assert ops._wino_ok(G3, 256, 16, 16, 1024, 1024)
     assert ops._wino_ok(G3, 256, 32, 32, 512, 512)
     assert ops._wino_ok(G3, 256, 32, 32, 1024, 512)
-    assert not ops._wino_ok(G3, 256, 64, 64, 256, 256)        # width above MAX_W
-    assert not ops._wino_ok(G3, 256, 32, 32, 256, 512)        # 256 input channels
+    assert ops._wino_ok(G3, 256, 64, 64, 256, 256)
+    assert not ops._wino_ok(G3, 256, 64, 64, 512, 256)        # 36 x 65,536 x 512 x 4 B > 4 GiB
+    assert not ops._wino_ok(G3, 256, 32, 32, 128, 512)        # 128 input channels
+    assert not ops._wino_ok(G3, 256, 14, 14, 256, 256)        # narrow images need 512 channels
+    assert not ops._wino_ok(G3, 64, 128, 128, 256, 256)       # width above MAX_W
     assert not ops._wino_ok(ops.ConvGeom(1, 1), 256, 16, 16, 1024, 1024)
     assert not ops._wino_ok(ops.ConvGeom(3, 3, 2, 0, 0, 1, 1), 256, 16, 16, 512, 512)
     assert not ops._wino_ok(ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, True), 256, 16, 16, 512, 512)
@@ -43,8 +48,6 @@ def test_small_batches_and_math_modes(rules):
 def test_size_rule_keeps_operands_under_4gib(rules):
     """A conv whose transformed operand would exceed one buffer descriptor stays on the implicit GEMM (the 64x64x512
     decoder conv at B = 256: 36 x 65,536 tiles x 512 channels x 4 B = 4.8 GB) instead of failing in the library."""
-    rules.setattr(ops, "WINOGRAD_MAX_W", 64)
-    rules.setattr(ops, "WINOGRAD_MIN_C", 256)
     assert ops._wino_ok(G3, 256, 64, 64, 256, 256)
     assert not ops._wino_ok(G3, 256, 64, 64, 512, 256)
     assert not ops._wino_ok(G3, 2048, 32, 32, 512, 512)       # c4's 32x32 level at B = 2048
