@@ -64,6 +64,7 @@ def _wino_on(monkeypatch, request):
     from medvae_disentangled_multimodal_amd import ops
     monkeypatch.setattr(ops, "WINOGRAD", True)
     monkeypatch.setattr(ops, "WINOGRAD_MIN_C", 1)
+    monkeypatch.setattr(ops, "WINOGRAD_MIN_C_WIDE", 1)
     monkeypatch.setattr(ops, "WINOGRAD_TILE", request.param)
     monkeypatch.setattr(ops, "WINOGRAD_MAX_W", 64)
     monkeypatch.setattr(ops, "WINOGRAD_MIN_MACS", 0.0)
