@@ -185,6 +185,12 @@ size_t mvae_conv2d_wgrad_upsample_workspace_bytes(int nb, int h, int w_, int cin
 int mvae_winograd_weight_transform(const float* w, void* u, int cin, int cout, int dgrad, int tile, void* stream);
 int mvae_winograd_input_transform(const float* x, void* v, int nb, int h, int w, int c, int x_split, int tile,
                                   void* stream);
+/* input_transform of silu?(GroupNorm(x)) with the normalization applied on load (x = the GroupNorm's INPUT, scale /
+ * shift [nb][c] = rstd * gamma, beta - mean * rstd * gamma from mvae_group_norm_stats_nhwc): the GroupNorm output that
+ * only feeds this conv is never written (the SURVEY §7 GroupNorm+SiLU-into-the-conv-operand fusion, on the Winograd
+ * form's one read of its input). */
+int mvae_winograd_input_transform_gn(const float* x, const float* scale, const float* shift, int silu, void* v, int nb,
+                                     int h, int w, int c, int tile, void* stream);
 int mvae_winograd_gemm(const void* v, const void* u, float* m, long long tiles, int k_in, int n_out, int tile,
                        void* stream);
 int mvae_winograd_output_transform(const float* m, const float* bias, const float* residual, float* y, double* gn_part,
@@ -316,6 +322,15 @@ int mvae_group_norm_bwd_split_nhwc(const float* x, const float* dy, const float*
  * 28x28 / 14x14 / 7x7 levels -- run the register-resident one-pass kernels: x read once per pass),
  * 1 = streaming only (statistics pass + apply pass). Both are deterministic; they agree to fp32 rounding. */
 int mvae_set_group_norm_path(int mode);
+/* GroupNorm statistics only, for a consumer that normalizes on load (mvae_winograd_input_transform_gn): mean / rstd
+ * [nb * groups] and the apply's affine scale = rstd * gamma, shift = beta - mean * scale ([nb][c]); part (nullable):
+ * the producing conv's epilogue statistics (no pass over x). mvae_group_norm_apply_nhwc materializes y = silu?(x * scale
+ * + shift) from them when a deferred output must exist after all (y_split as mvae_group_norm_fwd_nhwc, no dropout). */
+int mvae_group_norm_stats_nhwc(const float* x, const double* part, const float* gamma, const float* beta, float* mean,
+                               float* rstd, float* scale, float* shift, int nb, int hw, int c, int groups, float eps,
+                               void* workspace, size_t workspace_bytes, void* stream);
+int mvae_group_norm_apply_nhwc(const float* x, const float* scale, const float* shift, float* y, int nb, int hw, int c,
+                               int silu, int y_split, void* stream);
 /* mvae_group_norm_bwd_nhwc (drop_p = 0) from the partials of mvae_conv2d_dgrad_gnbwd_nhwc: no reduction
  * pass over x and dy. hw % 32 == 0. */
 int mvae_group_norm_bwd_part_nhwc(const float* x, const float* dy, const double* part, const float* gamma,

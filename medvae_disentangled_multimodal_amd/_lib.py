@@ -35,6 +35,9 @@ SIGNATURES = {
     "mvae_conv2d_wgrad_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, I, I, I, I, I, I, I, I, P, Z, P]),
     "mvae_winograd_weight_transform": (I, [P, P, I, I, I, I, P]),
     "mvae_winograd_input_transform": (I, [P, P, I, I, I, I, I, I, P]),
+    "mvae_winograd_input_transform_gn": (I, [P, P, P, I, P, I, I, I, I, I, P]),
+    "mvae_group_norm_stats_nhwc": (I, [P, P, P, P, P, P, P, P, I, I, I, I, F, P, Z, P]),
+    "mvae_group_norm_apply_nhwc": (I, [P, P, P, P, I, I, I, I, I, P]),
     "mvae_winograd_gemm": (I, [P, P, P, L, I, I, I, P]),
     "mvae_winograd_output_transform": (I, [P, P, P, P, P, I, I, I, I, I, P]),
     "mvae_winograd_output_gnbwd": (I, [P, P, P, P, P, P, P, I, I, P, I, I, I, I, I, P]),

@@ -1202,6 +1202,56 @@ int mvae_group_norm_fwd_part_nhwc(const float* x, const double* part, const floa
   return launch_status();
 }
 
+// Statistics only (the consumer applies the normalization itself: the Winograd input transform of the following conv,
+// mvae_winograd_input_transform_gn): mean / rstd [nb * groups] and the per-(sample, channel) affine of the apply,
+// scale = rstd * gamma, shift = beta - mean * scale ([nb][c] fp32 each, the bytes gn_apply uses). part (nullable): the
+// producing conv's epilogue statistics (mvae_conv2d_gnstats_nhwc layout; hw % 32 == 0, channels per group % 4 == 0);
+// without it one fp64 partial pass over x.
+int mvae_group_norm_stats_nhwc(const float* x, const double* part, const float* gamma, const float* beta, float* mean,
+                               float* rstd, float* scale, float* shift, int nb, int hw, int c, int groups, float eps,
+                               void* workspace, size_t workspace_bytes, void* stream) {
+  if (nb <= 0 || hw <= 0 || c <= 0 || (c & 3) || groups <= 0 || c % groups || !scale || !shift || !mean || !rstd ||
+      (part && ((c / groups) % 4 || hw % 32))) {
+    set_error("group_norm_stats: C %% 4 == 0 and %% groups (with part: hw %% 32 == 0, channels per group %% 4 == 0)");
+    return MVAE_EINVAL;
+  }
+  if (!part && workspace_bytes < mvae_group_norm_workspace_bytes(nb, hw, c)) {
+    set_error("group_norm_stats: workspace too small");
+    return MVAE_EWORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  GnArgs a{};
+  a.x = x; a.gamma = gamma; a.beta = beta; a.nb = nb; a.hw = hw; a.C = c; a.G = groups;
+  a.chunks = gn_chunks(nb, hw);
+  a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
+  a.ws = (double*)workspace;
+  const dim3 fg(cdiv((long long)nb * groups, 4));
+  if (part) {
+    hipLaunchKernelGGL(gn_stats_finalize_part_kernel, fg, dim3(256), 0, st, a, part, mean, rstd, scale, shift, eps);
+  } else {
+    hipLaunchKernelGGL(gn_partial_kernel<0>, dim3(a.chunks, nb), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(gn_stats_finalize_kernel, fg, dim3(256), 0, st, a, mean, rstd, scale, shift, eps);
+  }
+  return launch_status();
+}
+
+// y = silu?(x * scale + shift) from mvae_group_norm_stats_nhwc's affine (y_split as mvae_group_norm_fwd_nhwc; no
+// dropout): the normalization a deferred GroupNorm output needs when its consumer cannot apply it itself
+int mvae_group_norm_apply_nhwc(const float* x, const float* scale, const float* shift, float* y, int nb, int hw, int c,
+                               int silu, int y_split, void* stream) {
+  if (nb <= 0 || hw <= 0 || c <= 0 || (c & 3) || !x || !scale || !shift || !y) {
+    set_error("group_norm_apply: C %% 4 == 0");
+    return MVAE_EINVAL;
+  }
+  GnArgs a{};
+  a.x = x; a.nb = nb; a.hw = hw; a.C = c; a.G = 1;
+  a.chunks = gn_chunks(nb, hw);
+  a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
+  a.silu = silu; a.drop_p = 0.f; a.y_split = y_split; a.salt = dropout_salt();
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(a.chunks, nb), dim3(256), 0, (hipStream_t)stream, a, scale, shift, y);
+  return launch_status();
+}
+
 // dx = d/dx of the fused forward [+ dx_add when non-null]; dgamma/dbeta are ACCUMULATED (+=) when non-null.
 // pack (non-null dxp): also dxp = packed bf16 of dx and dbias = bias_beta * dbias + column sums of dx (the consuming
 // conv's bf16 output gradient and bias gradient; partials in cs_ws)

@@ -120,9 +120,18 @@ __device__ __forceinline__ float4 split4_to_f32(float4 r) {  // split4_bf16 grou
 
 // x [nb][H][W][C] (fp32, or split4_bf16 groups when XS) -> V [a^2][T][C] split4_bf16, T = nb (H/m) (W/m)
 // one thread per (tile, 4-channel group): a^2 coalesced 16-B loads (zeros outside the image), a^2 16-B stores
-template <int MT, bool XS>
+// GN (nullable): x is a GroupNorm INPUT -- each in-image element is normalized on load, y = silu?(x * scale[b][c] +
+// shift[b][c]) (mvae_group_norm_stats_nhwc's affine; the apply pass's arithmetic), so the GroupNorm output feeding this
+// conv is never written (zero padding stays zero: it pads y)
+struct WinoGn {
+  const float* scale;
+  const float* shift;
+  int silu;
+};
+
+template <int MT, bool XS, bool GN = false>
 __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ x, uint4* __restrict__ v, int nb, int H,
-                                                      int W, int C) {
+                                                      int W, int C, WinoGn gn) {
   constexpr int AL = MT + 2;
   const int C4 = C >> 2, th = (H + MT - 1) / MT, tw = (W + MT - 1) / MT;  // (edge tiles zero-filled)
   const long long T = (long long)nb * th * tw;
@@ -137,6 +146,11 @@ __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ 
   const unsigned cb = (unsigned)c4 * 16u;
   const unsigned plane = (unsigned)(T * C4 * 16), base = (unsigned)(t * C4 + c4) * 16u;
   const __amdgpu_buffer_rsrc_t vr = make_rsrc(v, plane * (unsigned)(AL * AL));
+  float4 sc{1.f, 1.f, 1.f, 1.f}, sh{0.f, 0.f, 0.f, 0.f};
+  if constexpr (GN) {
+    sc = *(const float4*)(gn.scale + (long long)b * C + c4 * 4);
+    sh = *(const float4*)(gn.shift + (long long)b * C + c4 * 4);
+  }
   float4 d[AL][AL];
 #pragma unroll
   for (int i = 0; i < AL; ++i)
@@ -145,7 +159,18 @@ __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ 
       const int h = MT * ti - 1 + i, w = MT * tj - 1 + j;
       const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
       const float4 r = bload4(xr, ok ? ((unsigned)((b * H + h) * W + w) * (unsigned)C) * 4u + cb : OOB);
-      d[i][j] = XS ? split4_to_f32(r) : r;
+      if constexpr (GN) {
+        float o[4] = {r.x * sc.x + sh.x, r.y * sc.y + sh.y, r.z * sc.z + sh.z, r.w * sc.w + sh.w};
+        // SiLU with the hardware reciprocal (1 ulp) instead of an IEEE division: each element is normalized once per
+        // patch that covers it (~2.25x at m = 4), so the division's ~10 instructions per element made this kernel
+        // VALU-bound (measured: the fused form lost 0.9 % on c4 with sigmoid_f)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (gn.silu) o[k] = o[k] * __builtin_amdgcn_rcpf(1.f + __expf(-o[k]));
+        d[i][j] = ok ? float4{o[0], o[1], o[2], o[3]} : float4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        d[i][j] = XS ? split4_to_f32(r) : r;
+      }
     }
   constexpr auto bt = [](int i, int k) { return wino_bt<MT>(i, k); };
 #pragma unroll
@@ -577,12 +602,35 @@ int mvae_winograd_input_transform(const float* x, void* v, int nb, int h, int w,
   hipStream_t st = (hipStream_t)stream;
   const dim3 g(egrid256(wino_tiles(nb, h, w, tile) * (c / 4)));
   if (tile == 2) {
-    if (x_split) hipLaunchKernelGGL((wino_in_kernel<2, true>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c);
-    else hipLaunchKernelGGL((wino_in_kernel<2, false>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c);
+    if (x_split) hipLaunchKernelGGL((wino_in_kernel<2, true>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c,
+                                 WinoGn{});
+    else hipLaunchKernelGGL((wino_in_kernel<2, false>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c,
+                                 WinoGn{});
   } else {
-    if (x_split) hipLaunchKernelGGL((wino_in_kernel<4, true>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c);
-    else hipLaunchKernelGGL((wino_in_kernel<4, false>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c);
+    if (x_split) hipLaunchKernelGGL((wino_in_kernel<4, true>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c,
+                                 WinoGn{});
+    else hipLaunchKernelGGL((wino_in_kernel<4, false>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c,
+                                 WinoGn{});
   }
+  return launch_status();
+}
+
+// V of silu?(GroupNorm(x)) without that GroupNorm output ever written: x the GroupNorm's input, scale / shift [nb][c]
+// from mvae_group_norm_stats_nhwc
+int mvae_winograd_input_transform_gn(const float* x, const float* scale, const float* shift, int silu, void* v, int nb,
+                                     int h, int w, int c, int tile, void* stream) {
+  if (!x || !v || !scale || !shift || !wino_geom_ok(tile, nb, h, w, c, c) || !al16(x) || !al16(v) || !al16(scale) ||
+      !al16(shift)) {
+    set_error("winograd_input_transform_gn: tile 2 or 4, c %% 4 == 0, 16-B aligned");
+    return MVAE_EINVAL;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g(egrid256(wino_tiles(nb, h, w, tile) * (c / 4)));
+  const WinoGn gn{scale, shift, silu};
+  if (tile == 2)
+    hipLaunchKernelGGL((wino_in_kernel<2, false, true>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, gn);
+  else
+    hipLaunchKernelGGL((wino_in_kernel<4, false, true>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, gn);
   return launch_status();
 }
 

@@ -12,6 +12,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import weakref
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -264,6 +265,15 @@ def _wino_ok(g, n: int, h: int, wd: int, cin: int, cout: int) -> bool:
 _MAX_DESC_BYTES = 0xFFFFFF00  # csrc/gemm_core.h MAX_DESC_BYTES
 
 
+def _lazy_wino(lazy, x, w, b, res, g, gn_part, wgrad: bool) -> bool:
+    """A deferred GroupNorm output can stay deferred: its conv runs the Winograd forward (normalizing on load) and, when
+    the weight gradient is wanted, the Winograd weight gradient on the kept input transform."""
+    n, c, h, wd = x.shape
+    return (_wino_ok(g, n, h, wd, c, w.shape[0]) and _al16(w, lazy.x) and (b is None or _al16(b)) and
+            (res is None or _al16(res)) and (gn_part is None or _wino_blocks(h, wd)) and
+            (not wgrad or WINOGRAD_WGRAD))
+
+
 def _wino_blocks(h: int, wd: int) -> bool:
     """The output transform's 32-pixel-block form (GroupNorm statistics / backward partials from it)."""
     return h % 4 == 0 and (wd in (8, 16) or wd % 32 == 0)
@@ -275,6 +285,33 @@ def _wino_tiles(n: int, h: int, wd: int) -> int:
 
 
 WINOGRAD_WGRAD = os.environ.get("MVAE_NO_WINOGRAD_WGRAD") is None
+# GroupNorm(+SiLU) -> Winograd conv: the GroupNorm computes its statistics only and the conv's input transform applies
+# the normalization on load (mvae_winograd_input_transform_gn), so the GroupNorm output is never written or read
+# (SURVEY §7 hard part 4 / VERDICT r4 item 3 on the Winograd form, which reads its input once). The output handed to the
+# conv is a deferred placeholder: an expanded NaN scalar carrying GN_LAZY_ATTR, never materialized on this path.
+# Opt-in (MVAE_WINOGRAD_GN=1): measured on c4 (same box, interleaved) the GroupNorm family drops 40.5 -> 32.7 ms per
+# step but the input transforms, now normalizing every patch element (~2.25 loads per element) from the GroupNorm's
+# input instead of reading the just-written output, take ~10 ms longer: 689 -> 686 img/s (profiles/r05_winograd_gn_ab.txt)
+WINOGRAD_GN = os.environ.get("MVAE_WINOGRAD_GN") is not None
+GN_LAZY_ATTR = "_mvae_gn_lazy"
+G3 = ConvGeom(3, 3, 1, 1, 1, 1, 1, False)  # the GroupNorm-fed convs' geometry (ResnetBlock conv1 / conv2, conv_out)
+
+
+class LazyGn:
+    """A GroupNorm output deferred to its consuming conv: x (the GroupNorm input), the apply's affine (scale, shift
+    [n][c]) and the SiLU flag. materialize() writes y for a consumer that cannot apply it itself."""
+    __slots__ = ("x", "scale", "shift", "silu")
+
+    def __init__(self, x, silu: bool):
+        self.x, self.silu = x, int(silu)
+        self.scale = self.shift = None
+
+    def materialize(self):
+        n, c, h, w = self.x.shape
+        y = torch.empty_like(self.x, memory_format=CL)
+        _lib.call("mvae_group_norm_apply_nhwc", self.x.data_ptr(), self.scale.data_ptr(), self.shift.data_ptr(),
+                  y.data_ptr(), n, h * w, c, self.silu, 0, _stream(self.x))
+        return y
 
 
 def _wino_wgrad_ok(g, x, dy, dw, dys) -> bool:
@@ -290,9 +327,11 @@ def _wino_wgrad_ok(g, x, dy, dw, dys) -> bool:
 WINOGRAD_KEEP_V = os.environ.get("MVAE_NO_WINOGRAD_KEEP_V") is None
 
 
-def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split: bool, dgrad: bool, st, keep=None):
+def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split: bool, dgrad: bool, st, keep=None,
+              gn=None, key=None):
     """U (filters), V (input tiles) and the (m+2)^2 position GEMMs M = V U^T; returns M (arena) for an output
-    transform. keep (a list): V is allocated outside the arena and appended to it (WINOGRAD_KEEP_V)."""
+    transform. keep (a list): V is allocated outside the arena and appended to it (WINOGRAD_KEEP_V), tagged with `key`
+    (the conv's input tensor; default src). gn (LazyGn): src is a GroupNorm input, normalized on load."""
     mt = WINOGRAD_TILE
     t = _wino_tiles(n, h, wd)
     pos = (mt + 2) ** 2
@@ -300,13 +339,19 @@ def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split:
     u = ARENA.get("wino_u", 4 * pos * k_in * n_out, dev)
     if keep is not None:
         v = torch.empty(4 * pos * t * k_in, dtype=torch.uint8, device=dev)
-        keep.append((v, mt, src.data_ptr(), src._version))
+        kt = src if key is None else key
+        keep.append((v, mt, kt.data_ptr(), kt._version))
     else:
         v = ARENA.get("wino_v", 4 * pos * t * k_in, dev)
     m = ARENA.get("wino_m", 4 * pos * t * n_out, dev)
     cin, cout = (n_out, k_in) if dgrad else (k_in, n_out)
     _lib.call("mvae_winograd_weight_transform", w.data_ptr(), u.data_ptr(), cin, cout, int(dgrad), mt, st)
-    _lib.call("mvae_winograd_input_transform", src.data_ptr(), v.data_ptr(), n, h, wd, k_in, int(src_split), mt, st)
+    if gn is not None:
+        _lib.call("mvae_winograd_input_transform_gn", src.data_ptr(), gn.scale.data_ptr(), gn.shift.data_ptr(), gn.silu,
+                  v.data_ptr(), n, h, wd, k_in, mt, st)
+    else:
+        _lib.call("mvae_winograd_input_transform", src.data_ptr(), v.data_ptr(), n, h, wd, k_in, int(src_split), mt,
+                  st)
     _lib.call("mvae_winograd_gemm", v.data_ptr(), u.data_ptr(), m.data_ptr(), t, k_in, n_out, mt, st)
     return m
 
@@ -591,7 +636,7 @@ def _conv_call(x, w, b, res, y, n, h, wd, c, co, kh, kw, stride, pad_t, pad_l, h
 
 
 def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part=None, x_bf16: bool = False,
-                       keep_v=None):
+                       keep_v=None, lazy=None):
     """gn_part (fp64 [n*ho*wo/32 * cout/4 * 2]): also emit the GroupNorm statistics of y from the GEMM
     epilogue (mvae_conv2d_gnstats_nhwc; only on the plain implicit-GEMM path -- the caller checks).
     x_bf16: x holds packed bf16 (BF16_ATTR; bf16-mixed mode)."""
@@ -613,10 +658,14 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
         return _conv_fwd_bf16(x, w, b, res, g, y, n, c, h, wd, co, ho, wo, sub, alg, ref, gn_part, st, x_bf16)
     if x_bf16:
         raise RuntimeError("conv2d: a packed bf16 input needs the bf16-mixed LDS-DMA conv path")
-    if _wino_ok(g, n, h, wd, c, co) and _al16(x, w) and (b is None or _al16(b)) and (res is None or _al16(res)) and \
-            (gn_part is None or _wino_blocks(h, wd)):
+    wino = _wino_ok(g, n, h, wd, c, co) and _al16(w) and (b is None or _al16(b)) and (res is None or _al16(res)) and \
+        (gn_part is None or _wino_blocks(h, wd)) and _al16(lazy.x if lazy is not None else x)
+    if lazy is not None and not wino:  # a deferred GroupNorm output whose conv cannot normalize on load: write it
+        x, lazy = lazy.materialize(), None
+    if wino:
         with _timed("conv_fwd", _wino_alg(ref), (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
-            m = _winograd(x, w, n, h, wd, c, co, x_split, False, st, keep_v)
+            src = lazy.x if lazy is not None else x
+            m = _winograd(src, w, n, h, wd, c, co, x_split, False, st, keep_v, gn=lazy, key=x)
             _lib.call("mvae_winograd_output_transform", m.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), _ptr(gn_part),
                       n, h, wd, co, WINOGRAD_TILE, st)
         return y
@@ -891,6 +940,8 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         dt = ARENA.get("wino_d", 4 * pos * t * co, dev)
         # the forward's V of this x when it was kept (same tile size, x unchanged since), else recomputed
         kept = wino_v is not None and wino_v[1] == mt and wino_v[2] == x.data_ptr() and wino_v[3] == x._version
+        if not kept and getattr(x, GN_LAZY_ATTR, None) is not None:
+            raise RuntimeError("conv2d wgrad: a deferred GroupNorm input needs the forward's kept Winograd transform")
         v = wino_v[0] if kept else ARENA.get("wino_v", 4 * pos * t * c, dev)
         m = ARENA.get("wino_mw", 4 * pos * co * c, dev)
         nbytes = _lib.query("mvae_gemm_workspace_bytes", co, c, t, pos)
@@ -968,23 +1019,27 @@ DYSPLIT_MIN_MACS = 1e11
 
 
 class DyPack:
-    __slots__ = ("bias_ref", "packed", "dx_ptr", "dx_version", "dx_shape", "bias_done", "db", "split")
+    __slots__ = ("bias_ref", "packed", "dx_ref", "dx_version", "dx_shape", "bias_done", "db", "split")
 
     def __init__(self, bias_ref, split: bool = False):
         self.bias_ref = bias_ref
         self.split = split  # False: packed bf16 (bf16-mixed); True: split4_bf16 (3xBF16)
-        self.packed = self.dx_ptr = self.dx_version = self.dx_shape = self.db = None
+        self.packed = self.dx_ref = self.dx_version = self.dx_shape = self.db = None
         self.bias_done = False
 
     def take(self, dy):
         """(packed dy, bias gradient done, returned bias gradient) when the GroupNorm backward produced them from
-        exactly this gradient tensor (same storage, untouched since), else None; consumed once."""
-        packed, ptr, ver, shp = self.packed, self.dx_ptr, self.dx_version, self.dx_shape
+        exactly this gradient tensor (same storage, untouched since), else None; consumed once. The GroupNorm's dx is
+        tracked by a weak reference, not its address: once autograd has summed another branch into a new tensor and
+        freed dx, that address can come back from the allocator for an unrelated dy (a layout copy of the sum) --
+        a stale address match the weak reference rules out."""
+        packed, ref, ver, shp = self.packed, self.dx_ref, self.dx_version, self.dx_shape
         out = (packed, self.bias_done, self.db)
-        self.packed = self.dx_ptr = self.dx_version = self.dx_shape = self.db = None
+        self.packed = self.dx_ref = self.dx_version = self.dx_shape = self.db = None
         self.bias_done = False
-        if packed is None or dy.data_ptr() != ptr or dy._version != ver or tuple(dy.shape) != shp or \
-                not dy.is_contiguous(memory_format=CL):
+        dx = ref() if ref is not None else None
+        if packed is None or dx is None or dy.data_ptr() != dx.data_ptr() or dy._version != ver or \
+                tuple(dy.shape) != shp or not dy.is_contiguous(memory_format=CL):
             return None
         return out
 
@@ -1033,13 +1088,17 @@ class Conv2dFn(torch.autograd.Function):
         _check(x, "conv input")
         xs = bool(getattr(x, XSPLIT_ATTR, False))
         xb16 = bool(getattr(x, BF16_ATTR, False))
+        lazy = getattr(x, GN_LAZY_ATTR, None)
         if (xs or xb16) and not x.is_contiguous(memory_format=CL):
             raise RuntimeError("conv2d: a pre-split / packed input must not be re-laid out")
-        x = nhwc(x)
         w = _krsc(weight)
         res = nhwc(residual) if residual is not None else None
-        keep = [] if WINOGRAD_KEEP_V and weight.requires_grad else None
-        y = conv2d_forward_raw(x, w, bias, res, geom, xs, gn_part, x_bf16=xb16, keep_v=keep)
+        if lazy is not None and not _lazy_wino(lazy, x, w, bias, res, geom, gn_part, weight.requires_grad):
+            x, lazy = lazy.materialize(), None  # (the conv cannot normalize on load: the GroupNorm output is written)
+        if lazy is None:
+            x = nhwc(x)
+        keep = [] if (WINOGRAD_KEEP_V or lazy is not None) and weight.requires_grad else None
+        y = conv2d_forward_raw(x, w, bias, res, geom, xs, gn_part, x_bf16=xb16, keep_v=keep, lazy=lazy)
         ctx.wino_v = keep[0] if keep else None
         ctx.math = _MATH[0]  # the backward GEMMs run in the forward's arithmetic
         ctx.geom = geom
@@ -1246,25 +1305,36 @@ class GnBwdLink:
 class GroupNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool, drop_p: float, seed: int,
-                y_split: bool = False, grad_sink=None, part=None, link=None, dypack=None):
+                y_split: bool = False, grad_sink=None, part=None, link=None, dypack=None, lazy=None):
         _check(x, "group_norm input")
         x = nhwc(x)
         n, c, h, w = x.shape
-        y = torch.empty_like(x, memory_format=CL)
         mean = torch.empty(n * groups, device=x.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
         nbytes = _lib.query("mvae_group_norm_workspace_bytes", n, h * w, c)
         ws = ARENA.get("gn", nbytes, x.device)
-        with _timed("gn_fwd", 8.0 * x.numel(), (n, c, h * w)):  # algorithmic HBM bytes: read x, write y
-            if part is not None:  # statistics from the producing conv's epilogue: no pass over x for them
-                _lib.call("mvae_group_norm_fwd_part_nhwc", x.data_ptr(), part.data_ptr(), gamma.data_ptr(),
-                          beta.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), n, h * w, c, groups,
-                          float(eps), int(silu), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, int(y_split),
-                          ws.data_ptr(), ws.numel(), _stream(x))
-            else:
-                _lib.call("mvae_group_norm_fwd_nhwc", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
-                          mean.data_ptr(), rstd.data_ptr(), n, h * w, c, groups, float(eps), int(silu), float(drop_p),
-                          int(seed) & 0xFFFFFFFFFFFFFFFF, int(y_split), ws.data_ptr(), ws.numel(), _stream(x))
+        if lazy is not None:  # statistics only; the consuming conv's input transform applies them (LazyGn)
+            lazy.x = x
+            lazy.scale = torch.empty(n * c, device=x.device, dtype=torch.float32)
+            lazy.shift = torch.empty_like(lazy.scale)
+            with _timed("gn_fwd", 0.0 if part is not None else 4.0 * x.numel(), (n, c, h * w)):
+                _lib.call("mvae_group_norm_stats_nhwc", x.data_ptr(), _ptr(part), gamma.data_ptr(), beta.data_ptr(),
+                          mean.data_ptr(), rstd.data_ptr(), lazy.scale.data_ptr(), lazy.shift.data_ptr(), n, h * w, c,
+                          groups, float(eps), ws.data_ptr(), ws.numel(), _stream(x))
+            y = torch.full((1,), float("nan"), device=x.device).expand(n, c, h, w)  # (never read on this path)
+        else:
+            y = torch.empty_like(x, memory_format=CL)
+            with _timed("gn_fwd", 8.0 * x.numel(), (n, c, h * w)):  # algorithmic HBM bytes: read x, write y
+                if part is not None:  # statistics from the producing conv's epilogue: no pass over x for them
+                    _lib.call("mvae_group_norm_fwd_part_nhwc", x.data_ptr(), part.data_ptr(), gamma.data_ptr(),
+                              beta.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), n, h * w, c, groups,
+                              float(eps), int(silu), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, int(y_split),
+                              ws.data_ptr(), ws.numel(), _stream(x))
+                else:
+                    _lib.call("mvae_group_norm_fwd_nhwc", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                              y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), n, h * w, c, groups, float(eps),
+                              int(silu), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, int(y_split), ws.data_ptr(),
+                              ws.numel(), _stream(x))
         ctx.save_for_backward(x, gamma, beta, mean, rstd)
         ctx.cfg = (groups, int(silu), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF)
         ctx.gamma_ref, ctx.beta_ref = gamma, beta
@@ -1325,7 +1395,8 @@ class GroupNormFn(torch.autograd.Function):
                           _ptr(db), n, h * w, c, groups, silu, drop_p, seed, ws.data_ptr(), ws.numel(),
                           packed.data_ptr(), _ptr(tgt), float(bbeta), _ptr(cs), cs.numel() if cs is not None else 0,
                           _stream(x))
-                req.packed, req.dx_ptr, req.dx_version, req.dx_shape = packed, dx.data_ptr(), dx._version, tuple(dx.shape)
+                req.packed, req.dx_ref, req.dx_version, req.dx_shape = packed, weakref.ref(dx), dx._version, \
+                    tuple(dx.shape)
                 req.bias_done = tgt is not None
             else:
                 _lib.call("mvae_group_norm_bwd_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
@@ -1335,7 +1406,7 @@ class GroupNormFn(torch.autograd.Function):
             _grad_done(ctx.gamma_ref)
         if ctx.needs_input_grad[2] and db_ret is None:
             _grad_done(ctx.beta_ref)
-        return dx, dg_ret, db_ret, None, None, None, None, None, None, None, None, None, None
+        return dx, dg_ret, db_ret, None, None, None, None, None, None, None, None, None, None, None
 
 
 # Activations handed to a convolution in the pre-split 3xBF16 operand layout carry this attribute
@@ -1365,12 +1436,20 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
             x.shape[1] % groups == 0 and x.is_contiguous(memory_format=CL)
         part = part[0] if ok else None
     link = GnBwdLink(groups, silu) if (for_conv and GN_BWD_FUSED and drop_p == 0.0 and x.requires_grad) else None
+    lazy = None
+    if (WINOGRAD_GN and for_conv and not isinstance(for_conv, bool) and drop_p == 0.0 and not packed and
+            link is None and x.dim() == 4 and _al16(x) and WINOGRAD_WGRAD):
+        n, c, h, w = x.shape
+        if _wino_ok(G3, n, h, w, c, int(for_conv)):  # (the consuming conv is 3x3 / stride 1 / pad 1: for_conv callers)
+            lazy, split = LazyGn(x, silu), 0
     dyp = getattr(x, DYPACK_ATTR, None)
     if dyp is not None:
         delattr(x, DYPACK_ATTR)  # one GroupNorm per conv output
         dyp = dyp[0] if dyp[1] == x._version and x.is_contiguous(memory_format=CL) and _al16(x) else None
-    y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink, part, link, dyp)
-    if split >= 2:
+    y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink, part, link, dyp, lazy)
+    if lazy is not None:
+        setattr(y, GN_LAZY_ATTR, lazy)
+    elif split >= 2:
         setattr(y, BF16_ATTR, True)
     elif split:
         setattr(y, XSPLIT_ATTR, True)

@@ -252,3 +252,93 @@ def test_winograd_kept_input_transform_feeds_weight_gradient(dev, monkeypatch):
     assert (nk, nr) == (1, 2)  # backward: dy's transform only, vs dy's and x's
     assert torch.equal(dwk, dwr) and torch.equal(dxk, dxr)
 
+
+
+def _gn_conv_step(dev, x0, g0, b0, w0, cb0, dy0, groups, monkeypatch, **flags):
+    """GroupNorm(+SiLU) -> 3x3 conv through ops.group_norm(for_conv=...) and ops.conv2d, forward + backward."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    for k, v in flags.items():
+        monkeypatch.setattr(ops, k, v)
+    seen = []
+    orig = _lib.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return orig(name, *args)
+    monkeypatch.setattr(_lib, "call", spy)
+    x = cl(x0, dev).requires_grad_(True)
+    gam, bet = g0.to(dev).requires_grad_(True), b0.to(dev).requires_grad_(True)
+    wt = w0.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    cb = cb0.to(dev).requires_grad_(True)
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
+    h = ops.group_norm(x, gam, bet, groups, 1e-6, silu=True, for_conv=w0.shape[0])
+    y = ops.conv2d(h, wt, cb, geom)
+    y.backward(cl(dy0, dev))
+    torch.cuda.synchronize()
+    monkeypatch.setattr(_lib, "call", orig)
+    return [t.detach().cpu() for t in (y, x.grad, gam.grad, bet.grad, wt.grad, cb.grad)], seen
+
+
+@pytest.mark.parametrize("n,c,co,h,w", [(2, 64, 64, 16, 16), (2, 128, 64, 8, 32), (3, 64, 64, 7, 7)])
+def test_groupnorm_applied_in_winograd_input_transform(dev, monkeypatch, n, c, co, h, w):
+    """GroupNorm+SiLU applied on load by the conv's Winograd input transform (the GroupNorm output never written):
+    output and every gradient against float64 autograd, and against the written-output path within 5e-5 (that path
+    hands the conv the GroupNorm output pre-split into 3xBF16 hi + lo, 2^-17 from the fp32 value, which the F4
+    transform amplifies ~10x)."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(n * c + h)
+    x0 = torch.randn(n, c, h, w, generator=g) * 1.3 + 0.2
+    g0, b0 = torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1
+    w0 = torch.randn(co, c, 3, 3, generator=g) / (3 * c ** 0.5)
+    cb0 = torch.randn(co, generator=g)
+    dy0 = torch.randn(n, co, h, w, generator=g)
+    fused, seen = _gn_conv_step(dev, x0, g0, b0, w0, cb0, dy0, 32, monkeypatch, WINOGRAD_GN=True)
+    assert "mvae_winograd_input_transform_gn" in seen and "mvae_group_norm_stats_nhwc" in seen
+    assert "mvae_group_norm_apply_nhwc" not in seen and "mvae_group_norm_fwd_nhwc" not in seen
+    plain, seen2 = _gn_conv_step(dev, x0, g0, b0, w0, cb0, dy0, 32, monkeypatch, WINOGRAD_GN=False)
+    assert "mvae_winograd_input_transform_gn" not in seen2
+    for a, b in zip(fused, plain):
+        assert rel(a, b) < 5e-5
+    xr = x0.double().requires_grad_()
+    gr, br = g0.double().requires_grad_(), b0.double().requires_grad_()
+    wr, cbr = w0.double().requires_grad_(), cb0.double().requires_grad_()
+    yr = F.conv2d(F.silu(F.group_norm(xr, 32, gr, br, eps=1e-6)), wr, cbr, padding=1)
+    yr.backward(dy0.double())
+    for a, b in zip(fused, (yr, xr.grad, gr.grad, br.grad, wr.grad, cbr.grad)):
+        assert rel(a, b) < CONV_TOL
+
+
+def test_deferred_groupnorm_output_is_written_when_the_conv_cannot_apply_it(dev, monkeypatch):
+    """A deferred GroupNorm output whose conv turns out not to run Winograd (here: switched off between the two
+    calls) is materialized by mvae_group_norm_apply_nhwc and the implicit GEMM runs on it."""
+    import torch.nn.functional as F
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    n, c, co, h, w = 2, 64, 64, 16, 16
+    g = torch.Generator().manual_seed(3)
+    x0 = torch.randn(n, c, h, w, generator=g)
+    g0, b0 = torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1
+    w0 = torch.randn(co, c, 3, 3, generator=g) / (3 * c ** 0.5)
+    monkeypatch.setattr(ops, "WINOGRAD_GN", True)
+    x = cl(x0, dev).requires_grad_(True)
+    gam, bet = g0.to(dev).requires_grad_(True), b0.to(dev).requires_grad_(True)
+    wt = w0.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    hgn = ops.group_norm(x, gam, bet, 32, 1e-6, silu=True, for_conv=co)
+    assert getattr(hgn, ops.GN_LAZY_ATTR, None) is not None
+    monkeypatch.setattr(ops, "WINOGRAD", False)
+    seen = []
+    orig = _lib.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return orig(name, *args)
+    monkeypatch.setattr(_lib, "call", spy)
+    y = ops.conv2d(hgn, wt, None, ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False))
+    y.backward(torch.ones_like(y))
+    torch.cuda.synchronize()
+    monkeypatch.setattr(_lib, "call", orig)
+    assert "mvae_group_norm_apply_nhwc" in seen and "mvae_winograd_gemm" not in seen
+    xr, gr, br, wr = (t.double().requires_grad_() for t in (x0, g0, b0, w0))
+    yr = F.conv2d(F.silu(F.group_norm(xr, 32, gr, br, eps=1e-6)), wr, None, padding=1)
+    yr.backward(torch.ones_like(yr))
+    for a, b in ((y, yr), (x.grad, xr.grad), (wt.grad, wr.grad), (gam.grad, gr.grad)):
+        assert rel(a, b) < CONV_TOL
