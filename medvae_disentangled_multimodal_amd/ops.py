@@ -258,8 +258,9 @@ def _wino_ok(g, n: int, h: int, wd: int, cin: int, cout: int) -> bool:
             cin % 4 == 0 and cout % 4 == 0 and
             min(cin, cout) >= (WINOGRAD_MIN_C_WIDE if wd >= 32 else WINOGRAD_MIN_C) and
             9.0 * n * h * wd * cin * cout >= WINOGRAD_MIN_MACS and
-            # (each transformed operand is addressed through one buffer descriptor: < 4 GiB)
-            (WINOGRAD_TILE + 2) ** 2 * _wino_tiles(n, h, wd) * max(cin, cout) * 4 <= _MAX_DESC_BYTES)
+            # (each transformed operand is addressed through one buffer descriptor, < 4 GiB: batches whose operands
+            # exceed it run in image chunks -- at most WINOGRAD_MAX_CHUNKS)
+            len(_wino_chunks(n, h, wd, max(cin, cout))) <= WINOGRAD_MAX_CHUNKS)
 
 
 _MAX_DESC_BYTES = 0xFFFFFF00  # csrc/gemm_core.h MAX_DESC_BYTES
@@ -272,6 +273,19 @@ def _lazy_wino(lazy, x, w, b, res, g, gn_part, wgrad: bool) -> bool:
     return (_wino_ok(g, n, h, wd, c, w.shape[0]) and _al16(w, lazy.x) and (b is None or _al16(b)) and
             (res is None or _al16(res)) and (gn_part is None or _wino_blocks(h, wd)) and
             (not wgrad or WINOGRAD_WGRAD))
+
+
+WINOGRAD_MAX_CHUNKS = 4
+
+
+def _wino_chunks(n: int, h: int, wd: int, cmax: int):
+    """[(b0, b1)] image ranges whose transformed operands ((m+2)^2 x tiles x channels x 4 B) each fit one 4 GiB buffer
+    descriptor (c4's 64x64x512 decoder conv at B = 256: two halves)."""
+    per_img = (WINOGRAD_TILE + 2) ** 2 * _wino_tiles(1, h, wd) * cmax * 4
+    per = max(1, _MAX_DESC_BYTES // per_img) if per_img <= _MAX_DESC_BYTES else 0
+    if per == 0:
+        return [None] * (WINOGRAD_MAX_CHUNKS + 1)  # (one image alone is too large)
+    return [(b0, min(n, b0 + per)) for b0 in range(0, n, per)]
 
 
 def _wino_blocks(h: int, wd: int) -> bool:
@@ -328,32 +342,35 @@ WINOGRAD_KEEP_V = os.environ.get("MVAE_NO_WINOGRAD_KEEP_V") is None
 
 
 def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split: bool, dgrad: bool, st, keep=None,
-              gn=None, key=None):
-    """U (filters), V (input tiles) and the (m+2)^2 position GEMMs M = V U^T; returns M (arena) for an output
-    transform. keep (a list): V is allocated outside the arena and appended to it (WINOGRAD_KEEP_V), tagged with `key`
-    (the conv's input tensor; default src). gn (LazyGn): src is a GroupNorm input, normalized on load."""
+              gn=None, key=None, u=None, chunk=(0, 0)):
+    """U (filters, unless `u` is given), V (input tiles) and the (m+2)^2 position GEMMs M = V U^T for the n images of
+    src; returns (M (arena), U) for an output transform. keep (a list): V is allocated outside the arena and appended
+    to it (WINOGRAD_KEEP_V), tagged with `key` (the conv's input tensor; default src) and the image range `chunk`.
+    gn (LazyGn): src is a GroupNorm input, normalized on load (its scale / shift rows of these images)."""
     mt = WINOGRAD_TILE
     t = _wino_tiles(n, h, wd)
     pos = (mt + 2) ** 2
     dev = src.device
-    u = ARENA.get("wino_u", 4 * pos * k_in * n_out, dev)
     if keep is not None:
         v = torch.empty(4 * pos * t * k_in, dtype=torch.uint8, device=dev)
         kt = src if key is None else key
-        keep.append((v, mt, kt.data_ptr(), kt._version))
+        keep.append((v, mt, kt.data_ptr(), kt._version, tuple(chunk)))
     else:
         v = ARENA.get("wino_v", 4 * pos * t * k_in, dev)
     m = ARENA.get("wino_m", 4 * pos * t * n_out, dev)
-    cin, cout = (n_out, k_in) if dgrad else (k_in, n_out)
-    _lib.call("mvae_winograd_weight_transform", w.data_ptr(), u.data_ptr(), cin, cout, int(dgrad), mt, st)
+    if u is None:
+        u = ARENA.get("wino_u", 4 * pos * k_in * n_out, dev)
+        cin, cout = (n_out, k_in) if dgrad else (k_in, n_out)
+        _lib.call("mvae_winograd_weight_transform", w.data_ptr(), u.data_ptr(), cin, cout, int(dgrad), mt, st)
     if gn is not None:
-        _lib.call("mvae_winograd_input_transform_gn", src.data_ptr(), gn.scale.data_ptr(), gn.shift.data_ptr(), gn.silu,
-                  v.data_ptr(), n, h, wd, k_in, mt, st)
+        b0 = chunk[0]
+        _lib.call("mvae_winograd_input_transform_gn", src.data_ptr(), gn.scale[b0 * k_in:].data_ptr(),
+                  gn.shift[b0 * k_in:].data_ptr(), gn.silu, v.data_ptr(), n, h, wd, k_in, mt, st)
     else:
         _lib.call("mvae_winograd_input_transform", src.data_ptr(), v.data_ptr(), n, h, wd, k_in, int(src_split), mt,
                   st)
     _lib.call("mvae_winograd_gemm", v.data_ptr(), u.data_ptr(), m.data_ptr(), t, k_in, n_out, mt, st)
-    return m
+    return m, u
 
 
 # Convolutions on DMA-staged operands: the GEMM stages them into LDS by DMA (no staging registers, conversion or
@@ -665,9 +682,14 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
     if wino:
         with _timed("conv_fwd", _wino_alg(ref), (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
             src = lazy.x if lazy is not None else x
-            m = _winograd(src, w, n, h, wd, c, co, x_split, False, st, keep_v, gn=lazy, key=x)
-            _lib.call("mvae_winograd_output_transform", m.data_ptr(), _ptr(b), _ptr(res), y.data_ptr(), _ptr(gn_part),
-                      n, h, wd, co, WINOGRAD_TILE, st)
+            u = None
+            for b0, b1 in _wino_chunks(n, h, wd, max(c, co)):
+                m, u = _winograd(src[b0:b1], w, b1 - b0, h, wd, c, co, x_split, False, st, keep_v, gn=lazy, key=x,
+                                 u=u, chunk=(b0, b1))
+                gp = gn_part[b0 * (h * wd // 32) * (co // 4) * 2:] if gn_part is not None else None
+                _lib.call("mvae_winograd_output_transform", m.data_ptr(), _ptr(b),
+                          _ptr(res[b0:b1] if res is not None else None), y[b0:b1].data_ptr(), _ptr(gp), b1 - b0, h,
+                          wd, co, WINOGRAD_TILE, st)
         return y
     wg = w
     if sub:  # tap-summed per-class weights (prepared outside the timed GEMM launch)
@@ -777,14 +799,20 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
         link = gn_link if gn_link is not None and gn_link.usable(dx) and _wino_blocks(h, wd) else None
         part = torch.empty(n * h * wd // 32 * c * 2, device=dy.device, dtype=torch.float64) if link else None
         with _timed("conv_dgrad", _wino_alg(flops), shp, flops):
-            m = _winograd(dya, w, n, h, wd, co, c, dys is not None, True, st)
-            if link is None:
-                _lib.call("mvae_winograd_output_transform", m.data_ptr(), None, None, dx.data_ptr(), None, n, h, wd, c,
-                          WINOGRAD_TILE, st)
-            else:  # with the GroupNorm backward partials (mvae_conv2d_dgrad_gnbwd_nhwc's epilogue sums)
-                _lib.call("mvae_winograd_output_gnbwd", m.data_ptr(), dx.data_ptr(), link.x.data_ptr(),
-                          link.mean.data_ptr(), link.rstd.data_ptr(), link.gamma.data_ptr(), link.beta.data_ptr(),
-                          link.groups, link.silu, part.data_ptr(), n, h, wd, c, WINOGRAD_TILE, st)
+            u = None
+            for b0, b1 in _wino_chunks(n, h, wd, max(c, co)):
+                nb = b1 - b0
+                m, u = _winograd(dya[b0:b1], w, nb, h, wd, co, c, dys is not None, True, st, u=u)
+                if link is None:
+                    _lib.call("mvae_winograd_output_transform", m.data_ptr(), None, None, dx[b0:b1].data_ptr(), None, nb,
+                              h, wd, c, WINOGRAD_TILE, st)
+                else:  # with the GroupNorm backward partials (mvae_conv2d_dgrad_gnbwd_nhwc's epilogue sums)
+                    L = link
+                    _lib.call("mvae_winograd_output_gnbwd", m.data_ptr(), dx[b0:b1].data_ptr(), L.x[b0:b1].data_ptr(),
+                              L.mean[b0 * L.groups:].data_ptr(), L.rstd[b0 * L.groups:].data_ptr(),
+                              L.gamma.data_ptr(), L.beta.data_ptr(), L.groups, L.silu,
+                              part[b0 * (h * wd // 32) * c * 2:].data_ptr(), nb, h, wd, c, WINOGRAD_TILE, st)
+            if link is not None:
                 link.part, link.dx = part, dx
         return dx
     if gn_link is not None and gn_link.usable(dx) and not g.pointwise and not g.upsample and g.stride == 1 and \
@@ -934,26 +962,34 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         # Winograd F(3x3, 2x2): dW = G^T [sum_tiles (A D A^T) (.) (B^T X B)] G (csrc/winograd.hip); the bias gradient is
         # left to the caller
         mt = WINOGRAD_TILE
-        t = _wino_tiles(n, h, wd)
         pos = (mt + 2) ** 2
         dev = dy.device
-        dt = ARENA.get("wino_d", 4 * pos * t * co, dev)
-        # the forward's V of this x when it was kept (same tile size, x unchanged since), else recomputed
-        kept = wino_v is not None and wino_v[1] == mt and wino_v[2] == x.data_ptr() and wino_v[3] == x._version
-        if not kept and getattr(x, GN_LAZY_ATTR, None) is not None:
-            raise RuntimeError("conv2d wgrad: a deferred GroupNorm input needs the forward's kept Winograd transform")
-        v = wino_v[0] if kept else ARENA.get("wino_v", 4 * pos * t * c, dev)
-        m = ARENA.get("wino_mw", 4 * pos * co * c, dev)
-        nbytes = _lib.query("mvae_gemm_workspace_bytes", co, c, t, pos)
-        ws = ARENA.get("ws", nbytes, dev)
         dya = dys if dys is not None else dy
-        _lib.call("mvae_winograd_dy_transform", dya.data_ptr(), dt.data_ptr(), n, h, wd, co, int(dys is not None), mt,
-                  st)
-        if not kept:
-            _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), n, h, wd, c, int(x_split), mt, st)
-        _lib.call("mvae_winograd_wgrad_gemm", dt.data_ptr(), v.data_ptr(), m.data_ptr(), t, co, c, mt, ws.data_ptr(),
-                  ws.numel(), st)
-        _lib.call("mvae_winograd_wgrad_output", m.data_ptr(), dw.data_ptr(), float(beta), co, c, mt, st)
+        # the forward's V of this x, per image chunk, when it was kept (same tile size, x unchanged since)
+        kept = {}
+        for e in wino_v or ():
+            if e[1] == mt and e[2] == x.data_ptr() and e[3] == x._version:
+                kept[e[4]] = e[0]
+        for i, (b0, b1) in enumerate(_wino_chunks(n, h, wd, max(c, co))):
+            nb, t = b1 - b0, _wino_tiles(b1 - b0, h, wd)
+            v = kept.get((b0, b1))
+            if v is None and getattr(x, GN_LAZY_ATTR, None) is not None:
+                raise RuntimeError("conv2d wgrad: a deferred GroupNorm input needs the forward's kept Winograd "
+                                   "transform")
+            dt = ARENA.get("wino_d", 4 * pos * t * co, dev)
+            m = ARENA.get("wino_mw", 4 * pos * co * c, dev)
+            ws = ARENA.get("ws", _lib.query("mvae_gemm_workspace_bytes", co, c, t, pos), dev)
+            _lib.call("mvae_winograd_dy_transform", dya[b0:b1].data_ptr(), dt.data_ptr(), nb, h, wd, co,
+                      int(dys is not None), mt, st)
+            if v is None:
+                v = ARENA.get("wino_v", 4 * pos * t * c, dev)
+                _lib.call("mvae_winograd_input_transform", x[b0:b1].data_ptr(), v.data_ptr(), nb, h, wd, c,
+                          int(x_split), mt, st)
+            _lib.call("mvae_winograd_wgrad_gemm", dt.data_ptr(), v.data_ptr(), m.data_ptr(), t, co, c, mt,
+                      ws.data_ptr(), ws.numel(), st)
+            # (image chunks accumulate: the first with the caller's beta, the rest onto it)
+            _lib.call("mvae_winograd_wgrad_output", m.data_ptr(), dw.data_ptr(), float(beta) if i == 0 else 1.0, co, c,
+                      mt, st)
         return False
     nbytes = _lib.query("mvae_conv2d_wgrad_workspace_bytes", n, c, co, g.kh, g.kw, ho, wo)
     ws = ARENA.get("ws", nbytes, dy.device)
@@ -1099,7 +1135,7 @@ class Conv2dFn(torch.autograd.Function):
             x = nhwc(x)
         keep = [] if (WINOGRAD_KEEP_V or lazy is not None) and weight.requires_grad else None
         y = conv2d_forward_raw(x, w, bias, res, geom, xs, gn_part, x_bf16=xb16, keep_v=keep, lazy=lazy)
-        ctx.wino_v = keep[0] if keep else None
+        ctx.wino_v = keep if keep else None
         ctx.math = _MATH[0]  # the backward GEMMs run in the forward's arithmetic
         ctx.geom = geom
         ctx.x_split = xs

@@ -342,3 +342,36 @@ def test_deferred_groupnorm_output_is_written_when_the_conv_cannot_apply_it(dev,
     yr.backward(torch.ones_like(yr))
     for a, b in ((y, yr), (x.grad, xr.grad), (wt.grad, wr.grad), (gam.grad, gr.grad)):
         assert rel(a, b) < CONV_TOL
+
+
+def test_winograd_image_chunks(dev, monkeypatch, _wino_on):
+    """A batch whose transformed operands exceed one buffer descriptor runs in image chunks (here forced by a small
+    limit: 5 images in chunks of 2 / 2 / 1): forward with bias, residual and statistics, input gradient, and the weight
+    gradient accumulated over the chunks from the kept per-chunk transforms, against float64."""
+    import torch.nn.functional as F
+    from medvae_disentangled_multimodal_amd import ops
+    n, c, co, h, w = 5, 64, 32, 8, 16
+    per_img = (_wino_on + 2) ** 2 * ops._wino_tiles(1, h, w) * c * 4
+    monkeypatch.setattr(ops, "_MAX_DESC_BYTES", 2 * per_img)
+    assert ops._wino_chunks(n, h, w, c) == [(0, 2), (2, 4), (4, 5)]
+    g = torch.Generator().manual_seed(21)
+    x0 = torch.randn(n, c, h, w, generator=g)
+    w0 = torch.randn(co, c, 3, 3, generator=g) / (3 * c ** 0.5)
+    b0 = torch.randn(co, generator=g)
+    r0 = torch.randn(n, co, h, w, generator=g)
+    dy0 = torch.randn(n, co, h, w, generator=g)
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
+    x = cl(x0, dev).requires_grad_(True)
+    wt = w0.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    b = b0.to(dev).requires_grad_(True)
+    y = ops.conv2d(x, wt, b, geom, residual=cl(r0, dev), gn_stats=True)
+    part = getattr(y, ops.GN_PART_ATTR)[0]
+    y.backward(cl(dy0, dev))
+    torch.cuda.synchronize()
+    xr, wr, br = (t.double().requires_grad_() for t in (x0, w0, b0))
+    yr = F.conv2d(xr, wr, br, padding=1) + r0.double()
+    yr.backward(dy0.double())
+    assert rel(y, yr) < CONV_TOL
+    assert rel(part, _stats64(y.detach().double().cpu())) < 1e-9
+    for a, ref in ((x.grad, xr.grad), (wt.grad, wr.grad), (b.grad, br.grad)):
+        assert rel(a, ref) < CONV_TOL

@@ -27,7 +27,7 @@ def test_c4_levels(rules):
     assert ops._wino_ok(G3, 256, 32, 32, 512, 512)
     assert ops._wino_ok(G3, 256, 32, 32, 1024, 512)
     assert ops._wino_ok(G3, 256, 64, 64, 256, 256)
-    assert not ops._wino_ok(G3, 256, 64, 64, 512, 256)        # 36 x 65,536 x 512 x 4 B > 4 GiB
+    assert ops._wino_ok(G3, 256, 64, 64, 512, 256)            # 36 x 65,536 x 512 x 4 B > 4 GiB: two image chunks
     assert not ops._wino_ok(G3, 256, 32, 32, 128, 512)        # 128 input channels
     assert not ops._wino_ok(G3, 256, 14, 14, 256, 256)        # narrow images need 512 channels
     assert not ops._wino_ok(G3, 64, 128, 128, 256, 256)       # width above MAX_W
@@ -45,12 +45,16 @@ def test_small_batches_and_math_modes(rules):
     assert not ops._wino_ok(G3, 256, 8, 8, 2048, 2048)
 
 
-def test_size_rule_keeps_operands_under_4gib(rules):
-    """A conv whose transformed operand would exceed one buffer descriptor stays on the implicit GEMM (the 64x64x512
-    decoder conv at B = 256: 36 x 65,536 tiles x 512 channels x 4 B = 4.8 GB) instead of failing in the library."""
-    assert ops._wino_ok(G3, 256, 64, 64, 256, 256)
-    assert not ops._wino_ok(G3, 256, 64, 64, 512, 256)
-    assert not ops._wino_ok(G3, 2048, 32, 32, 512, 512)       # c4's 32x32 level at B = 2048
+def test_size_rule_chunks_operands_under_4gib(rules):
+    """Transformed operands over one 4 GiB buffer descriptor run in image chunks (the 64x64x512 decoder conv at B = 256:
+    36 x 65,536 tiles x 512 channels x 4 B = 4.8 GB -> two halves); more than WINOGRAD_MAX_CHUNKS chunks stay on the
+    implicit GEMM."""
+    assert ops._wino_chunks(256, 64, 64, 256) == [(0, 256)]
+    chunks = ops._wino_chunks(256, 64, 64, 512)
+    assert len(chunks) == 2 and chunks[0][0] == 0 and chunks[-1][1] == 256
+    assert all(36 * ops._wino_tiles(b1 - b0, 64, 64) * 512 * 4 <= ops._MAX_DESC_BYTES for b0, b1 in chunks)
+    assert ops._wino_ok(G3, 1024, 32, 32, 512, 512)           # c4's 32x32 level at B = 1024: 2 chunks
+    assert not ops._wino_ok(G3, 2048, 64, 64, 512, 256)       # 10 chunks
 
 
 def test_block_geometry_and_flop_accounting(rules):
