@@ -100,7 +100,7 @@ def _pmc_traffic(config, family="gemm"):
     committed PMC passes (tools/gpu_evidence.sh traffic: FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc, separate passes) --
     counters cannot be read inside this timed run, so the profile of the same command is attached (newest round
     first)."""
-    for tag in ("r04", "r03", "r02", "r01"):
+    for tag in ("r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", f"{tag}_{config}_{family}_traffic.json")
         if os.path.exists(path):
             break
@@ -261,12 +261,20 @@ def _roofline(rec_all, bf16, config, step_ms, detail, rank, exact=False):
     ach = tot_fl / (tot_ms * 1e-3) / 1e12
     alg_bytes = sum(gemm_algorithmic_bytes(r[0], r[4]) for r in rec) / max(len(rec), 1)
     peak = BF16_DENSE_PEAK_TF if bf16 else FP32_MFMA_PEAK_TF if exact else PEAK_3XBF16_TF
-    pmc = _pmc_traffic(config)
+    # HBM traffic of every kernel the timed passes launch (implicit GEMM, reducers, Winograd transforms, attention):
+    # the PMC bytes of one step over the passes of one step, so `traffic` and `algorithmic_bytes_per_launch` are per
+    # timed pass alike (older rounds: gemm3x_kernel launches only)
+    pmc = _pmc_traffic(config, "mfma")
+    if pmc is not None and rec:
+        pmc["bytes_per_launch"] = round(pmc["total_bytes_per_step"] / len(rec))
+        pmc["unit_note"] = "HBM bytes per timed pass (PMC family bytes per step / passes per step)"
+    else:
+        pmc = _pmc_traffic(config)
     roofline = {"bound": "mfma", "kernel": ("gemm3x_kernel (implicit-GEMM conv, Winograd position GEMMs with their "
                                             "transforms, attention bmm; all launches)"),
                 "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(ach / peak, 4), "traffic": (pmc or {}).get("bytes_per_launch"),
-                "traffic_unit": "HBM bytes per launch (PMC)", "traffic_detail": pmc,
+                "traffic_unit": (pmc or {}).get("unit_note", "HBM bytes per gemm3x launch (PMC)"), "traffic_detail": pmc,
                 "algorithmic_bytes_per_launch": round(alg_bytes),
                 "peak_note": ("bf16 dense MFMA peak 2.5 PF/s (bf16 operands, fp32 accumulate)" if bf16 else
                               "exact fp32: dense f32-input MFMA peak 157.3 TF/s" if exact else

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Recompute a bench line's GEMM-family roofline fraction from a rocprofv3 per-step kernel table.
 
-    python3 tools/frac_from_prof.py <bench_detail.json> <prof_<cfg>_per_step.txt> [--peak TFLOPS]
+    python3 tools/frac_from_prof.py <bench_detail.json> <prof_<cfg>_per_step.txt> [--peak TFLOPS] [--config CFG]
+
+(--config: a config of the detail file's `configs` block -- c1, c2, c3, c5, c4x -- instead of the headline c4.)
 
 The bench's `by_pass` entries carry each pass's algorithmic FLOPs per step (TF/s x ms); the rocprof table (tools/
 prof_diff.py output: ms/step per kernel over replayed steps) gives the device time of the kernels those passes launch
@@ -20,6 +22,8 @@ def main():
     detail, table = sys.argv[1], sys.argv[2]
     peak = float(sys.argv[sys.argv.index("--peak") + 1]) if "--peak" in sys.argv else None
     d = json.load(open(detail))
+    if "--config" in sys.argv:
+        d = d["configs"][sys.argv[sys.argv.index("--config") + 1]]
     r = d["roofline"]
     peak = peak or float(r["peak"])
     flops = sum(p["TFLOP/s"] * p["ms"] * 1e9 for p in r["by_pass"].values())

@@ -9,7 +9,7 @@
 #   tools/gpu_evidence.sh perstep  <tag> <config> [S1 S2]         per-step rocprofv3 kernel table: two --kernel-trace
 #                                                                 --stats runs differing in timed steps, differenced
 #                                                                 by tools/prof_diff.py (set-up / warmup cancel)
-#   tools/gpu_evidence.sh traffic  <tag> <config> [family]        HBM bytes of a kernel family (gemm | gn | loss)
+#   tools/gpu_evidence.sh traffic  <tag> <config> [family]        HBM bytes of a kernel family (gemm | mfma | gn | loss)
 #                                                                 over one step: FETCH_SIZE and WRITE_SIZE in separate
 #                                                                 --pmc passes, gfx950 correction in pmc_traffic.py
 #   tools/gpu_evidence.sh pmc      <tag> <shape> <pass> <prec>    conv counter sets (MFMA busy, waits, VALU / SALU /
@@ -70,8 +70,8 @@ perstep() {
 
 traffic() {
   local cfg=$1 fam=${2:-gemm} re
-  case $fam in gemm) re=gemm3x;; gn) re=gn_;; loss) re="reparam_|reduce_partial|reduce_final|kl_bwd|recon_bwd";;
-    *) echo "family: gemm | gn | loss"; return 2;; esac
+  case $fam in gemm) re=gemm3x;; gn) re=gn_;; mfma) re=$(python3 -c "import sys; sys.path.insert(0, 'tools'); from frac_from_prof import FAMILY; print(FAMILY.pattern)");; loss) re="reparam_|reduce_partial|reduce_final|kl_bwd|recon_bwd";;
+    *) echo "family: gemm | mfma | gn | loss"; return 2;; esac
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 400 rocprofv3 --pmc $c --kernel-include-regex "$re" -d gpurun_out/traffic_${cfg}_${fam}_$c -o run \
       --output-format csv -- python3 bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline \

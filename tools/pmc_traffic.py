@@ -1,15 +1,19 @@
 #!/usr/bin/env python3
-"""Per-launch HBM bytes of a kernel family (gemm: gemm3x_kernel; gn: the gn_* GroupNorm chains; loss: the
+"""Per-launch HBM bytes of a kernel family (gemm: gemm3x_kernel; mfma: every kernel of the bench's MFMA-roofline passes --
+implicit GEMM, split-K reducers, Winograd transforms, attention; gn: the gn_* GroupNorm chains; loss: the
 reparameterization / KL / reconstruction kernels) from the FETCH_SIZE /
 WRITE_SIZE passes of tools/gpu_evidence.sh traffic.
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts 64 B per 128-B request of
 wide streaming reads -> x2; WRITE_SIZE is exact for 16-B/lane stores. Both are reported in KB."""
 import csv, glob, json, os, re, sys
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from frac_from_prof import FAMILY as MFMA_FAMILY  # noqa: E402  (the kernels of the bench's MFMA-roofline passes)
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c4"
 tag = sys.argv[2] if len(sys.argv) > 2 else "r02"
 short = sys.argv[3] if len(sys.argv) > 3 else "gemm"  # family: gemm | gn | loss
-FAMILY_RE = {"gemm": "gemm3x", "gn": "gn_", "loss": "reparam_|reduce_partial|reduce_final|kl_bwd|recon_bwd"}
+FAMILY_RE = {"gemm": "gemm3x", "mfma": MFMA_FAMILY.pattern, "gn": "gn_",
+             "loss": "reparam_|reduce_partial|reduce_final|kl_bwd|recon_bwd"}
 fam = FAMILY_RE[short]
 root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 
@@ -28,7 +32,8 @@ fetch, write = per_dispatch("FETCH_SIZE"), per_dispatch("WRITE_SIZE")
 n = len(fetch)
 fb = 2.0 * 1024 * sum(fetch.values()) / max(n, 1)
 wb = 1024 * sum(write.values()) / max(len(write), 1)
-kname = {"gemm": "gemm3x_kernel", "gn": "gn_* (GroupNorm chains)"}.get(short, f"loss family ({fam})")
+kname = {"gemm": "gemm3x_kernel", "mfma": f"MFMA-roofline family ({fam})",
+         "gn": "gn_* (GroupNorm chains)"}.get(short, f"loss family ({fam})")
 out = {"config": cfg, "kernel": kname, "launches": n, "fetch_bytes_per_launch": fb,
        "write_bytes_per_launch": wb, "traffic_bytes_per_launch": fb + wb,
        "traffic_bytes_total": 2.0 * 1024 * sum(fetch.values()) + 1024 * sum(write.values()), "steps": 1,
