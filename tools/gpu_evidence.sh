@@ -14,6 +14,8 @@
 #                                                                 --pmc passes, gfx950 correction in pmc_traffic.py
 #   tools/gpu_evidence.sh pmc      <tag> <shape> <pass> <prec>    conv counter sets (MFMA busy, waits, VALU / SALU /
 #                                                                 LDS issue) of one tools/conv_bench.py shape + pass
+#   tools/gpu_evidence.sh pmcrun   <tag> <name> <regex> <cmd...>  the same counter sets over any program (the kernels
+#                                                                 matching regex; settings through exported env vars)
 #   tools/gpu_evidence.sh ab       <tag> <config> <variant...>    interleaved A/B of library builds variants/<v>/
 #                                                                 (tools/build_variant.sh), "default" (in-tree) or
 #                                                                 "env:VAR=VAL[,...]" (in-tree under those settings)
@@ -98,6 +100,17 @@ pmc() {
   python3 tools/pmc_summary.py "$OUT/s${shape}_${pass}_${prec}_*/**/*counter_collection.csv"
 }
 
+pmcrun() {
+  local name=$1 re=$2 i=0; shift 2
+  for set in "${PMC_SETS[@]}"; do
+    timeout -s KILL 120 rocprofv3 --pmc $set --kernel-include-regex "$re" -d $OUT/${name}_$i -o run --output-format csv \
+      -- "$@" > $OUT/${name}_$i.log 2>&1 || return $?
+    i=$((i + 1))
+  done
+  echo "== $name"
+  python3 tools/pmc_summary.py "$OUT/${name}_*/**/*counter_collection.csv"
+}
+
 ab() {
   local cfg=$1; shift
   for r in 1 2; do
@@ -136,6 +149,7 @@ case $CMD in
   perstep) perstep "$@" ;;
   traffic) traffic "$@" ;;
   pmc) pmc "$@" ;;
+  pmcrun) pmcrun "$@" ;;
   ab) ab "$@" ;;
   loops) loops "$@" ;;
   final) suite && bench && perstep c3 && perstep c4 ;;

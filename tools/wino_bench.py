@@ -2,7 +2,8 @@
 """Time each Winograd F(m x m, 3x3) C-ABI stage on the c4 level shapes (HIP events on the current stream): the
 transforms against the HBM roofline (algorithmic bytes: every operand read once, every output written once), the
 position GEMMs in executed TF/s.
-usage: tools/wino_bench.py [reps] [tile]"""
+usage: tools/wino_bench.py [reps] [tile]
+env WB_SHAPES=i,j (indices into SHAPES) and WB_STAGES=gemm,wgemm restrict the run (PMC passes over one kernel)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -15,6 +16,9 @@ POS = (MT + 2) ** 2
 ops.set_precision("32")  # 3xBF16 (the Winograd path's arithmetic)
 SHAPES = [(256, 8, 8, 2048, 2048), (256, 16, 16, 1024, 1024), (256, 32, 32, 512, 512), (128, 64, 64, 256, 256),
           (128, 64, 64, 512, 256)]
+if os.environ.get("WB_SHAPES"):
+    SHAPES = [SHAPES[int(i)] for i in os.environ["WB_SHAPES"].split(",")]
+ONLY = set(os.environ["WB_STAGES"].split(",")) if os.environ.get("WB_STAGES") else None
 st = torch.cuda.current_stream().cuda_stream
 
 
@@ -61,6 +65,8 @@ for nb, h, w, ci, co in SHAPES:
     ]
     row = []
     for name, fn, nbytes, flops in stages:
+        if ONLY and name not in ONLY and not (name == "in" and "wgemm" in ONLY) and not (name == "dy" and "wgemm" in ONLY):
+            continue
         us = timed(fn)
         tot[name] = tot.get(name, 0.0) + us
         rate = f"{flops / us / 1e6:6.1f}TF/s" if flops else f"{nbytes / us / 1e6:5.2f}TB/s"
