@@ -15,7 +15,8 @@ MT = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 POS = (MT + 2) ** 2
 ops.set_precision("32")  # 3xBF16 (the Winograd path's arithmetic)
 SHAPES = [(256, 8, 8, 2048, 2048), (256, 16, 16, 1024, 1024), (256, 32, 32, 512, 512), (128, 64, 64, 256, 256),
-          (128, 64, 64, 512, 256)]
+          (128, 64, 64, 512, 256),
+          (256, 7, 7, 512, 512), (256, 14, 14, 256, 256), (256, 28, 28, 128, 128)]  # c2 levels (WB_SHAPES=5,6,7)
 if os.environ.get("WB_SHAPES"):
     SHAPES = [SHAPES[int(i)] for i in os.environ["WB_SHAPES"].split(",")]
 ONLY = set(os.environ["WB_STAGES"].split(",")) if os.environ.get("WB_STAGES") else None
@@ -45,12 +46,16 @@ for nb, h, w, ci, co in SHAPES:
     m = torch.empty(POS * t * co, device=dev)
     mw = torch.empty(POS * ci * co, device=dev)
     dw = torch.empty_like(wt)
+    sc = torch.rand(nb, ci, device=dev) + 0.5  # GroupNorm scale / shift rows (input transform with GroupNorm+SiLU)
+    sh = torch.randn(nb, ci, device=dev) * 0.1
     ws = torch.empty(_lib.query("mvae_gemm_workspace_bytes", co, ci, t, POS), dtype=torch.uint8, device=dev)
     stages = [
         ("wt_fwd", lambda: _lib.call("mvae_winograd_weight_transform", wt.data_ptr(), u.data_ptr(), ci, co, 0, MT, st),
          4.0 * co * ci * (9 + POS), 0),
         ("in", lambda: _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), nb, h, w, ci, 0, MT, st),
          4.0 * (x.numel() + POS * t * ci), 0),
+        ("in_gn", lambda: _lib.call("mvae_winograd_input_transform_gn", x.data_ptr(), sc.data_ptr(), sh.data_ptr(), 1,
+                                    v.data_ptr(), nb, h, w, ci, MT, st), 4.0 * (x.numel() + POS * t * ci), 0),
         ("gemm", lambda: _lib.call("mvae_winograd_gemm", v.data_ptr(), u.data_ptr(), m.data_ptr(), t, ci, co, MT, st),
          4.0 * POS * (t * ci + ci * co + t * co), 2.0 * POS * t * ci * co),
         ("out", lambda: _lib.call("mvae_winograd_output_transform", m.data_ptr(), None, None, y.data_ptr(), None, nb, h,
@@ -72,6 +77,6 @@ for nb, h, w, ci, co in SHAPES:
         rate = f"{flops / us / 1e6:6.1f}TF/s" if flops else f"{nbytes / us / 1e6:5.2f}TB/s"
         row.append(f"{name} {us:7.1f}us {rate}")
     print((nb, h, w, ci, co), " | ".join(row), flush=True)
-    del x, dy, y, wt, u, v, d, m, mw, dw, ws
+    del x, dy, y, wt, u, v, d, m, mw, dw, ws, sc, sh
     torch.cuda.empty_cache()
 print("total us:", {k: round(v, 1) for k, v in tot.items()})
