@@ -126,6 +126,28 @@ int mvae_conv2d_dgrad_gnbwd_nhwc(const float* dy, const float* wt, float* dx, in
 
 }  // extern "C"
 
+// Wave-quantization tail: a conv GEMM whose tiles fill k whole rounds of the chip's resident slots (256 CUs x tiles
+// per CU) plus a sliver of one more runs that last round on a few CUs for a whole tile time -- c2's 28x28x128 passes
+// at B = 256 are 784 tiles of 256x128 = 3.06 rounds, measured 250 us against 190 us at B = 250 (tools/quant_probe.py).
+// Such a batch is launched as the images that fit the k rounds, then the remaining images on their own (the cost model
+// gives them small tiles spread over the chip). Returns the image count of the first launch (nb: no split).
+// MVAE_NO_TAIL_SPLIT=1 turns it off.
+static int tail_split_images(int nb, long long hw, int n_cols, int k, bool v) {
+  static const bool off = getenv("MVAE_NO_TAIL_SPLIT") != nullptr;
+  if (off || nb < 2) return nb;
+  GemmArgs t{};
+  t.M = (int)std::min<long long>((long long)nb * hw, 1LL << 30); t.N = n_cols; t.K = k; t.batch = 1;
+  const int cfg = choose_tile(t, v, false);
+  if (cfg < T256x256 || cfg > T64x64) return nb;
+  static const int res[5] = {1, 1, 1, 2, 4}, bm[5] = {256, 256, 128, 128, 64}, bn[5] = {256, 128, 256, 128, 64};
+  const long long slots = 256LL * res[cfg], tiles = tiles_of(cfg, t);
+  const long long full = tiles / slots, rem = tiles - full * slots;
+  if (full < 1 || rem == 0 || rem * 2 >= slots) return nb;
+  const long long tn = (n_cols + bn[cfg] - 1) / bn[cfg];
+  const long long nm = (full * slots / tn) * bm[cfg] / hw;
+  return (nm >= 1 && nm < nb) ? (int)nm : nb;
+}
+
 static int conv2d_impl(const float* x, const float* w, const float* bias, const float* residual, float* y, int nb,
                        int h, int wd, int cin, int cout, int kh, int kw, int stride, int pad_t, int pad_l, int ho,
                        int wo, int mode, double* gn_part, void* stream, const GnBwdLink* gnb, float* ws,
@@ -170,8 +192,10 @@ static int conv2d_impl(const float* x, const float* w, const float* bias, const 
   }
   int shift = 0;
   while ((1 << shift) < stride) ++shift;
-  for (int b0 = 0; b0 < nb; b0 += chunk) {
-    const int n = std::min(chunk, nb - b0);
+  const int n_main = (!bf && nb <= chunk) ? tail_split_images(nb, (long long)ho * wo, cout, kh * kw * cin, v) : nb;
+  for (int b0 = 0, n_ = 0; b0 < nb; b0 += n_) {
+    n_ = (b0 == 0 && n_main < nb) ? n_main : std::min(chunk, nb - b0);
+    const int n = n_;
     GemmArgs a{};
     a.M = n * ho * wo; a.N = cout; a.K = kh * kw * cin; a.batch = 1; a.splits = 1; a.k_split = a.K;
     a.A = bf ? (const float*)((const __bf16*)x + (long long)b0 * (in_img / 4)) : x + (long long)b0 * (in_img / 4);

@@ -129,7 +129,7 @@ struct WinoGn {
   int silu;
 };
 
-template <int MT, bool XS, bool GN = false>
+template <int MT, bool XS, int GN = 0>  // GN: 0 none, 1 GroupNorm affine on load, 2 affine + SiLU
 __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ x, uint4* __restrict__ v, int nb, int H,
                                                       int W, int C, WinoGn gn) {
   constexpr int AL = MT + 2;
@@ -146,11 +146,6 @@ __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ 
   const unsigned cb = (unsigned)c4 * 16u;
   const unsigned plane = (unsigned)(T * C4 * 16), base = (unsigned)(t * C4 + c4) * 16u;
   const __amdgpu_buffer_rsrc_t vr = make_rsrc(v, plane * (unsigned)(AL * AL));
-  float4 sc{1.f, 1.f, 1.f, 1.f}, sh{0.f, 0.f, 0.f, 0.f};
-  if constexpr (GN) {
-    sc = *(const float4*)(gn.scale + (long long)b * C + c4 * 4);
-    sh = *(const float4*)(gn.shift + (long long)b * C + c4 * 4);
-  }
   float4 d[AL][AL];
 #pragma unroll
   for (int i = 0; i < AL; ++i)
@@ -159,19 +154,30 @@ __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ 
       const int h = MT * ti - 1 + i, w = MT * tj - 1 + j;
       const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
       const float4 r = bload4(xr, ok ? ((unsigned)((b * H + h) * W + w) * (unsigned)C) * 4u + cb : OOB);
-      if constexpr (GN) {
-        float o[4] = {r.x * sc.x + sh.x, r.y * sc.y + sh.y, r.z * sc.z + sh.z, r.w * sc.w + sh.w};
-        // SiLU with the hardware reciprocal (1 ulp) instead of an IEEE division: each element is normalized once per
-        // patch that covers it (~2.25x at m = 4), so the division's ~10 instructions per element made this kernel
-        // VALU-bound (measured: the fused form lost 0.9 % on c4 with sigmoid_f)
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (gn.silu) o[k] = o[k] * __builtin_amdgcn_rcpf(1.f + __expf(-o[k]));
-        d[i][j] = ok ? float4{o[0], o[1], o[2], o[3]} : float4{0.f, 0.f, 0.f, 0.f};
-      } else {
-        d[i][j] = XS ? split4_to_f32(r) : r;
-      }
+      d[i][j] = XS ? split4_to_f32(r) : r;
     }
+  if constexpr (GN != 0) {
+    // normalized after all 36 loads are in flight, in branch-free code (SiLU a template choice: a per-element branch
+    // on a runtime flag split the load sequence into one load-wait-compute chain per element, 1.7x the plain
+    // transform's time); the hardware reciprocal (1 ulp) instead of an IEEE division. Padding stays zero (it pads
+    // the normalized output).
+    const float4 sc = *(const float4*)(gn.scale + (long long)b * C + c4 * 4);
+    const float4 sh = *(const float4*)(gn.shift + (long long)b * C + c4 * 4);
+#pragma unroll
+    for (int i = 0; i < AL; ++i)
+#pragma unroll
+      for (int j = 0; j < AL; ++j) {
+        const int h = MT * ti - 1 + i, w = MT * tj - 1 + j;
+        const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        float o[4] = {fmaf(d[i][j].x, sc.x, sh.x), fmaf(d[i][j].y, sc.y, sh.y), fmaf(d[i][j].z, sc.z, sh.z),
+                      fmaf(d[i][j].w, sc.w, sh.w)};
+        if constexpr (GN == 2) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) o[k] = o[k] * __builtin_amdgcn_rcpf(1.f + __expf(-o[k]));
+        }
+        d[i][j] = ok ? float4{o[0], o[1], o[2], o[3]} : float4{0.f, 0.f, 0.f, 0.f};
+      }
+  }
   constexpr auto bt = [](int i, int k) { return wino_bt<MT>(i, k); };
 #pragma unroll
   for (int j = 0; j < AL; ++j) wlin<AL, AL>(&d[0][j], AL, &d[0][j], AL, bt);  // columns: B^T d
@@ -627,10 +633,13 @@ int mvae_winograd_input_transform_gn(const float* x, const float* scale, const f
   hipStream_t st = (hipStream_t)stream;
   const dim3 g(egrid256(wino_tiles(nb, h, w, tile) * (c / 4)));
   const WinoGn gn{scale, shift, silu};
-  if (tile == 2)
-    hipLaunchKernelGGL((wino_in_kernel<2, false, true>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, gn);
-  else
-    hipLaunchKernelGGL((wino_in_kernel<4, false, true>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, gn);
+  if (tile == 2) {
+    if (silu) hipLaunchKernelGGL((wino_in_kernel<2, false, 2>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, gn);
+    else hipLaunchKernelGGL((wino_in_kernel<2, false, 1>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, gn);
+  } else {
+    if (silu) hipLaunchKernelGGL((wino_in_kernel<4, false, 2>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, gn);
+    else hipLaunchKernelGGL((wino_in_kernel<4, false, 1>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, gn);
+  }
   return launch_status();
 }
 

@@ -303,10 +303,11 @@ WINOGRAD_WGRAD = os.environ.get("MVAE_NO_WINOGRAD_WGRAD") is None
 # the normalization on load (mvae_winograd_input_transform_gn), so the GroupNorm output is never written or read
 # (SURVEY §7 hard part 4 / VERDICT r4 item 3 on the Winograd form, which reads its input once). The output handed to the
 # conv is a deferred placeholder: an expanded NaN scalar carrying GN_LAZY_ATTR, never materialized on this path.
-# Opt-in (MVAE_WINOGRAD_GN=1): measured on c4 (same box, interleaved) the GroupNorm family drops 40.5 -> 32.7 ms per
-# step but the input transforms, now normalizing every patch element (~2.25 loads per element) from the GroupNorm's
-# input instead of reading the just-written output, take ~10 ms longer: 689 -> 686 img/s (profiles/r05_winograd_gn_ab.txt)
-WINOGRAD_GN = os.environ.get("MVAE_WINOGRAD_GN") is not None
+# Default since the transform normalizes in branch-free code after its 36 loads (the first build branched on the SiLU
+# flag per element, which serialized the loads: 1.7x the plain transform's time, c4 -0.4 %); now the fused transform
+# runs at the plain one's speed and c4 gains 2 % (704-706 -> 717-721 img/s, GroupNorm family 40.5 -> 31.9 ms; same box,
+# interleaved, profiles/r05_winograd_gn_ab.txt). MVAE_NO_WINOGRAD_GN=1 writes the GroupNorm output as before.
+WINOGRAD_GN = os.environ.get("MVAE_NO_WINOGRAD_GN") is None
 GN_LAZY_ATTR = "_mvae_gn_lazy"
 G3 = ConvGeom(3, 3, 1, 1, 1, 1, 1, False)  # the GroupNorm-fed convs' geometry (ResnetBlock conv1 / conv2, conv_out)
 
