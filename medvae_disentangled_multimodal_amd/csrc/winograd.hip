@@ -664,7 +664,30 @@ int mvae_winograd_gemm(const void* v, const void* u, float* m, long long tiles, 
   a.c_bytes = (unsigned)(tiles * n_out * 4);
   set_splits(a, 1);
   const int cfg = choose_tile(a, true, false);
+  // wave-quantization tail (as conv2d_impl's): positions whose tiles would leave a nearly empty last round (c2's 7x7x512
+  // level: 16 tiles of 256x128 per position x 36 = 2.25 rounds) go in a second launch the cost model tiles finely
+  static const bool no_tail = getenv("MVAE_NO_TAIL_SPLIT") != nullptr;
+  static const int res[5] = {1, 1, 1, 2, 4};
+  int b_main = a.batch;
+  if (!no_tail && cfg >= T256x256 && cfg <= T64x64) {
+    GemmArgs one = a;
+    one.batch = 1;
+    const long long tp = tiles_of(cfg, one), slots = 256LL * res[cfg], tot = tp * a.batch;
+    const long long full = tot / slots, rem = tot - full * slots;
+    if (full >= 1 && rem > 0 && rem * 2 < slots) b_main = (int)std::max<long long>(1, full * slots / tp);
+  }
+  if (b_main >= a.batch) {
+    launch_big<A_ROWK_SPLIT, 4, B_ROWK_SPLIT, 4>(a, (hipStream_t)stream, cfg);
+    return launch_status();
+  }
+  GemmArgs t = a;
+  a.batch = b_main;
   launch_big<A_ROWK_SPLIT, 4, B_ROWK_SPLIT, 4>(a, (hipStream_t)stream, cfg);
+  t.batch -= b_main;
+  t.A += (long long)b_main * t.sA;
+  t.B += (long long)b_main * t.sB;
+  t.C += (long long)b_main * t.sC;
+  launch_big<A_ROWK_SPLIT, 4, B_ROWK_SPLIT, 4>(t, (hipStream_t)stream, choose_tile(t, true, false));
   return launch_status();
 }
 
