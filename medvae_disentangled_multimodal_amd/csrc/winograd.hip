@@ -674,7 +674,8 @@ int mvae_winograd_gemm(const void* v, const void* u, float* m, long long tiles, 
     one.batch = 1;
     const long long tp = tiles_of(cfg, one), slots = 256LL * res[cfg], tot = tp * a.batch;
     const long long full = tot / slots, rem = tot - full * slots;
-    if (full >= 1 && rem > 0 && rem * 2 < slots) b_main = (int)std::max<long long>(1, full * slots / tp);
+    // (up to half a round: c4's 8x8x2048 level is 32 tiles x 36 = 4.5 rounds of 256x256)
+    if (full >= 1 && rem > 0 && rem * 2 <= slots) b_main = (int)std::max<long long>(1, full * slots / tp);
   }
   if (b_main >= a.batch) {
     launch_big<A_ROWK_SPLIT, 4, B_ROWK_SPLIT, 4>(a, (hipStream_t)stream, cfg);
