@@ -200,6 +200,11 @@ int mvae_winograd_output_gnbwd(const float* m, float* dx, const float* x, const 
                                int w, int n, int tile, void* stream);
 int mvae_winograd_dy_transform(const float* dy, void* d, int nb, int h, int w, int k, int dy_split, int tile,
                                void* stream);
+// Both backward transforms of dy in one pass (a conv whose input and weight gradients both run the Winograd form):
+// v = mvae_winograd_input_transform(dy) and d = mvae_winograd_dy_transform(dy), each [a^2][T][k] split4_bf16.
+// Replaces the two separate passes over dy of the conv backward (encoder_decoder.py ResnetBlock convs, autograd).
+int mvae_winograd_dy_transforms(const float* dy, void* v, void* d, int nb, int h, int w, int k, int dy_split, int tile,
+                                void* stream);
 int mvae_winograd_wgrad_gemm(const void* d, const void* v, float* m, long long tiles, int cout, int cin, int tile,
                              float* workspace, size_t workspace_bytes, void* stream);
 int mvae_winograd_wgrad_output(const float* m, float* dw, float beta, int cout, int cin, int tile, void* stream);

@@ -42,6 +42,7 @@ SIGNATURES = {
     "mvae_winograd_output_transform": (I, [P, P, P, P, P, I, I, I, I, I, P]),
     "mvae_winograd_output_gnbwd": (I, [P, P, P, P, P, P, P, I, I, P, I, I, I, I, I, P]),
     "mvae_winograd_dy_transform": (I, [P, P, I, I, I, I, I, I, P]),
+    "mvae_winograd_dy_transforms": (I, [P, P, P, I, I, I, I, I, I, P]),
     "mvae_winograd_wgrad_gemm": (I, [P, P, P, L, I, I, I, P, Z, P]),
     "mvae_winograd_wgrad_output": (I, [P, P, F, I, I, I, P]),
     "mvae_conv2d_wgrad_workspace_bytes": (Z, [I, I, I, I, I, I, I]),

@@ -477,6 +477,68 @@ __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ 
     for (int j = 0; j < AL; ++j) wstore(vr, base + (unsigned)(i * AL + j) * plane, split4_bf16(o[i][j]));
 }
 
+// dy -> both backward operands in one pass over dy (a conv whose input and weight gradients both run the Winograd
+// form): V' = B^T P B of the a x a patch P (the input gradient's transformed input, as wino_in_kernel on dy) and
+// D' = A D A^T of the m x m tile D = P[1..m][1..m] inside it (the weight gradient's transformed output gradient, as
+// wino_dy_kernel) -- the separate kernels each read all of dy. One thread per (tile, 4-group); D' one output row at a
+// time (184 VGPRs: the patch plus one row).
+template <int MT, bool XS>
+__global__ void __launch_bounds__(256) wino_dy2_kernel(const float* __restrict__ dy, uint4* __restrict__ v,
+                                                       uint4* __restrict__ d, int nb, int H, int W, int K) {
+  constexpr int AL = MT + 2;
+  const int K4 = K >> 2, th = (H + MT - 1) / MT, tw = (W + MT - 1) / MT;
+  const long long T = (long long)nb * th * tw;
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= T * K4) return;
+  const long long t = idx / K4;
+  const int k4 = (int)(idx - t * K4);
+  const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(dy, (unsigned)((long long)nb * H * W * K * 4));
+  const unsigned kb = (unsigned)k4 * 16u;
+  const unsigned plane = (unsigned)(T * K4 * 16), base = (unsigned)(t * K4 + k4) * 16u;
+  const __amdgpu_buffer_rsrc_t vr = make_rsrc(v, plane * (unsigned)(AL * AL));
+  const __amdgpu_buffer_rsrc_t dr = make_rsrc(d, plane * (unsigned)(AL * AL));
+  float4 p[AL][AL];
+#pragma unroll
+  for (int i = 0; i < AL; ++i)
+#pragma unroll
+    for (int j = 0; j < AL; ++j) {
+      const int h = MT * ti - 1 + i, w = MT * tj - 1 + j;
+      const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const float4 r = bload4(xr, ok ? ((unsigned)((b * H + h) * W + w) * (unsigned)K) * 4u + kb : OOB);
+      p[i][j] = XS ? split4_to_f32(r) : r;
+    }
+#pragma unroll
+  for (int i = 0; i < AL; ++i) {  // D' row i = (A D)[i] A^T, A[i][u] = A^T[u][i]
+    float4 ci[MT], o[AL];
+#pragma unroll
+    for (int e = 0; e < MT; ++e) {
+      bool first = true;
+      ci[e] = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < MT; ++u) wmadd(ci[e], first, wino_at<MT>(u, i), p[1 + u][1 + e]);
+    }
+#pragma unroll
+    for (int j = 0; j < AL; ++j) {
+      bool first = true;
+      o[j] = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < MT; ++e) wmadd(o[j], first, wino_at<MT>(e, j), ci[e]);
+    }
+#pragma unroll
+    for (int j = 0; j < AL; ++j) wstore(dr, base + (unsigned)(i * AL + j) * plane, split4_bf16(o[j]));
+  }
+  constexpr auto bt = [](int i, int k) { return wino_bt<MT>(i, k); };
+#pragma unroll
+  for (int j = 0; j < AL; ++j) wlin<AL, AL>(&p[0][j], AL, &p[0][j], AL, bt);
+#pragma unroll
+  for (int i = 0; i < AL; ++i) wlin<AL, AL>(&p[i][0], 1, &p[i][0], 1, bt);
+#pragma unroll
+  for (int i = 0; i < AL; ++i)
+#pragma unroll
+    for (int j = 0; j < AL; ++j) wstore(vr, base + (unsigned)(i * AL + j) * plane, split4_bf16(p[i][j]));
+}
+
 // dw [cout][3][3][cin] = beta * dw + G^T M G, M [a^2][cout][cin] fp32: one thread per (k, 4-group of c)
 template <int MT>
 __global__ void __launch_bounds__(256) wino_wout_kernel(const float* __restrict__ m, float* __restrict__ dw, float beta,
@@ -743,6 +805,27 @@ int mvae_winograd_dy_transform(const float* dy, void* d, int nb, int h, int w, i
   } else {
     if (dy_split) hipLaunchKernelGGL((wino_dy_kernel<4, true>), g, dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
     else hipLaunchKernelGGL((wino_dy_kernel<4, false>), g, dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
+  }
+  return launch_status();
+}
+
+// Both backward transforms of dy in one pass: v = the input gradient's V' (as mvae_winograd_input_transform on dy) and
+// d = the weight gradient's D' (as mvae_winograd_dy_transform), each [a^2][T][k] split4_bf16
+int mvae_winograd_dy_transforms(const float* dy, void* v, void* d, int nb, int h, int w, int k, int dy_split, int tile,
+                                void* stream) {
+  if (!dy || !v || !d || !wino_geom_ok(tile, nb, h, w, k, k) || !al16(dy) || !al16(v) || !al16(d)) {
+    set_error("winograd_dy_transforms: tile 2 or 4, k %% 4 == 0, 16-B aligned");
+    return MVAE_EINVAL;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g(egrid256(wino_tiles(nb, h, w, tile) * (k / 4)));
+  uint4 *vv = (uint4*)v, *dd = (uint4*)d;
+  if (tile == 2) {
+    if (dy_split) hipLaunchKernelGGL((wino_dy2_kernel<2, true>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
+    else hipLaunchKernelGGL((wino_dy2_kernel<2, false>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
+  } else {
+    if (dy_split) hipLaunchKernelGGL((wino_dy2_kernel<4, true>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
+    else hipLaunchKernelGGL((wino_dy2_kernel<4, false>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
   }
   return launch_status();
 }

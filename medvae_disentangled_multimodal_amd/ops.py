@@ -299,6 +299,9 @@ def _wino_tiles(n: int, h: int, wd: int) -> int:
 
 
 WINOGRAD_WGRAD = os.environ.get("MVAE_NO_WINOGRAD_WGRAD") is None
+# the conv backward's two passes over dy (the input gradient's input transform, the weight gradient's dy transform) as
+# one (mvae_winograd_dy_transforms); MVAE_NO_WINOGRAD_DY2=1: two kernels
+WINOGRAD_DY2 = os.environ.get("MVAE_NO_WINOGRAD_DY2") is None
 # GroupNorm(+SiLU) -> Winograd conv: the GroupNorm computes its statistics only and the conv's input transform applies
 # the normalization on load (mvae_winograd_input_transform_gn), so the GroupNorm output is never written or read
 # (SURVEY §7 hard part 4 / VERDICT r4 item 3 on the Winograd form, which reads its input once). The output handed to the
@@ -343,11 +346,13 @@ WINOGRAD_KEEP_V = os.environ.get("MVAE_NO_WINOGRAD_KEEP_V") is None
 
 
 def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split: bool, dgrad: bool, st, keep=None,
-              gn=None, key=None, u=None, chunk=(0, 0)):
+              gn=None, key=None, u=None, chunk=(0, 0), dkeep=None):
     """U (filters, unless `u` is given), V (input tiles) and the (m+2)^2 position GEMMs M = V U^T for the n images of
     src; returns (M (arena), U) for an output transform. keep (a list): V is allocated outside the arena and appended
     to it (WINOGRAD_KEEP_V), tagged with `key` (the conv's input tensor; default src) and the image range `chunk`.
-    gn (LazyGn): src is a GroupNorm input, normalized on load (its scale / shift rows of these images)."""
+    gn (LazyGn): src is a GroupNorm input, normalized on load (its scale / shift rows of these images).
+    dkeep (a list; input gradient only): src is dy, and the weight gradient's D' = A dy A^T comes out of the same pass
+    over dy (mvae_winograd_dy_transforms), appended like keep's entries for conv2d_wgrad_raw."""
     mt = WINOGRAD_TILE
     t = _wino_tiles(n, h, wd)
     pos = (mt + 2) ** 2
@@ -363,7 +368,13 @@ def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split:
         u = ARENA.get("wino_u", 4 * pos * k_in * n_out, dev)
         cin, cout = (n_out, k_in) if dgrad else (k_in, n_out)
         _lib.call("mvae_winograd_weight_transform", w.data_ptr(), u.data_ptr(), cin, cout, int(dgrad), mt, st)
-    if gn is not None:
+    if dkeep is not None:
+        d = torch.empty(4 * pos * t * k_in, dtype=torch.uint8, device=dev)
+        kt = src if key is None else key
+        dkeep.append((d, mt, kt.data_ptr(), kt._version, tuple(chunk)))
+        _lib.call("mvae_winograd_dy_transforms", src.data_ptr(), v.data_ptr(), d.data_ptr(), n, h, wd, k_in,
+                  int(src_split), mt, st)
+    elif gn is not None:
         b0 = chunk[0]
         _lib.call("mvae_winograd_input_transform_gn", src.data_ptr(), gn.scale[b0 * k_in:].data_ptr(),
                   gn.shift[b0 * k_in:].data_ptr(), gn.silu, v.data_ptr(), n, h, wd, k_in, mt, st)
@@ -778,11 +789,12 @@ def split_dy(dy: torch.Tensor) -> Optional[torch.Tensor]:
     return ds
 
 
-def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=None):
+def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=None, dkeep=None):
     """gn_link (GnBwdLink): the conv's input was silu?(GroupNorm(x)) -- also emit that GroupNorm's backward
     partials from the GEMM epilogue (mvae_conv2d_dgrad_gnbwd_nhwc) into gn_link.part when the launch allows it.
     dys: dy pre-split by split_dy (same values; used as the gathered GEMM operand when given).
-    dyb: dy as packed bf16 (pack_dy; bf16-mixed mode)."""
+    dyb: dy as packed bf16 (pack_dy; bf16-mixed mode).
+    dkeep (a list): on the Winograd path also keep the weight gradient's transformed dy per image chunk (_winograd)."""
     n, c, h, wd = x_shape
     co = w.shape[0]
     _, _, ho, wo = dy.shape
@@ -803,7 +815,8 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
             u = None
             for b0, b1 in _wino_chunks(n, h, wd, max(c, co)):
                 nb = b1 - b0
-                m, u = _winograd(dya[b0:b1], w, nb, h, wd, co, c, dys is not None, True, st, u=u)
+                m, u = _winograd(dya[b0:b1], w, nb, h, wd, co, c, dys is not None, True, st, u=u, key=dya,
+                                 chunk=(b0, b1), dkeep=dkeep)
                 if link is None:
                     _lib.call("mvae_winograd_output_transform", m.data_ptr(), None, None, dx[b0:b1].data_ptr(), None, nb,
                               h, wd, c, WINOGRAD_TILE, st)
@@ -894,7 +907,7 @@ def _conv_dgrad_bf16(dyb, w, dx, g, n, c, h, wd, co, ho, wo, flops, shp, st):
 
 
 def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool = False, dys=None, dyb=None,
-                     x_bf16: bool = False, wino_v=None):
+                     x_bf16: bool = False, wino_v=None, wino_d=None):
     """dw (+ db when given and the conv is not pointwise) accumulate with `beta`. Returns True when
     the bias gradient was produced by the fused wgrad kernel. dys: dy pre-split by split_dy; dyb: dy as packed bf16
     (pack_dy, bf16-mixed mode)."""
@@ -920,10 +933,11 @@ def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool
     if x_bf16:
         raise RuntimeError("conv2d wgrad: a packed bf16 input needs the bf16-mixed LDS-DMA path (packed dy, cout % 8)")
     with _timed("conv_wgrad", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
-        return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db, x_split, dys, wino_v)
+        return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db, x_split, dys, wino_v, wino_d)
 
 
-def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_split=False, dys=None, wino_v=None):
+def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_split=False, dys=None, wino_v=None,
+                       wino_d=None):
     st = _stream(dy)
     if x_split and (g.pointwise or g.upsample):
         raise RuntimeError("conv2d wgrad: a pre-split input needs a non-pointwise, non-upsample conv")
@@ -971,17 +985,23 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         for e in wino_v or ():
             if e[1] == mt and e[2] == x.data_ptr() and e[3] == x._version:
                 kept[e[4]] = e[0]
+        kept_d = {}  # the input gradient's pass over dy kept D' too (mvae_winograd_dy_transforms)
+        for e in wino_d or ():
+            if e[1] == mt and e[2] == dya.data_ptr() and e[3] == dya._version:
+                kept_d[e[4]] = e[0]
         for i, (b0, b1) in enumerate(_wino_chunks(n, h, wd, max(c, co))):
             nb, t = b1 - b0, _wino_tiles(b1 - b0, h, wd)
             v = kept.get((b0, b1))
             if v is None and getattr(x, GN_LAZY_ATTR, None) is not None:
                 raise RuntimeError("conv2d wgrad: a deferred GroupNorm input needs the forward's kept Winograd "
                                    "transform")
-            dt = ARENA.get("wino_d", 4 * pos * t * co, dev)
+            dt = kept_d.get((b0, b1))
             m = ARENA.get("wino_mw", 4 * pos * co * c, dev)
             ws = ARENA.get("ws", _lib.query("mvae_gemm_workspace_bytes", co, c, t, pos), dev)
-            _lib.call("mvae_winograd_dy_transform", dya[b0:b1].data_ptr(), dt.data_ptr(), nb, h, wd, co,
-                      int(dys is not None), mt, st)
+            if dt is None:
+                dt = ARENA.get("wino_d", 4 * pos * t * co, dev)
+                _lib.call("mvae_winograd_dy_transform", dya[b0:b1].data_ptr(), dt.data_ptr(), nb, h, wd, co,
+                          int(dys is not None), mt, st)
             if v is None:
                 v = ARENA.get("wino_v", 4 * pos * t * c, dev)
                 _lib.call("mvae_winograd_input_transform", x[b0:b1].data_ptr(), v.data_ptr(), nb, h, wd, c,
@@ -1198,6 +1218,7 @@ class Conv2dFn(torch.autograd.Function):
                 db_ret = None
         if dys is None and not g.pointwise and not _subpixel_upsample(g) and dyb is None:
             dys = split_dy(dy)
+        dkeep = None  # (set below when the input gradient's pass over dy also writes the weight gradient's D')
 
         def wgrad():
             nonlocal dw_ret, bias_done
@@ -1207,14 +1228,15 @@ class Conv2dFn(torch.autograd.Function):
             xs, xb16 = ctx.x_split, ctx.x_bf16
             if tgt is not None and (not want_b_w or btgt is not None):
                 fused = conv2d_wgrad_raw(dy, x, tgt, 1.0, g, btgt, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16,
-                                         wino_v=ctx.wino_v)
+                                         wino_v=ctx.wino_v, wino_d=dkeep)
                 bias_done = bias_done or fused
             elif tgt is not None:
-                conv2d_wgrad_raw(dy, x, tgt, 1.0, g, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16, wino_v=ctx.wino_v)
+                conv2d_wgrad_raw(dy, x, tgt, 1.0, g, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16, wino_v=ctx.wino_v,
+                                 wino_d=dkeep)
             else:
                 dw_ret = torch.empty_like(w, memory_format=CL)
                 conv2d_wgrad_raw(dy, x, dw_ret, 0.0, g, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16,
-                                 wino_v=ctx.wino_v)
+                                 wino_v=ctx.wino_v, wino_d=dkeep)
 
         side = _bwd_side(dy) if ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and \
             _main_grad(ctx.weight_ref) is not None and _overlap_ok(x, dy, g) else None
@@ -1228,15 +1250,22 @@ class Conv2dFn(torch.autograd.Function):
             with torch.cuda.stream(stream):
                 wgrad()
             ev_join.record(stream)
+        # both gradients on the Winograd form, one after the other: the input gradient's pass over dy also writes the
+        # weight gradient's transformed dy (mvae_winograd_dy_transforms), instead of a second pass
+        n_, c_, h_, w_ = x.shape
+        dkeep = [] if (WINOGRAD_DY2 and side is None and dyb is None and ctx.needs_input_grad[0] and
+                       ctx.needs_input_grad[1] and WINOGRAD_WGRAD and not g.pointwise and
+                       _wino_ok(g, n_, h_, w_, c_, w.shape[0])) else None
         if ctx.needs_input_grad[0]:
-            dx = conv2d_dgrad_raw(dy, w, x.shape, g, link if ctx.x_sink is None else None, dys=dys, dyb=dyb)
+            dx = conv2d_dgrad_raw(dy, w, x.shape, g, link if ctx.x_sink is None else None, dys=dys, dyb=dyb,
+                                  dkeep=dkeep)
             if ctx.x_sink is not None and ctx.x_sink.park(dx):
                 dx = None
         if side is not None:
             main.wait_event(ev_join)
         elif ctx.needs_input_grad[1]:
             wgrad()
-        ctx.wino_v = None  # (released after the join: a later main-stream allocation is ordered after its last use)
+        ctx.wino_v = dkeep = None  # (released after the join: a later main-stream allocation is ordered after its last use)
         if ctx.has_bias and ctx.needs_input_grad[2] and not bias_done:
             tgt = _main_grad(ctx.bias_ref)
             n, co, ho, wo = dy.shape

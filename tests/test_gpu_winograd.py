@@ -228,6 +228,8 @@ def test_winograd_kept_input_transform_feeds_weight_gradient(dev, monkeypatch):
     dy0 = torch.randn(n, c, h, w, generator=g)
     geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
 
+    monkeypatch.setattr(ops, "WINOGRAD_DY2", False)  # (dy's transforms as two kernels: counted below)
+
     def run(keep):
         monkeypatch.setattr(ops, "WINOGRAD_KEEP_V", keep)
         seen = []
@@ -252,6 +254,65 @@ def test_winograd_kept_input_transform_feeds_weight_gradient(dev, monkeypatch):
     assert (nk, nr) == (1, 2)  # backward: dy's transform only, vs dy's and x's
     assert torch.equal(dwk, dwr) and torch.equal(dxk, dxr)
 
+
+
+@pytest.mark.parametrize("n,ci,co,h,w", CASES)
+@pytest.mark.parametrize("dy_split", [False, True])
+def test_winograd_dy_transforms_match_the_two_passes(dev, n, ci, co, h, w, dy_split, _wino_on):
+    """mvae_winograd_dy_transforms (one pass over dy) writes exactly what the input gradient's input transform and the
+    weight gradient's dy transform write (bitwise: the same operation order)."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    mt = _wino_on
+    g = torch.Generator().manual_seed(n * 131 + h * 7 + w)
+    dy = cl(torch.randn(n, co, h, w, generator=g), dev)
+    src = _split(dy) if dy_split else dy
+    t = n * -(-h // mt) * -(-w // mt)
+    nbytes = 4 * (mt + 2) ** 2 * t * co
+    v1, d1, v2, d2 = (torch.full((nbytes,), 7, dtype=torch.uint8, device=dev) for _ in range(4))
+    st = ops._stream(dy)
+    _lib.call("mvae_winograd_dy_transforms", src.data_ptr(), v1.data_ptr(), d1.data_ptr(), n, h, w, co,
+              int(dy_split), mt, st)
+    _lib.call("mvae_winograd_input_transform", src.data_ptr(), v2.data_ptr(), n, h, w, co, int(dy_split), mt, st)
+    _lib.call("mvae_winograd_dy_transform", src.data_ptr(), d2.data_ptr(), n, h, w, co, int(dy_split), mt, st)
+    torch.cuda.synchronize()
+    assert torch.equal(v1, v2) and torch.equal(d1, d2)
+
+
+def test_winograd_backward_one_pass_over_dy(dev, monkeypatch):
+    """Through Conv2dFn's backward: the input gradient's pass over dy keeps D' for the weight gradient (WINOGRAD_DY2):
+    one dy kernel instead of two, dx and dW bitwise equal to the two-pass backward."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    n, c, h, w = 2, 128, 16, 16
+    g = torch.Generator().manual_seed(11)
+    x0 = torch.randn(n, c, h, w, generator=g)
+    w0 = torch.randn(c, c, 3, 3, generator=g) / (3 * c ** 0.5)
+    dy0 = torch.randn(n, c, h, w, generator=g)
+    geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
+
+    def run(dy2):
+        monkeypatch.setattr(ops, "WINOGRAD_DY2", dy2)
+        seen = []
+        orig = _lib.call
+
+        def spy(name, *args):
+            seen.append(name)
+            return orig(name, *args)
+        x = cl(x0, dev).requires_grad_(True)
+        wt = w0.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        y = ops.conv2d(x, wt, None, geom)
+        monkeypatch.setattr(_lib, "call", spy)
+        try:
+            y.backward(cl(dy0, dev))
+        finally:
+            monkeypatch.setattr(_lib, "call", orig)
+        torch.cuda.synchronize()
+        return x.grad.cpu(), wt.grad.cpu(), [seen.count(k) for k in (
+            "mvae_winograd_dy_transforms", "mvae_winograd_dy_transform", "mvae_winograd_input_transform")]
+
+    dx1, dw1, n1 = run(True)
+    dx2, dw2, n2 = run(False)
+    assert n1 == [1, 0, 0] and n2 == [0, 1, 1]
+    assert torch.equal(dx1, dx2) and torch.equal(dw1, dw2)
 
 
 def _gn_conv_step(dev, x0, g0, b0, w0, cb0, dy0, groups, monkeypatch, **flags):
