@@ -481,7 +481,7 @@ __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ 
 // form): V' = B^T P B of the a x a patch P (the input gradient's transformed input, as wino_in_kernel on dy) and
 // D' = A D A^T of the m x m tile D = P[1..m][1..m] inside it (the weight gradient's transformed output gradient, as
 // wino_dy_kernel) -- the separate kernels each read all of dy. One thread per (tile, 4-group); D' one output row at a
-// time (184 VGPRs: the patch plus one row).
+// time (181-215 VGPRs: the patch plus one row; 2 waves per SIMD, as the input transform).
 template <int MT, bool XS>
 __global__ void __launch_bounds__(256) wino_dy2_kernel(const float* __restrict__ dy, uint4* __restrict__ v,
                                                        uint4* __restrict__ d, int nb, int H, int W, int K) {
