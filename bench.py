@@ -536,7 +536,7 @@ def _compact_roofline(r):
                              "launches_per_step", "avg_launch_us", "gemm_ms_per_step", "instrumented_step_ms",
                              "reference_equivalent_TFLOP/s")
            if k in r}
-    out["kernel"] = "gemm3x_kernel"
+    out["kernel"] = "gemm3x_kernel + wino_* (MFMA-roofline family)"
     if r.get("by_pass"):  # per pass: [launches, ms per step, TFLOP/s]
         out["by_pass"] = {k: [v["launches"], v["ms"], v["TFLOP/s"]] for k, v in r["by_pass"].items()}
     for fam in ("hbm_kernels", "hbm_loss_kernels"):
