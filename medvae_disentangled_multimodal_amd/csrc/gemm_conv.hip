@@ -139,12 +139,11 @@ static int tail_split_images(int nb, long long hw, int n_cols, int k, bool v) {
   t.M = (int)std::min<long long>((long long)nb * hw, 1LL << 30); t.N = n_cols; t.K = k; t.batch = 1;
   const int cfg = choose_tile(t, v, false);
   if (cfg < T256x256 || cfg > T64x64) return nb;
-  static const int res[5] = {1, 1, 1, 2, 4}, bm[5] = {256, 256, 128, 128, 64}, bn[5] = {256, 128, 256, 128, 64};
-  const long long slots = 256LL * res[cfg], tiles = tiles_of(cfg, t);
+  const long long slots = 256LL * resident_of(cfg), tiles = tiles_of(cfg, t);
   const long long full = tiles / slots, rem = tiles - full * slots;
   if (full < 1 || rem == 0 || rem * 2 >= slots) return nb;
-  const long long tn = (n_cols + bn[cfg] - 1) / bn[cfg];
-  const long long nm = (full * slots / tn) * bm[cfg] / hw;
+  const long long tn = (n_cols + tile_n_of(cfg) - 1) / tile_n_of(cfg);
+  const long long nm = (full * slots / tn) * tile_m_of(cfg) / hw;
   return (nm >= 1 && nm < nb) ? (int)nm : nb;
 }
 

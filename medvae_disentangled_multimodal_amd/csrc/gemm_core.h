@@ -1915,6 +1915,22 @@ enum { T256x256 = 0, T256x128 = 1, T128x256 = 2, T128x128 = 3, T64x64 = 4, T128x
 enum { MATH_3XBF16 = 0, MATH_BF16 = 1, MATH_FP32 = 2 };
 int math_mode();
 
+// workgroups of a tile config resident per CU at once (LDS-bound: 160, 120, 120, 80, 40 KB per workgroup; the skinny
+// tiles 4 / 3): a "round" of a launch is 256 CUs x this many tiles
+inline int resident_of(int cfg) {
+  static const int r[7] = {1, 1, 1, 2, 4, 4, 3};
+  return (cfg >= 0 && cfg < 7) ? r[cfg] : 1;
+}
+// tile edge lengths of a config (rows of M, columns of N)
+inline int tile_m_of(int cfg) {
+  static const int m[7] = {256, 256, 128, 128, 64, 128, 128};
+  return (cfg >= 0 && cfg < 7) ? m[cfg] : 64;
+}
+inline int tile_n_of(int cfg) {
+  static const int n[7] = {256, 128, 256, 128, 64, 16, 32};
+  return (cfg >= 0 && cfg < 7) ? n[cfg] : 64;
+}
+
 inline long long tiles_of(int cfg, const GemmArgs& a) {
   static const int TM_[] = {256, 256, 128, 128, 64, 128, 128};
   static const int TN_[] = {256, 128, 256, 128, 64, 16, 32};

@@ -729,12 +729,11 @@ int mvae_winograd_gemm(const void* v, const void* u, float* m, long long tiles, 
   // wave-quantization tail (as conv2d_impl's): positions whose tiles would leave a nearly empty last round (c2's 7x7x512
   // level: 16 tiles of 256x128 per position x 36 = 2.25 rounds) go in a second launch the cost model tiles finely
   static const bool no_tail = getenv("MVAE_NO_TAIL_SPLIT") != nullptr;
-  static const int res[5] = {1, 1, 1, 2, 4};
   int b_main = a.batch;
   if (!no_tail && cfg >= T256x256 && cfg <= T64x64) {
     GemmArgs one = a;
     one.batch = 1;
-    const long long tp = tiles_of(cfg, one), slots = 256LL * res[cfg], tot = tp * a.batch;
+    const long long tp = tiles_of(cfg, one), slots = 256LL * resident_of(cfg), tot = tp * a.batch;
     const long long full = tot / slots, rem = tot - full * slots;
     // (up to half a round: c4's 8x8x2048 level is 32 tiles x 36 = 4.5 rounds of 256x256)
     if (full >= 1 && rem > 0 && rem * 2 <= slots) b_main = (int)std::max<long long>(1, full * slots / tp);
