@@ -227,19 +227,28 @@ __global__ void __launch_bounds__(256) wino_wt_fwd_kernel(const float* __restric
 // contiguous along n and the destination along k, so a workgroup transposes a 32 (n) x KQ (k groups of 4) block through
 // LDS: loads coalesced over n (32 lanes), stores in KQ * 16-B runs over k
 constexpr int WDG_N = 32;
-template <int MT>
-constexpr int wdg_kq() { return MT == 2 ? 8 : 4; }
-template <int MT>
+// KQ k-groups per workgroup (store runs of KQ x 16 B), the a^2 positions staged through LDS in passes of PP (the stage
+// is PP x 32 x KQ x 16 B): m = 4 large filters (cin x cout >= 2^20: c4's 16x16 / 8x8 levels) take 8 x 16 B runs in two
+// passes of 18 positions (72 KB, 256 threads; 8x8x2048: 274 -> 205 us), the small ones one pass of 4 x 16 B (fewer
+// barriers: the two-pass form measured 30-40 % slower on them); m = 2 one pass of 8
+template <int MT, bool BIG>
+constexpr int wdg_kq() { return (MT == 2 || BIG) ? 8 : 4; }
+template <int MT, bool BIG>
+constexpr int wdg_pp() { return MT == 2 ? 16 : BIG ? 18 : 36; }
+template <int MT, bool BIG>
 __global__ void __launch_bounds__(256) wino_wt_dgrad_kernel(const float* __restrict__ w, uint4* __restrict__ u,
                                                             int cout, int cin) {
-  constexpr int AL = MT + 2, KQ = wdg_kq<MT>(), NT = WDG_N * KQ;
-  __shared__ uint4 lds[AL * AL][WDG_N][KQ];  // 64 KB (m = 2), 72 KB (m = 4)
+  constexpr int AL = MT + 2, KQ = wdg_kq<MT, BIG>(), NT = WDG_N * KQ, PP = wdg_pp<MT, BIG>();
+  static_assert((AL * AL) % PP == 0, "position passes");
+  __shared__ uint4 lds[PP][WDG_N][KQ];
   const int K4 = cout >> 2;
   const int n0 = blockIdx.x * WDG_N, kb = blockIdx.y * KQ;
   const int nl = threadIdx.x % WDG_N, kq = threadIdx.x / WDG_N;
   const int n = n0 + nl, k4 = kb + kq;
-  if (n < cin && k4 < K4) {
-    float4 g[3][3], o[AL][AL];
+  const bool act = n < cin && k4 < K4;
+  float4 o[AL][AL];
+  if (act) {
+    float4 g[3][3];
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -250,16 +259,23 @@ __global__ void __launch_bounds__(256) wino_wt_dgrad_kernel(const float* __restr
         g[r][s] = float4{e[0], e[1], e[2], e[3]};
       }
     wino_filter<MT>(g, o);
-#pragma unroll
-    for (int i = 0; i < AL; ++i)
-#pragma unroll
-      for (int j = 0; j < AL; ++j) lds[i * AL + j][nl][kq] = split4_bf16(o[i][j]);
   }
-  __syncthreads();
-  for (int e = threadIdx.x; e < AL * AL * WDG_N * KQ; e += NT) {
-    const int xi = e / (WDG_N * KQ), rem = e % (WDG_N * KQ);
-    const int nn = n0 + rem / KQ, kk = kb + rem % KQ;
-    if (nn < cin && kk < K4) u[((long long)xi * cin + nn) * K4 + kk] = lds[xi][rem / KQ][rem % KQ];
+#pragma unroll
+  for (int p0 = 0; p0 < AL * AL; p0 += PP) {
+    if (act) {
+#pragma unroll
+      for (int i = 0; i < AL; ++i)
+#pragma unroll
+        for (int j = 0; j < AL; ++j)
+          if (i * AL + j >= p0 && i * AL + j < p0 + PP) lds[i * AL + j - p0][nl][kq] = split4_bf16(o[i][j]);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < PP * WDG_N * KQ; e += NT) {
+      const int xi = e / (WDG_N * KQ), rem = e % (WDG_N * KQ);
+      const int nn = n0 + rem / KQ, kk = kb + rem % KQ;
+      if (nn < cin && kk < K4) u[((long long)(p0 + xi) * cin + nn) * K4 + kk] = lds[xi][rem / KQ][rem % KQ];
+    }
+    __syncthreads();
   }
 }
 
@@ -647,11 +663,14 @@ int mvae_winograd_weight_transform(const float* w, void* u, int cin, int cout, i
   hipStream_t st = (hipStream_t)stream;
   if (dgrad) {
     if (tile == 2)
-      hipLaunchKernelGGL(wino_wt_dgrad_kernel<2>, dim3(cdiv(cin, WDG_N), cdiv(cout / 4, wdg_kq<2>())),
-                         dim3(WDG_N * wdg_kq<2>()), 0, st, w, (uint4*)u, cout, cin);
+      hipLaunchKernelGGL((wino_wt_dgrad_kernel<2, false>), dim3(cdiv(cin, WDG_N), cdiv(cout / 4, wdg_kq<2, false>())),
+                         dim3(WDG_N * wdg_kq<2, false>()), 0, st, w, (uint4*)u, cout, cin);
+    else if ((long long)cin * cout >= (1LL << 20))
+      hipLaunchKernelGGL((wino_wt_dgrad_kernel<4, true>), dim3(cdiv(cin, WDG_N), cdiv(cout / 4, wdg_kq<4, true>())),
+                         dim3(WDG_N * wdg_kq<4, true>()), 0, st, w, (uint4*)u, cout, cin);
     else
-      hipLaunchKernelGGL(wino_wt_dgrad_kernel<4>, dim3(cdiv(cin, WDG_N), cdiv(cout / 4, wdg_kq<4>())),
-                         dim3(WDG_N * wdg_kq<4>()), 0, st, w, (uint4*)u, cout, cin);
+      hipLaunchKernelGGL((wino_wt_dgrad_kernel<4, false>), dim3(cdiv(cin, WDG_N), cdiv(cout / 4, wdg_kq<4, false>())),
+                         dim3(WDG_N * wdg_kq<4, false>()), 0, st, w, (uint4*)u, cout, cin);
   } else {
     const dim3 g(egrid256((long long)cout * (cin / 4)));
     if (tile == 2) hipLaunchKernelGGL(wino_wt_fwd_kernel<2>, g, dim3(256), 0, st, w, (uint4*)u, cout, cin);

@@ -24,6 +24,7 @@ CASES = [
     (1, 32, 64, 12, 64),   # W = 64: two 32-pixel segments per row
     (3, 64, 64, 7, 7),     # c2's 7x7 level: edge tiles cut (no fused statistics)
     (2, 32, 48, 14, 10),   # ragged both ways
+    (1, 1024, 1024, 4, 4), # cin x cout >= 2^20: the two-pass input-gradient filter transform (m = 4)
 ]
 
 

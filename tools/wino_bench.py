@@ -52,6 +52,8 @@ for nb, h, w, ci, co in SHAPES:
     stages = [
         ("wt_fwd", lambda: _lib.call("mvae_winograd_weight_transform", wt.data_ptr(), u.data_ptr(), ci, co, 0, MT, st),
          4.0 * co * ci * (9 + POS), 0),
+        ("wt_dgrad", lambda: _lib.call("mvae_winograd_weight_transform", wt.data_ptr(), u.data_ptr(), ci, co, 1, MT,
+                                       st), 4.0 * co * ci * (9 + POS), 0),
         ("in", lambda: _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), nb, h, w, ci, 0, MT, st),
          4.0 * (x.numel() + POS * t * ci), 0),
         ("in_gn", lambda: _lib.call("mvae_winograd_input_transform_gn", x.data_ptr(), sc.data_ptr(), sh.data_ptr(), 1,
