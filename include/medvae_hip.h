@@ -163,13 +163,16 @@ size_t mvae_conv2d_wgrad_upsample_workspace_bytes(int nb, int h, int w_, int cin
 
 /* Winograd F(m x m, 3x3) form of a 3x3 / stride-1 / pad-1 conv, m = `tile` in {2, 4} (ResnetBlock conv1 / conv2 and
  * the mid blocks at the 8x8 / 16x16 levels, encoder_decoder.py:123-170; forward, input gradient, weight gradient),
- * 3xBF16 math mode only; a = m + 2, P = a^2 transformed positions, T = nb (h/m) (w/m) output tiles. Stages on the
+ * every math mode (mvae_set_math_mode); a = m + 2, P = a^2 transformed positions, T = nb (h/m) (w/m) output tiles. Stages on the
  * stream: U = G g G^T of the filters, V = B^T d B of the input's a x a patches, M_xi = V_xi U_xi^T for the P positions
  * (one batched MFMA GEMM: P / (9 m^2) of the direct conv's MACs -- 4/9 at m = 2, 1/4 at m = 4), output A^T M A
  * (+ bias, + residual, + the following GroupNorm's statistics). The input gradient is the same conv of dy with the
  * flipped, transposed filters (weight_transform dgrad = 1) and may emit the GroupNorm backward partials of
- * mvae_conv2d_dgrad_gnbwd_nhwc (output_gnbwd). V, U: split4_bf16 (16 B per 4 values), M: fp32. Conditions: w in
- * {8, 16}, h % 4 == 0, channel counts % 4 == 0, 16-B aligned operands.
+ * mvae_conv2d_dgrad_gnbwd_nhwc (output_gnbwd). V, U, D': 16 B per 4 values in the math mode's pre-split layout --
+ * split4_bf16 in the 3xBF16 and bf16 modes (the bf16 GEMM reads the hi halves), the split4 bit split (upper / lower 16
+ * bits of each fp32 word) in the exact fp32 mode, where x_split / dy_split must be 0; M: fp32. Conditions: channel counts
+ * % 4 == 0, 16-B aligned operands, each transformed operand < 4 GiB; the statistics / GroupNorm-backward forms need
+ * h % 4 == 0 and w in {8, 16} or a multiple of 32.
  *   weight_transform: w [cout][3][3][cin] -> u [P][cout][cin] (dgrad 0) or [P][cin][cout] (dgrad 1)
  *   input_transform:  x [nb][h][w][c] (fp32, or split4_bf16 groups when x_split) -> v [P][T][c]
  *   gemm:             m [P][tiles][n_out] = v . u^T over k_in

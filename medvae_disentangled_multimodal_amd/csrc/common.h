@@ -71,6 +71,21 @@ __device__ __forceinline__ uint4 split4_bf16(float4 v) {
                pk_bf16x2(v.z - __uint_as_float(h23 << 16), v.w - __uint_as_float(h23 & 0xFFFF0000u))};
 }
 
+// the exact-fp32 arithmetic's pre-split layout (gemm_core.h st_split<0>): the same 16-B group shape as split4_bf16, but
+// a BIT split -- the upper 16 bits of x0..x3 in the first 8 B, the lower 16 bits in the last 8 B -- so the GEMM's exact
+// MMA step reassembles each fp32 operand bit for bit
+__device__ __forceinline__ uint4 split4_bits(float4 v) {
+  const unsigned bx = __float_as_uint(v.x), by = __float_as_uint(v.y), bz = __float_as_uint(v.z), bw = __float_as_uint(v.w);
+  return uint4{(bx >> 16) | (by & 0xFFFF0000u), (bz >> 16) | (bw & 0xFFFF0000u), (bx & 0xFFFFu) | (by << 16),
+               (bz & 0xFFFFu) | (bw << 16)};
+}
+// pre-split group of format SF: 0 = split4_bf16 (3xBF16 value split; its hi half is the bf16 operand), 1 = split4_bits
+template <int SF>
+__device__ __forceinline__ uint4 split4_fmt(float4 v) {
+  if constexpr (SF == 1) return split4_bits(v);
+  else return split4_bf16(v);
+}
+
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace mvae

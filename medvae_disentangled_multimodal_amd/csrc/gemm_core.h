@@ -219,12 +219,14 @@ __device__ __forceinline__ void st_split(__bf16* img, int plane, int off, const 
   }
 }
 
-// slot already split in HBM (split4_bf16 layout: per 4 elements hi0..hi3 then lo0..lo3, 16 B)
+// slot already split in HBM (split4_bf16 layout: per 4 elements hi0..hi3 then lo0..lo3, 16 B; in the exact fp32
+// arithmetic, PREC 0, the split4_bits bit split of the same shape -- st_split<0>'s planes)
 template <int PREC>
 __device__ __forceinline__ void st_presplit(__bf16* img, int plane, int off, const float4& v) {
   typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
   *(u32x2_t*)(img + off) = u32x2_t{__float_as_uint(v.x), __float_as_uint(v.y)};
-  if constexpr (PREC == 3) *(u32x2_t*)(img + plane + off) = u32x2_t{__float_as_uint(v.z), __float_as_uint(v.w)};
+  if constexpr (PREC == 3 || PREC == 0)
+    *(u32x2_t*)(img + plane + off) = u32x2_t{__float_as_uint(v.z), __float_as_uint(v.w)};
 }
 
 // MFMA operand fragment, k-step ks of the K-tile.
@@ -2040,12 +2042,16 @@ void launch_cfg(GemmArgs& a, hipStream_t st) {
   constexpr bool presplit = AK == A_CONV_FWD_SPLIT || AK == A_CONV_DGRAD_SPLIT || AK == A_COLM_SPLIT || AK == A_ROWK_SPLIT ||
                             BKIND == B_ROWK_SPLIT || BKIND == B_WGRAD_FWD_SPLIT || BKIND == B_WGRAD_P2_SPLIT ||
                             BKIND == B_COLN_SPLIT;
+  // the Winograd position / weight-gradient GEMMs: their pre-split operands come in the arithmetic's own layout (a bit
+  // split in the exact mode, csrc/winograd.hip); every other pre-split operand is a 3xBF16 value split, never launched
+  // in the exact mode
+  constexpr bool wino = (AK == A_ROWK_SPLIT && BKIND == B_ROWK_SPLIT) || (AK == A_COLM_SPLIT && BKIND == B_COLN_SPLIT);
   const int mm = math_mode();
   if constexpr (PO >= 0)
     hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, PO>), grid, dim3(64 * WGM * WGN), 0, st, a);
   else if (mm == MATH_BF16)
     hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, 1>), grid, dim3(64 * WGM * WGN), 0, st, a);
-  else if (mm == MATH_FP32 && !presplit)  // (pre-split operands are value splits: never launched in this mode)
+  else if (mm == MATH_FP32 && (!presplit || wino))
     hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, 0>), grid, dim3(64 * WGM * WGN), 0, st, a);
   else
     hipLaunchKernelGGL((gemm3x_kernel<BM, BN, WGM, WGN, AK, VA, BKIND, VB, 3>), grid, dim3(64 * WGM * WGN), 0, st, a);

@@ -9,10 +9,13 @@
 //   m = 2: B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1], G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1],
 //          A^T = [1 1 1 0; 0 1 -1 -1]
 //   m = 4: points 0, +-1, +-2, inf (wino_bt / wino_g / wino_at below)
-// The transforms run in fp32; V and U are written in the 3xBF16 pre-split layout (split4_bf16) so the batched GEMM
-// (gemm3x_kernel, A_ROWK_SPLIT x B_ROWK_SPLIT, a^2 batch entries) stages them without split arithmetic. Error against
-// float64 (tests/test_gpu_winograd.py): m = 2 ~1e-5, m = 4 ~5e-5 norm-wise relative (the larger m = 4 coefficients
-// amplify the 3xBF16 operand rounding; the north_star bar is 1e-3). The cost against the direct conv is the transform
+// The transforms run in fp32; V and U are written pre-split so the batched GEMM (gemm3x_kernel, A_ROWK_SPLIT x
+// B_ROWK_SPLIT, a^2 batch entries) stages them without split arithmetic, in the layout of the process's GEMM arithmetic:
+// 3xBF16 and bf16 -- split4_bf16 (the bf16 GEMM stages the hi halves: V and U rounded to bf16); exact fp32 -- split4_bits
+// (a bit split the f32-input MFMA reassembles exactly). Error against float64 (tests/test_gpu_winograd.py): 3xBF16 m = 2
+// ~1e-5, m = 4 ~5e-5 norm-wise relative (the larger m = 4 coefficients amplify the operand rounding; the north_star bar
+// is 1e-3); exact fp32 m = 4 ~5e-7; bf16 m = 2 ~4e-3 (1.7x the direct bf16 conv; m = 4 would be ~11x, so the bf16 mode
+// uses m = 2 -- ops.py). The cost against the direct conv is the transform
 // traffic -- V is a^2 / m^2 times the input (4x for m = 2, 2.25x for m = 4), M as much of the output -- small next to
 // the GEMM when the channel count is large and the image small, which is where the dispatcher (ops.py) uses it.
 //
@@ -129,7 +132,7 @@ struct WinoGn {
   int silu;
 };
 
-template <int MT, bool XS, int GN = 0>  // GN: 0 none, 1 GroupNorm affine on load, 2 affine + SiLU
+template <int MT, bool XS, int GN = 0, int SF = 0>  // GN: 0 none, 1 GroupNorm affine on load, 2 affine + SiLU
 __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ x, uint4* __restrict__ v, int nb, int H,
                                                       int W, int C, WinoGn gn) {
   constexpr int AL = MT + 2;
@@ -186,7 +189,7 @@ __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ 
 #pragma unroll
   for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < AL; ++j) wstore(vr, base + (unsigned)(i * AL + j) * plane, split4_bf16(d[i][j]));
+    for (int j = 0; j < AL; ++j) wstore(vr, base + (unsigned)(i * AL + j) * plane, split4_fmt<SF>(d[i][j]));
 }
 
 // G g G^T of a 3x3 filter of float4 groups
@@ -203,7 +206,7 @@ __device__ __forceinline__ void wino_filter(const float4 (&g)[3][3], float4 (&o)
 
 // forward filters U[a^2][cout][cin] split4_bf16 from KRSC weights w [cout][3][3][cin], g(n, k) = w[n][.][.][k]:
 // one thread per (cout n, 4-group of cin k), 9 coalesced 16-B loads, a^2 coalesced 16-B stores
-template <int MT>
+template <int MT, int SF>
 __global__ void __launch_bounds__(256) wino_wt_fwd_kernel(const float* __restrict__ w, uint4* __restrict__ u, int cout,
                                                           int cin) {
   constexpr int AL = MT + 2;
@@ -220,7 +223,7 @@ __global__ void __launch_bounds__(256) wino_wt_fwd_kernel(const float* __restric
 #pragma unroll
   for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < AL; ++j) u[((long long)(i * AL + j) * cout + n) * K4 + k4] = split4_bf16(o[i][j]);
+    for (int j = 0; j < AL; ++j) u[((long long)(i * AL + j) * cout + n) * K4 + k4] = split4_fmt<SF>(o[i][j]);
 }
 
 // input-gradient filters U'[a^2][cin][cout] split4_bf16, g'(n = cin, k = cout)[r][s] = w[k][2-r][2-s][n]: the source is
@@ -235,7 +238,7 @@ template <int MT, bool BIG>
 constexpr int wdg_kq() { return (MT == 2 || BIG) ? 8 : 4; }
 template <int MT, bool BIG>
 constexpr int wdg_pp() { return MT == 2 ? 16 : BIG ? 18 : 36; }
-template <int MT, bool BIG>
+template <int MT, bool BIG, int SF>
 __global__ void __launch_bounds__(256) wino_wt_dgrad_kernel(const float* __restrict__ w, uint4* __restrict__ u,
                                                             int cout, int cin) {
   constexpr int AL = MT + 2, KQ = wdg_kq<MT, BIG>(), NT = WDG_N * KQ, PP = wdg_pp<MT, BIG>();
@@ -267,7 +270,7 @@ __global__ void __launch_bounds__(256) wino_wt_dgrad_kernel(const float* __restr
       for (int i = 0; i < AL; ++i)
 #pragma unroll
         for (int j = 0; j < AL; ++j)
-          if (i * AL + j >= p0 && i * AL + j < p0 + PP) lds[i * AL + j - p0][nl][kq] = split4_bf16(o[i][j]);
+          if (i * AL + j >= p0 && i * AL + j < p0 + PP) lds[i * AL + j - p0][nl][kq] = split4_fmt<SF>(o[i][j]);
     }
     __syncthreads();
     for (int e = threadIdx.x; e < PP * WDG_N * KQ; e += NT) {
@@ -457,7 +460,7 @@ __global__ void __launch_bounds__(256) wino_out_any_kernel(WinoOut p) {
 
 // dy [nb][H][W][K] (fp32, or split4_bf16 groups when XS) -> D' = A D A^T [a^2][T][K] split4_bf16: one thread per
 // (tile, 4-group)
-template <int MT, bool XS>
+template <int MT, bool XS, int SF = 0>
 __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ dy, uint4* __restrict__ d, int nb, int H,
                                                       int W, int K) {
   constexpr int AL = MT + 2;
@@ -490,7 +493,7 @@ __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ 
 #pragma unroll
   for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < AL; ++j) wstore(vr, base + (unsigned)(i * AL + j) * plane, split4_bf16(o[i][j]));
+    for (int j = 0; j < AL; ++j) wstore(vr, base + (unsigned)(i * AL + j) * plane, split4_fmt<SF>(o[i][j]));
 }
 
 // dy -> both backward operands in one pass over dy (a conv whose input and weight gradients both run the Winograd
@@ -498,7 +501,7 @@ __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ 
 // D' = A D A^T of the m x m tile D = P[1..m][1..m] inside it (the weight gradient's transformed output gradient, as
 // wino_dy_kernel) -- the separate kernels each read all of dy. One thread per (tile, 4-group); D' one output row at a
 // time (181-215 VGPRs: the patch plus one row; 2 waves per SIMD, as the input transform).
-template <int MT, bool XS>
+template <int MT, bool XS, int SF = 0>
 __global__ void __launch_bounds__(256) wino_dy2_kernel(const float* __restrict__ dy, uint4* __restrict__ v,
                                                        uint4* __restrict__ d, int nb, int H, int W, int K) {
   constexpr int AL = MT + 2;
@@ -542,7 +545,7 @@ __global__ void __launch_bounds__(256) wino_dy2_kernel(const float* __restrict__
       for (int e = 0; e < MT; ++e) wmadd(o[j], first, wino_at<MT>(e, j), ci[e]);
     }
 #pragma unroll
-    for (int j = 0; j < AL; ++j) wstore(dr, base + (unsigned)(i * AL + j) * plane, split4_bf16(o[j]));
+    for (int j = 0; j < AL; ++j) wstore(dr, base + (unsigned)(i * AL + j) * plane, split4_fmt<SF>(o[j]));
   }
   constexpr auto bt = [](int i, int k) { return wino_bt<MT>(i, k); };
 #pragma unroll
@@ -552,7 +555,7 @@ __global__ void __launch_bounds__(256) wino_dy2_kernel(const float* __restrict__
 #pragma unroll
   for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < AL; ++j) wstore(vr, base + (unsigned)(i * AL + j) * plane, split4_bf16(p[i][j]));
+    for (int j = 0; j < AL; ++j) wstore(vr, base + (unsigned)(i * AL + j) * plane, split4_fmt<SF>(p[i][j]));
 }
 
 // dw [cout][3][3][cin] = beta * dw + G^T M G, M [a^2][cout][cin] fp32: one thread per (k, 4-group of c)
@@ -609,10 +612,63 @@ static bool wino_blocks_ok(int h, int w) { return h % 4 == 0 && (w == 8 || w == 
 
 static int egrid256(long long n) { return (int)std::min<long long>((n + 255) / 256, 1LL << 30); }
 
-static bool wino_math_ok() {
-  if (math_mode() == MATH_3XBF16) return true;
-  set_error("winograd: the 3xBF16 (fp32-class) arithmetic only");
+// every GEMM arithmetic: 3xBF16 (V / U value-split into split4_bf16), bf16 (the same groups; the GEMM stages the hi
+// halves) and exact fp32 (bit split, split4_bits: the f32-input MFMA reassembles the transforms' fp32 words exactly)
+static int wino_sf() { return math_mode() == MATH_FP32 ? 1 : 0; }
+// a pre-split INPUT is a 3xBF16 value split: there is none in the exact mode
+static bool wino_split_in_ok(int split) {
+  if (!split || wino_sf() == 0) return true;
+  set_error("winograd: pre-split (3xBF16) inputs are not used in the exact fp32 arithmetic");
   return false;
+}
+
+template <int MT, int SF>
+static void wt_go(const float* w, void* u, int cin, int cout, int dgrad, hipStream_t st) {
+  if (dgrad) {
+    if constexpr (MT == 4) {
+      if ((long long)cin * cout >= (1LL << 20)) {
+        hipLaunchKernelGGL((wino_wt_dgrad_kernel<4, true, SF>), dim3(cdiv(cin, WDG_N), cdiv(cout / 4, wdg_kq<4, true>())),
+                           dim3(WDG_N * wdg_kq<4, true>()), 0, st, w, (uint4*)u, cout, cin);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((wino_wt_dgrad_kernel<MT, false, SF>), dim3(cdiv(cin, WDG_N), cdiv(cout / 4, wdg_kq<MT, false>())),
+                       dim3(WDG_N * wdg_kq<MT, false>()), 0, st, w, (uint4*)u, cout, cin);
+  } else {
+    hipLaunchKernelGGL((wino_wt_fwd_kernel<MT, SF>), dim3(egrid256((long long)cout * (cin / 4))), dim3(256), 0, st, w,
+                       (uint4*)u, cout, cin);
+  }
+}
+
+// gn: 0 plain (xs: x pre-split), 1 GroupNorm affine on load, 2 affine + SiLU
+template <int MT, int SF>
+static void in_go(const float* x, void* v, int nb, int h, int w, int c, int xs, int gn, WinoGn p, hipStream_t st) {
+  const dim3 g(egrid256(wino_tiles(nb, h, w, MT) * (c / 4)));
+  if constexpr (SF == 0) {
+    if (xs) {
+      hipLaunchKernelGGL((wino_in_kernel<MT, true, 0, 0>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, p);
+      return;
+    }
+  }
+  if (gn == 2) hipLaunchKernelGGL((wino_in_kernel<MT, false, 2, SF>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, p);
+  else if (gn == 1) hipLaunchKernelGGL((wino_in_kernel<MT, false, 1, SF>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, p);
+  else hipLaunchKernelGGL((wino_in_kernel<MT, false, 0, SF>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, p);
+}
+
+// both = 0: D' only (wino_dy_kernel); 1: V' and D' in one pass (wino_dy2_kernel)
+template <int MT, int SF>
+static void dy_go(const float* dy, void* v, void* d, int nb, int h, int w, int k, int xs, bool both, hipStream_t st) {
+  const dim3 g(egrid256(wino_tiles(nb, h, w, MT) * (k / 4)));
+  uint4 *vv = (uint4*)v, *dd = (uint4*)d;
+  if constexpr (SF == 0) {
+    if (xs) {
+      if (both) hipLaunchKernelGGL((wino_dy2_kernel<MT, true, 0>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
+      else hipLaunchKernelGGL((wino_dy_kernel<MT, true, 0>), g, dim3(256), 0, st, dy, dd, nb, h, w, k);
+      return;
+    }
+  }
+  if (both) hipLaunchKernelGGL((wino_dy2_kernel<MT, false, SF>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
+  else hipLaunchKernelGGL((wino_dy_kernel<MT, false, SF>), g, dim3(256), 0, st, dy, dd, nb, h, w, k);
 }
 
 template <int MT, int WSEG>
@@ -659,23 +715,10 @@ int mvae_winograd_weight_transform(const float* w, void* u, int cin, int cout, i
     set_error("winograd_weight_transform: cin, cout multiples of 4, 16-B aligned w / u, tile 2 or 4");
     return MVAE_EINVAL;
   }
-  if (!wino_math_ok()) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  if (dgrad) {
-    if (tile == 2)
-      hipLaunchKernelGGL((wino_wt_dgrad_kernel<2, false>), dim3(cdiv(cin, WDG_N), cdiv(cout / 4, wdg_kq<2, false>())),
-                         dim3(WDG_N * wdg_kq<2, false>()), 0, st, w, (uint4*)u, cout, cin);
-    else if ((long long)cin * cout >= (1LL << 20))
-      hipLaunchKernelGGL((wino_wt_dgrad_kernel<4, true>), dim3(cdiv(cin, WDG_N), cdiv(cout / 4, wdg_kq<4, true>())),
-                         dim3(WDG_N * wdg_kq<4, true>()), 0, st, w, (uint4*)u, cout, cin);
-    else
-      hipLaunchKernelGGL((wino_wt_dgrad_kernel<4, false>), dim3(cdiv(cin, WDG_N), cdiv(cout / 4, wdg_kq<4, false>())),
-                         dim3(WDG_N * wdg_kq<4, false>()), 0, st, w, (uint4*)u, cout, cin);
-  } else {
-    const dim3 g(egrid256((long long)cout * (cin / 4)));
-    if (tile == 2) hipLaunchKernelGGL(wino_wt_fwd_kernel<2>, g, dim3(256), 0, st, w, (uint4*)u, cout, cin);
-    else hipLaunchKernelGGL(wino_wt_fwd_kernel<4>, g, dim3(256), 0, st, w, (uint4*)u, cout, cin);
-  }
+  const int sf = wino_sf();
+  if (tile == 2) (sf ? wt_go<2, 1> : wt_go<2, 0>)(w, u, cin, cout, dgrad, st);
+  else (sf ? wt_go<4, 1> : wt_go<4, 0>)(w, u, cin, cout, dgrad, st);
   return launch_status();
 }
 
@@ -686,19 +729,11 @@ int mvae_winograd_input_transform(const float* x, void* v, int nb, int h, int w,
     set_error("winograd_input_transform: tile 2 or 4, c %% 4 == 0, 16-B aligned");
     return MVAE_EINVAL;
   }
+  if (!wino_split_in_ok(x_split)) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  const dim3 g(egrid256(wino_tiles(nb, h, w, tile) * (c / 4)));
-  if (tile == 2) {
-    if (x_split) hipLaunchKernelGGL((wino_in_kernel<2, true>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c,
-                                 WinoGn{});
-    else hipLaunchKernelGGL((wino_in_kernel<2, false>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c,
-                                 WinoGn{});
-  } else {
-    if (x_split) hipLaunchKernelGGL((wino_in_kernel<4, true>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c,
-                                 WinoGn{});
-    else hipLaunchKernelGGL((wino_in_kernel<4, false>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c,
-                                 WinoGn{});
-  }
+  const int sf = wino_sf();
+  if (tile == 2) (sf ? in_go<2, 1> : in_go<2, 0>)(x, v, nb, h, w, c, x_split, 0, WinoGn{}, st);
+  else (sf ? in_go<4, 1> : in_go<4, 0>)(x, v, nb, h, w, c, x_split, 0, WinoGn{}, st);
   return launch_status();
 }
 
@@ -712,15 +747,10 @@ int mvae_winograd_input_transform_gn(const float* x, const float* scale, const f
     return MVAE_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;
-  const dim3 g(egrid256(wino_tiles(nb, h, w, tile) * (c / 4)));
   const WinoGn gn{scale, shift, silu};
-  if (tile == 2) {
-    if (silu) hipLaunchKernelGGL((wino_in_kernel<2, false, 2>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, gn);
-    else hipLaunchKernelGGL((wino_in_kernel<2, false, 1>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, gn);
-  } else {
-    if (silu) hipLaunchKernelGGL((wino_in_kernel<4, false, 2>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, gn);
-    else hipLaunchKernelGGL((wino_in_kernel<4, false, 1>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, gn);
-  }
+  const int sf = wino_sf(), mode = silu ? 2 : 1;
+  if (tile == 2) (sf ? in_go<2, 1> : in_go<2, 0>)(x, v, nb, h, w, c, 0, mode, gn, st);
+  else (sf ? in_go<4, 1> : in_go<4, 0>)(x, v, nb, h, w, c, 0, mode, gn, st);
   return launch_status();
 }
 
@@ -734,7 +764,6 @@ int mvae_winograd_gemm(const void* v, const void* u, float* m, long long tiles, 
     set_error("winograd_gemm: k_in, n_out multiples of 4, 16-B aligned, one position < 4 GiB, tile 2 or 4");
     return MVAE_EINVAL;
   }
-  if (!wino_math_ok()) return MVAE_EINVAL;
   GemmArgs a{};
   a.M = (int)tiles; a.N = n_out; a.K = k_in; a.batch = (tile + 2) * (tile + 2);
   a.A = (const float*)v; a.lda = k_in; a.sA = tiles * k_in;
@@ -815,15 +844,11 @@ int mvae_winograd_dy_transform(const float* dy, void* d, int nb, int h, int w, i
     set_error("winograd_dy_transform: tile 2 or 4, k %% 4 == 0, 16-B aligned");
     return MVAE_EINVAL;
   }
+  if (!wino_split_in_ok(dy_split)) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  const dim3 g(egrid256(wino_tiles(nb, h, w, tile) * (k / 4)));
-  if (tile == 2) {
-    if (dy_split) hipLaunchKernelGGL((wino_dy_kernel<2, true>), g, dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
-    else hipLaunchKernelGGL((wino_dy_kernel<2, false>), g, dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
-  } else {
-    if (dy_split) hipLaunchKernelGGL((wino_dy_kernel<4, true>), g, dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
-    else hipLaunchKernelGGL((wino_dy_kernel<4, false>), g, dim3(256), 0, st, dy, (uint4*)d, nb, h, w, k);
-  }
+  const int sf = wino_sf();
+  if (tile == 2) (sf ? dy_go<2, 1> : dy_go<2, 0>)(dy, nullptr, d, nb, h, w, k, dy_split, false, st);
+  else (sf ? dy_go<4, 1> : dy_go<4, 0>)(dy, nullptr, d, nb, h, w, k, dy_split, false, st);
   return launch_status();
 }
 
@@ -835,16 +860,11 @@ int mvae_winograd_dy_transforms(const float* dy, void* v, void* d, int nb, int h
     set_error("winograd_dy_transforms: tile 2 or 4, k %% 4 == 0, 16-B aligned");
     return MVAE_EINVAL;
   }
+  if (!wino_split_in_ok(dy_split)) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  const dim3 g(egrid256(wino_tiles(nb, h, w, tile) * (k / 4)));
-  uint4 *vv = (uint4*)v, *dd = (uint4*)d;
-  if (tile == 2) {
-    if (dy_split) hipLaunchKernelGGL((wino_dy2_kernel<2, true>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
-    else hipLaunchKernelGGL((wino_dy2_kernel<2, false>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
-  } else {
-    if (dy_split) hipLaunchKernelGGL((wino_dy2_kernel<4, true>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
-    else hipLaunchKernelGGL((wino_dy2_kernel<4, false>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
-  }
+  const int sf = wino_sf();
+  if (tile == 2) (sf ? dy_go<2, 1> : dy_go<2, 0>)(dy, v, d, nb, h, w, k, dy_split, true, st);
+  else (sf ? dy_go<4, 1> : dy_go<4, 0>)(dy, v, d, nb, h, w, k, dy_split, true, st);
   return launch_status();
 }
 
@@ -858,7 +878,6 @@ int mvae_winograd_wgrad_gemm(const void* d, const void* v, float* m, long long t
     set_error("winograd_wgrad_gemm: cout, cin multiples of 4, 16-B aligned, one position < 4 GiB, tile 2 or 4");
     return MVAE_EINVAL;
   }
-  if (!wino_math_ok()) return MVAE_EINVAL;
   GemmArgs a{};
   a.M = cout; a.N = cin; a.K = (int)tiles; a.batch = (tile + 2) * (tile + 2);
   a.A = (const float*)d; a.lda = cout; a.sA = tiles * cout;

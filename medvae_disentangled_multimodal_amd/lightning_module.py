@@ -33,6 +33,16 @@ except Exception:  # pragma: no cover - not installed in this image
     _Base = nn.Module
 
 
+_CAPTURE_ERR_MARKS = ("captur", "graph", "not permitted when stream")
+
+
+def _is_capture_error(e: BaseException) -> bool:
+    """An error raised by recording the step (HIP stream capture / graph instantiation, or a collective the runtime
+    cannot record), as opposed to an error of the step itself, which must propagate."""
+    msg = str(e).lower()
+    return any(m in msg for m in _CAPTURE_ERR_MARKS)
+
+
 def _model_kind(model: nn.Module) -> str:
     if isinstance(model, DisentangledConditionalVAE) or hasattr(model, "modality_decoders"):
         return "indices"
@@ -309,11 +319,24 @@ class VAELightningModule(_Base):
             return self.fit_step(batch, batch_idx, eps=eps)
         g = getattr(self, "_graph", None)
         if g is None or g["key"] != key:
+            err = None
             try:
                 g = self._capture_step(ins, len(batch), batch_idx, key, mode)
-            except RuntimeError as e:  # (e.g. a collective the runtime cannot record): fall back to eager steps
+            except RuntimeError as e:
+                if not _is_capture_error(e):
+                    raise
+                err, g = e, None
+            # the fall-back decision is collective: a rank that replays its graphs while a peer runs the eager exchange
+            # would issue a different collective sequence (every rank falls back when any capture failed)
+            pg = self.process_group
+            if pg is not None and getattr(pg, "world", 1) > 1:
+                failed = torch.tensor([err is not None], device=ins[0].device)
+                if bool(pg.any_across_ranks(failed)[0]) and err is None:
+                    err = RuntimeError("a peer rank's step capture failed")
+            if err is not None:  # (e.g. a collective the runtime cannot record): eager steps from here on
                 import warnings
-                warnings.warn(f"fit_step_graphed: step capture failed ({e}); running eager steps")
+                warnings.warn(f"fit_step_graphed: step capture failed ({err}); running eager steps")
+                self._graph = None
                 self._graph_failed = key
                 torch.cuda.synchronize(ins[0].device)
                 return self.fit_step(batch, batch_idx, eps=eps)
@@ -383,7 +406,10 @@ class VAELightningModule(_Base):
                 rec.update(graph_opt=graph_opt, used=used)
         finally:
             ops.ARENA.pinning = None
-        self.global_step_count = step0
+            # (recording executes no step: the host-side counter the recorded fit_step advanced -- it drives the LR
+            # schedule and the discriminator start -- is restored whether or not the capture completed; the optimizer's
+            # step counts live on the device and were not touched)
+            self.global_step_count = step0
         rec.update(graph=graph, loss=loss)
         self._graph = rec
         return self._graph

@@ -49,9 +49,9 @@ def nhwc(t: torch.Tensor) -> torch.Tensor:
 
 
 class _Arena:
-    """Per-device, per-stream scratch buffers reused across launches: the work of one stream is ordered, so a buffer
-    keyed by (name, device, stream) is never used by two kernels at once -- the side-stream weight gradient of the
-    two-stream conv backward (Conv2dFn._backward) gets buffers of its own whatever names it asks for.
+    """Per-device scratch buffers reused across launches: the work of one stream is ordered, so a buffer keyed by
+    (name, device) is never used by two kernels at once -- the side-stream weight gradient of the two-stream conv
+    backward (Conv2dFn._backward) gets buffers of its own (keyed by its stream) whatever names it asks for.
 
     A buffer that is outgrown is replaced (and its memory returned to the caching allocator). A captured
     HIP graph bakes in the raw pointers of the buffers it used, so while a capture records (`pinning`
@@ -66,7 +66,11 @@ class _Arena:
 
     def get(self, key: str, nbytes: int, device) -> torch.Tensor:
         dev = torch.device(device)
-        k = (key, str(dev), torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0)
+        # (only the backward's side streams get buffers of their own: the default stream and a graph-capture stream
+        # never run at once, so they share one set -- two copies of the multi-GB Winograd buffers would otherwise stay
+        # allocated for a graphed run)
+        s = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
+        k = (key, str(dev), s if s in _SIDE_STREAMS else 0)
         t = self.bufs.get(k)
         if t is None or t.numel() < nbytes:
             t = torch.empty(max(int(nbytes * 1.25) + 256, 256), dtype=torch.uint8, device=device)
@@ -78,6 +82,7 @@ class _Arena:
 
 
 ARENA = _Arena()
+_SIDE_STREAMS = set()  # cuda_stream handles of the conv backward's side streams (_bwd_side)
 
 # Optional live kernel timing (bench.py): when PROFILE is a list, every implicit-GEMM launch is
 # bracketed by HIP events on the current stream and recorded as
@@ -235,9 +240,28 @@ if WINOGRAD_TILE not in (2, 4):
     raise ValueError("MVAE_WINOGRAD_TILE must be 2 or 4")
 
 
+# The other two GEMM arithmetics. Exact fp32 ("32-exact", mode 2): the transforms write V / U as
+# a bit split the f32-input MFMA reassembles exactly, so only the Winograd algorithm's own fp32 rounding differs from the
+# direct conv -- F(4x4) errs ~5e-7 against float64 (direct fp32 ~4e-8), far inside the exact mode's 1e-4 step bar;
+# MVAE_NO_WINOGRAD_EXACT=1 keeps the direct implicit GEMM there. bf16-mixed (mode 1): V and U rounded to bf16 in the
+# transform domain amplify the rounding -- simulated against float64 at 16x16x256 the direct bf16 conv errs 2.4e-3, F(2x2)
+# 4.0e-3, F(4x4) 2.7e-2 -- so that mode uses m = 2 (MVAE_WINOGRAD_TILE_BF16), at 4x the input / output transform traffic
+# for 4/9 of the MACs: only where the images are small and the channels wide (MVAE_WINOGRAD_BF16_MAX_W, default 16: c5's
+# 8x8x2048 and 16x16x1024 levels). MVAE_NO_WINOGRAD_BF16=1 keeps its convs on the LDS-DMA implicit GEMM.
+WINOGRAD_EXACT = os.environ.get("MVAE_NO_WINOGRAD_EXACT") is None
+WINOGRAD_BF16 = os.environ.get("MVAE_NO_WINOGRAD_BF16") is None
+WINOGRAD_TILE_BF16 = int(os.environ.get("MVAE_WINOGRAD_TILE_BF16", "2"))
+WINOGRAD_BF16_MAX_W = int(os.environ.get("MVAE_WINOGRAD_BF16_MAX_W", "16"))
+
+
+def _wtile() -> int:
+    """The output tile m of F(m x m, 3x3) in the current GEMM arithmetic."""
+    return WINOGRAD_TILE_BF16 if _MATH[0] == 1 else WINOGRAD_TILE
+
+
 def _wino_alg(ref: float) -> float:
     """GEMM FLOPs of the Winograd form of a conv whose direct form is `ref`: (m+2)^2 / (9 m^2)."""
-    m = WINOGRAD_TILE
+    m = _wtile()
     return ref * (m + 2) ** 2 / (9.0 * m * m)
 
 
@@ -253,8 +277,15 @@ WINOGRAD_MIN_MACS = float(os.environ.get("MVAE_WINOGRAD_MIN_MACS", "1e10"))
 def _wino_ok(g, n: int, h: int, wd: int, cin: int, cout: int) -> bool:
     """Any image size (edge tiles are zero-filled / cut: c2's 7x7 level in 2x2 tiles of 4x4); the fused GroupNorm
     statistics / partials additionally need _wino_blocks."""
-    return (WINOGRAD and _MATH[0] == 0 and _dma_fmt() == 0 and g.kh == 3 and g.kw == 3 and g.stride == 1 and
-            not g.upsample and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and wd <= WINOGRAD_MAX_W and
+    mode = _MATH[0]
+    if mode == 0:  # (3xBF16 on the register-staged loop; the opt-in planar LDS-DMA format has no Winograd form)
+        on, maxw = _dma_fmt() == 0, WINOGRAD_MAX_W
+    elif mode == 2:
+        on, maxw = WINOGRAD_EXACT, WINOGRAD_MAX_W
+    else:
+        on, maxw = WINOGRAD_BF16, min(WINOGRAD_MAX_W, WINOGRAD_BF16_MAX_W)
+    return (WINOGRAD and on and g.kh == 3 and g.kw == 3 and g.stride == 1 and
+            not g.upsample and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and wd <= maxw and
             cin % 4 == 0 and cout % 4 == 0 and
             min(cin, cout) >= (WINOGRAD_MIN_C_WIDE if wd >= 32 else WINOGRAD_MIN_C) and
             9.0 * n * h * wd * cin * cout >= WINOGRAD_MIN_MACS and
@@ -281,7 +312,7 @@ WINOGRAD_MAX_CHUNKS = 4
 def _wino_chunks(n: int, h: int, wd: int, cmax: int):
     """[(b0, b1)] image ranges whose transformed operands ((m+2)^2 x tiles x channels x 4 B) each fit one 4 GiB buffer
     descriptor (c4's 64x64x512 decoder conv at B = 256: two halves)."""
-    per_img = (WINOGRAD_TILE + 2) ** 2 * _wino_tiles(1, h, wd) * cmax * 4
+    per_img = (_wtile() + 2) ** 2 * _wino_tiles(1, h, wd) * cmax * 4
     per = max(1, _MAX_DESC_BYTES // per_img) if per_img <= _MAX_DESC_BYTES else 0
     if per == 0:
         return [None] * (WINOGRAD_MAX_CHUNKS + 1)  # (one image alone is too large)
@@ -294,7 +325,7 @@ def _wino_blocks(h: int, wd: int) -> bool:
 
 
 def _wino_tiles(n: int, h: int, wd: int) -> int:
-    mt = WINOGRAD_TILE
+    mt = _wtile()
     return n * (-(-h // mt)) * (-(-wd // mt))
 
 
@@ -305,7 +336,8 @@ WINOGRAD_DY2 = os.environ.get("MVAE_NO_WINOGRAD_DY2") is None
 # GroupNorm(+SiLU) -> Winograd conv: the GroupNorm computes its statistics only and the conv's input transform applies
 # the normalization on load (mvae_winograd_input_transform_gn), so the GroupNorm output is never written or read
 # (SURVEY §7 hard part 4 / VERDICT r4 item 3 on the Winograd form, which reads its input once). The output handed to the
-# conv is a deferred placeholder: an expanded NaN scalar carrying GN_LAZY_ATTR, never materialized on this path.
+# conv is a deferred placeholder (DeferredGnOutput: an expanded scalar carrying GN_LAZY_ATTR whose values any torch op
+# refuses to read), never materialized on this path.
 # Default since the transform normalizes in branch-free code after its 36 loads (the first build branched on the SiLU
 # flag per element, which serialized the loads: 1.7x the plain transform's time, c4 -0.4 %); now the fused transform
 # runs at the plain one's speed and c4 gains 2 % (704-706 -> 717-721 img/s, GroupNorm family 40.5 -> 31.9 ms; same box,
@@ -332,6 +364,33 @@ class LazyGn:
         return y
 
 
+class DeferredGnOutput(torch.Tensor):
+    """The placeholder group_norm hands its consuming conv when the GroupNorm output is deferred (LazyGn): an expanded
+    scalar with the output's shape, dtype and device, attached to the GroupNorm's autograd node. Its values are never
+    computed, so every read of them raises -- a forward hook, user code on a Normalize output, any torch op -- instead
+    of returning the placeholder's bytes. Only metadata queries (shape, device, dtype, data_ptr, version, layout
+    checks) pass; ops.conv2d takes the values from the LazyGn record it carries. MVAE_NO_WINOGRAD_GN=1 writes the
+    GroupNorm output instead."""
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        if func in _DEFERRED_META:
+            with torch._C.DisableTorchFunctionSubclass():
+                return func(*args, **(kwargs or {}))
+        name = getattr(func, "__qualname__", None) or getattr(func, "__name__", repr(func))
+        raise RuntimeError(f"{name}: this GroupNorm output is deferred to its consuming convolution (the conv's Winograd "
+                           "input transform applies the normalization); its values exist nowhere else. Read the conv's "
+                           "output instead, or set MVAE_NO_WINOGRAD_GN=1 to have the GroupNorm write its output.")
+
+
+_DEFERRED_META = {torch.Tensor.shape.__get__, torch.Tensor.size, torch.Tensor.dim, torch.Tensor.ndim.__get__,
+                  torch.Tensor.data_ptr, torch.Tensor._version.__get__, torch.Tensor.is_contiguous,
+                  torch.Tensor.device.__get__, torch.Tensor.dtype.__get__, torch.Tensor.is_cuda.__get__,
+                  torch.Tensor.requires_grad.__get__, torch.Tensor.grad_fn.__get__, torch.Tensor.numel,
+                  torch.Tensor.layout.__get__, torch.Tensor.stride, torch.Tensor.is_leaf.__get__,
+                  torch.Tensor.__hash__, torch.Tensor.element_size, torch.Tensor.get_device}
+
+
 def _wino_wgrad_ok(g, x, dy, dw, dys) -> bool:
     n, c, h, wd = x.shape
     co = dy.shape[1]
@@ -353,7 +412,7 @@ def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split:
     gn (LazyGn): src is a GroupNorm input, normalized on load (its scale / shift rows of these images).
     dkeep (a list; input gradient only): src is dy, and the weight gradient's D' = A dy A^T comes out of the same pass
     over dy (mvae_winograd_dy_transforms), appended like keep's entries for conv2d_wgrad_raw."""
-    mt = WINOGRAD_TILE
+    mt = _wtile()
     t = _wino_tiles(n, h, wd)
     pos = (mt + 2) ** 2
     dev = src.device
@@ -682,13 +741,14 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
     split = WEIGHT_SPLIT and _splits_ok() and c % 4 == 0 and _al16(x) and not g.pointwise and g.kh * g.kw <= 32
     if x_split and (g.pointwise or g.upsample or c % 4 or not _al16(x)):
         raise RuntimeError("conv2d: a pre-split input needs a non-pointwise, non-upsample conv with cin % 4 == 0")
-    if _dma_ok(ref / 2) and c % 8 == 0 and not x_split and _al16(x) and not g.pointwise and g.kh * g.kw <= 32 and \
-            (sub or not g.upsample):
+    # (the Winograd form first: in the bf16-mixed mode it takes the small wide levels off the LDS-DMA path)
+    wino = not x_bf16 and _wino_ok(g, n, h, wd, c, co) and _al16(w) and (b is None or _al16(b)) and \
+        (res is None or _al16(res)) and (gn_part is None or _wino_blocks(h, wd)) and _al16(lazy.x if lazy is not None else x)
+    if not wino and _dma_ok(ref / 2) and c % 8 == 0 and not x_split and _al16(x) and not g.pointwise and \
+            g.kh * g.kw <= 32 and (sub or not g.upsample):
         return _conv_fwd_bf16(x, w, b, res, g, y, n, c, h, wd, co, ho, wo, sub, alg, ref, gn_part, st, x_bf16)
     if x_bf16:
         raise RuntimeError("conv2d: a packed bf16 input needs the bf16-mixed LDS-DMA conv path")
-    wino = _wino_ok(g, n, h, wd, c, co) and _al16(w) and (b is None or _al16(b)) and (res is None or _al16(res)) and \
-        (gn_part is None or _wino_blocks(h, wd)) and _al16(lazy.x if lazy is not None else x)
     if lazy is not None and not wino:  # a deferred GroupNorm output whose conv cannot normalize on load: write it
         x, lazy = lazy.materialize(), None
     if wino:
@@ -701,7 +761,7 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
                 gp = gn_part[b0 * (h * wd // 32) * (co // 4) * 2:] if gn_part is not None else None
                 _lib.call("mvae_winograd_output_transform", m.data_ptr(), _ptr(b),
                           _ptr(res[b0:b1] if res is not None else None), y[b0:b1].data_ptr(), _ptr(gp), b1 - b0, h,
-                          wd, co, WINOGRAD_TILE, st)
+                          wd, co, _wtile(), st)
         return y
     wg = w
     if sub:  # tap-summed per-class weights (prepared outside the timed GEMM launch)
@@ -765,7 +825,8 @@ def pack_dy(dy: torch.Tensor, g: ConvGeom, cin: int, bias_out=None, beta: float 
     bias_out: also accumulate the conv bias gradient (beta * bias_out + column sums of the fp32 dy) from the same pass
     (mvae_pack_bf16_colsum). Returns (packed dy or None, whether the bias gradient was produced)."""
     if not _bf16_dma() or g.pointwise or dy.dim() != 4 or dy.shape[1] % 8 or g.kh * g.kw > 32 or not _al16(dy) or \
-            not dy.is_contiguous(memory_format=CL) or not _dma_ok(float(dy.numel()) * cin * g.kh * g.kw):
+            not dy.is_contiguous(memory_format=CL) or not _dma_ok(float(dy.numel()) * cin * g.kh * g.kw) or \
+            _wino_ok(g, dy.shape[0], dy.shape[2], dy.shape[3], cin, dy.shape[1]):  # (Winograd: both passes read fp32 dy)
         return None, False
     if bias_out is None:
         return pack_bf16(dy, "dybf"), False
@@ -819,13 +880,13 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
                                  chunk=(b0, b1), dkeep=dkeep)
                 if link is None:
                     _lib.call("mvae_winograd_output_transform", m.data_ptr(), None, None, dx[b0:b1].data_ptr(), None, nb,
-                              h, wd, c, WINOGRAD_TILE, st)
+                              h, wd, c, _wtile(), st)
                 else:  # with the GroupNorm backward partials (mvae_conv2d_dgrad_gnbwd_nhwc's epilogue sums)
                     L = link
                     _lib.call("mvae_winograd_output_gnbwd", m.data_ptr(), dx[b0:b1].data_ptr(), L.x[b0:b1].data_ptr(),
                               L.mean[b0 * L.groups:].data_ptr(), L.rstd[b0 * L.groups:].data_ptr(),
                               L.gamma.data_ptr(), L.beta.data_ptr(), L.groups, L.silu,
-                              part[b0 * (h * wd // 32) * c * 2:].data_ptr(), nb, h, wd, c, WINOGRAD_TILE, st)
+                              part[b0 * (h * wd // 32) * c * 2:].data_ptr(), nb, h, wd, c, _wtile(), st)
             if link is not None:
                 link.part, link.dx = part, dx
         return dx
@@ -907,16 +968,19 @@ def _conv_dgrad_bf16(dyb, w, dx, g, n, c, h, wd, co, ho, wo, flops, shp, st):
 
 
 def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool = False, dys=None, dyb=None,
-                     x_bf16: bool = False, wino_v=None, wino_d=None):
+                     x_bf16: bool = False, wino_v=None, wino_d=None, lazy=None):
     """dw (+ db when given and the conv is not pointwise) accumulate with `beta`. Returns True when
     the bias gradient was produced by the fused wgrad kernel. dys: dy pre-split by split_dy; dyb: dy as packed bf16
-    (pack_dy, bf16-mixed mode)."""
+    (pack_dy, bf16-mixed mode). lazy (LazyGn): x is a deferred GroupNorm output -- the Winograd weight gradient takes
+    the forward's kept V (or re-derives it from the GroupNorm input); any other weight gradient gets x written first."""
     n, c, h, wd = x.shape
     co = dy.shape[1]
     _, _, ho, wo = dy.shape
+    if lazy is not None and (dyb is not None or not _wino_wgrad_ok(g, lazy.x, dy, dw, dys)):
+        x, lazy = lazy.materialize(), None
     ref = 2.0 * n * ho * wo * co * c * g.kh * g.kw
     alg = ref * 4 / 9 if _subpixel_upsample(g) else ref
-    if dyb is None and _wino_wgrad_ok(g, x, dy, dw, dys):
+    if dyb is None and _wino_wgrad_ok(g, x if lazy is None else lazy.x, dy, dw, dys):
         alg = _wino_alg(ref)
     if dyb is not None and not x_split and not g.upsample and c % 8 == 0 and co % 8 == 0 and _al16(x):
         # bf16-mixed weight gradient on packed bf16 dy and x (LDS-DMA main loop); the bias gradient is summed from the
@@ -933,12 +997,15 @@ def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool
     if x_bf16:
         raise RuntimeError("conv2d wgrad: a packed bf16 input needs the bf16-mixed LDS-DMA path (packed dy, cout % 8)")
     with _timed("conv_wgrad", alg, (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
-        return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db, x_split, dys, wino_v, wino_d)
+        return _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db, x_split, dys, wino_v, wino_d, lazy)
 
 
 def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_split=False, dys=None, wino_v=None,
-                       wino_d=None):
+                       wino_d=None, lazy=None):
     st = _stream(dy)
+    if isinstance(x, DeferredGnOutput) and (lazy is None or not _wino_wgrad_ok(g, lazy.x, dy, dw, dys)):
+        # (conv2d_wgrad_raw materializes such an x for every other path: reaching here would read the placeholder)
+        raise RuntimeError("conv2d wgrad: a deferred GroupNorm output reached a weight-gradient kernel that reads x")
     if x_split and (g.pointwise or g.upsample):
         raise RuntimeError("conv2d wgrad: a pre-split input needs a non-pointwise, non-upsample conv")
     if g.pointwise and db is None:
@@ -973,10 +1040,10 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         _lib.call("mvae_conv2d_wgrad_upsample_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db),
                   float(beta), n, h, wd, c, co, ws.data_ptr(), ws.numel(), st)
         return db is not None
-    if _wino_wgrad_ok(g, x, dy, dw, dys):
+    if _wino_wgrad_ok(g, x if lazy is None else lazy.x, dy, dw, dys):
         # Winograd F(3x3, 2x2): dW = G^T [sum_tiles (A D A^T) (.) (B^T X B)] G (csrc/winograd.hip); the bias gradient is
         # left to the caller
-        mt = WINOGRAD_TILE
+        mt = _wtile()
         pos = (mt + 2) ** 2
         dev = dy.device
         dya = dys if dys is not None else dy
@@ -992,9 +1059,6 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         for i, (b0, b1) in enumerate(_wino_chunks(n, h, wd, max(c, co))):
             nb, t = b1 - b0, _wino_tiles(b1 - b0, h, wd)
             v = kept.get((b0, b1))
-            if v is None and getattr(x, GN_LAZY_ATTR, None) is not None:
-                raise RuntimeError("conv2d wgrad: a deferred GroupNorm input needs the forward's kept Winograd "
-                                   "transform")
             dt = kept_d.get((b0, b1))
             m = ARENA.get("wino_mw", 4 * pos * co * c, dev)
             ws = ARENA.get("ws", _lib.query("mvae_gemm_workspace_bytes", co, c, t, pos), dev)
@@ -1002,7 +1066,11 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
                 dt = ARENA.get("wino_d", 4 * pos * t * co, dev)
                 _lib.call("mvae_winograd_dy_transform", dya[b0:b1].data_ptr(), dt.data_ptr(), nb, h, wd, co,
                           int(dys is not None), mt, st)
-            if v is None:
+            if v is None and lazy is not None:  # (the kept V is gone -- a second backward: re-derived, normalized on load)
+                v = ARENA.get("wino_v", 4 * pos * t * c, dev)
+                _lib.call("mvae_winograd_input_transform_gn", lazy.x[b0:b1].data_ptr(), lazy.scale[b0 * c:].data_ptr(),
+                          lazy.shift[b0 * c:].data_ptr(), lazy.silu, v.data_ptr(), nb, h, wd, c, mt, st)
+            elif v is None:
                 v = ARENA.get("wino_v", 4 * pos * t * c, dev)
                 _lib.call("mvae_winograd_input_transform", x[b0:b1].data_ptr(), v.data_ptr(), nb, h, wd, c,
                           int(x_split), mt, st)
@@ -1121,6 +1189,7 @@ def _bwd_side(t: torch.Tensor):
         if torch.cuda.is_current_stream_capturing():
             return None
         side = _SIDE[t.device] = (torch.cuda.Stream(t.device), torch.cuda.Event(), torch.cuda.Event())
+        _SIDE_STREAMS.add(side[0].cuda_stream)
     return side
 
 
@@ -1141,7 +1210,9 @@ def _overlap_ok(x, dy, g) -> bool:
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, geom: ConvGeom, res_sink=None, x_sink=None, gn_part=None,
-                gn_link=None, dypack=None):
+                gn_link=None, dypack=None, grad_on: bool = True):
+        """grad_on: grad mode at the call (inside forward it is always off): no kept Winograd transform for a conv
+        that will have no backward (eval / validation under torch.no_grad)."""
         _check(x, "conv input")
         xs = bool(getattr(x, XSPLIT_ATTR, False))
         xb16 = bool(getattr(x, BF16_ATTR, False))
@@ -1150,13 +1221,15 @@ class Conv2dFn(torch.autograd.Function):
             raise RuntimeError("conv2d: a pre-split / packed input must not be re-laid out")
         w = _krsc(weight)
         res = nhwc(residual) if residual is not None else None
-        if lazy is not None and not _lazy_wino(lazy, x, w, bias, res, geom, gn_part, weight.requires_grad):
+        want_w = bool(weight.requires_grad and grad_on)
+        if lazy is not None and not _lazy_wino(lazy, x, w, bias, res, geom, gn_part, want_w):
             x, lazy = lazy.materialize(), None  # (the conv cannot normalize on load: the GroupNorm output is written)
         if lazy is None:
             x = nhwc(x)
-        keep = [] if (WINOGRAD_KEEP_V or lazy is not None) and weight.requires_grad else None
+        keep = [] if (WINOGRAD_KEEP_V or lazy is not None) and want_w else None
         y = conv2d_forward_raw(x, w, bias, res, geom, xs, gn_part, x_bf16=xb16, keep_v=keep, lazy=lazy)
         ctx.wino_v = keep if keep else None
+        ctx.lazy = lazy  # (the weight gradient re-derives V from it if the kept one is gone: a second backward)
         ctx.math = _MATH[0]  # the backward GEMMs run in the forward's arithmetic
         ctx.geom = geom
         ctx.x_split = xs
@@ -1226,17 +1299,18 @@ class Conv2dFn(torch.autograd.Function):
             btgt = _main_grad(ctx.bias_ref) if want_b and not bias_done else None
             want_b_w = want_b and not bias_done
             xs, xb16 = ctx.x_split, ctx.x_bf16
+            lz = ctx.lazy
             if tgt is not None and (not want_b_w or btgt is not None):
                 fused = conv2d_wgrad_raw(dy, x, tgt, 1.0, g, btgt, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16,
-                                         wino_v=ctx.wino_v, wino_d=dkeep)
+                                         wino_v=ctx.wino_v, wino_d=dkeep, lazy=lz)
                 bias_done = bias_done or fused
             elif tgt is not None:
                 conv2d_wgrad_raw(dy, x, tgt, 1.0, g, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16, wino_v=ctx.wino_v,
-                                 wino_d=dkeep)
+                                 wino_d=dkeep, lazy=lz)
             else:
                 dw_ret = torch.empty_like(w, memory_format=CL)
                 conv2d_wgrad_raw(dy, x, dw_ret, 0.0, g, x_split=xs, dys=dys, dyb=dyb, x_bf16=xb16,
-                                 wino_v=ctx.wino_v, wino_d=dkeep)
+                                 wino_v=ctx.wino_v, wino_d=dkeep, lazy=lz)
 
         side = _bwd_side(dy) if ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and \
             _main_grad(ctx.weight_ref) is not None and _overlap_ok(x, dy, g) else None
@@ -1282,7 +1356,7 @@ class Conv2dFn(torch.autograd.Function):
             _grad_done(ctx.weight_ref)
         if want_b and db_ret is None:
             _grad_done(ctx.bias_ref)
-        return dx, dw_ret, db_ret, dres, None, None, None, None, None, None
+        return dx, dw_ret, db_ret, dres, None, None, None, None, None, None, None
 
 
 # The GroupNorm statistics of a conv output emitted by its GEMM epilogue travel with the output tensor
@@ -1312,14 +1386,18 @@ def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink
     if link is not None and not link.matches(x):
         link = None
     dyp = None
-    if gn_stats and DYPACK and _dma_fmt() == 2 and not geom.pointwise and weight.shape[0] % 8 == 0 and \
+    # (a Winograd conv of the bf16-mixed mode reads dy in fp32 or 3xBF16-split form, not packed: the GroupNorm backward
+    # writes it split, as in the 3xBF16 mode)
+    wino_bf16 = _MATH[0] == 1 and x.dim() == 4 and _wino_ok(geom, x.shape[0], x.shape[2], x.shape[3], x.shape[1],
+                                                             weight.shape[0])
+    if gn_stats and DYPACK and _dma_fmt() == 2 and not wino_bf16 and not geom.pointwise and weight.shape[0] % 8 == 0 and \
             geom.kh * geom.kw <= 32 and torch.is_grad_enabled():
         dyp = DyPack(bias)
-    elif gn_stats and DYSPLIT and _dma_fmt() == 0 and _MATH[0] == 0 and not geom.pointwise and \
+    elif gn_stats and DYSPLIT and ((_dma_fmt() == 0 and _MATH[0] == 0) or wino_bf16) and not geom.pointwise and \
             not _subpixel_upsample(geom) and weight.shape[0] % 4 == 0 and geom.kh * geom.kw <= 32 and \
             torch.is_grad_enabled() and _conv_macs(x, weight, geom) >= DYSPLIT_MIN_MACS:
         dyp = DyPack(bias, split=True)
-    y = Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink, part, link, dyp)
+    y = Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink, part, link, dyp, torch.is_grad_enabled())
     if part is not None:
         setattr(y, GN_PART_ATTR, (part, y._version))
     if dyp is not None:
@@ -1387,7 +1465,8 @@ class GroupNormFn(torch.autograd.Function):
                 _lib.call("mvae_group_norm_stats_nhwc", x.data_ptr(), _ptr(part), gamma.data_ptr(), beta.data_ptr(),
                           mean.data_ptr(), rstd.data_ptr(), lazy.scale.data_ptr(), lazy.shift.data_ptr(), n, h * w, c,
                           groups, float(eps), ws.data_ptr(), ws.numel(), _stream(x))
-            y = torch.full((1,), float("nan"), device=x.device).expand(n, c, h, w)  # (never read on this path)
+            # (group_norm hands it on as a DeferredGnOutput: never read, any read raises)
+            y = torch.full((1,), float("nan"), device=x.device).expand(n, c, h, w)
         else:
             y = torch.empty_like(x, memory_format=CL)
             with _timed("gn_fwd", 8.0 * x.numel(), (n, c, h * w)):  # algorithmic HBM bytes: read x, write y
@@ -1491,7 +1570,8 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
     the ResnetBlock / norm_out pattern, encoder_decoder.py:141-163, :318-328); in the bf16-mixed mode, with a known
     output channel count that is a multiple of 8, packed bf16 for the LDS-DMA GEMM."""
     packed = bool(for_conv and not isinstance(for_conv, bool) and int(for_conv) % 8 == 0 and _bf16_dma() and
-                  x.shape[1] % 8 == 0 and _al16(x) and _dma_ok(9.0 * x.numel() * int(for_conv)))
+                  x.shape[1] % 8 == 0 and _al16(x) and _dma_ok(9.0 * x.numel() * int(for_conv)) and
+                  not (x.dim() == 4 and _wino_ok(G3, x.shape[0], x.shape[2], x.shape[3], x.shape[1], int(for_conv))))
     split = _dma_fmt() if packed else int(bool(for_conv and ACT_SPLIT and _splits_ok() and not _bf16_dma() and
                                                 x.shape[1] % 4 == 0))
     part = getattr(x, GN_PART_ATTR, None)
@@ -1514,6 +1594,7 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
         dyp = dyp[0] if dyp[1] == x._version and x.is_contiguous(memory_format=CL) and _al16(x) else None
     y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink, part, link, dyp, lazy)
     if lazy is not None:
+        y = y.as_subclass(DeferredGnOutput)  # (same autograd node; any read of its values raises)
         setattr(y, GN_LAZY_ATTR, lazy)
     elif split >= 2:
         setattr(y, BF16_ATTR, True)

@@ -226,3 +226,110 @@ def test_dp_graphed_step_matches_eager_dp_step():
         assert torch.equal(r["graphed"]["losses"], r["eager"]["losses"])
         assert torch.equal(r["graphed"]["steps"], r["eager"]["steps"])
     assert torch.equal(r0["graphed"]["params"], r1["graphed"]["params"])
+
+
+# a ConditionalVAE of the c4 family (concat conditioning, attention, 3 levels) small enough for 4 ranks on one card; the
+# workers and the single-process reference force the Winograd convs (the c4 bench's conv form) onto its 3x3 convs
+CKW = dict(input_channels=3, latent_dim=8, hidden_channels=32, ch_mult=(1, 2, 4), num_res_blocks=1, attn_resolutions=[8],
+           dropout=0.0, resolution=32, condition_method="concat")
+WINO_ENV = {"MVAE_WINOGRAD_MIN_C": "32", "MVAE_WINOGRAD_MIN_C_WIDE": "32", "MVAE_WINOGRAD_MIN_MACS": "0"}
+
+
+def _cdata(n=8):
+    g = torch.Generator().manual_seed(21)
+    x = torch.rand(n, 3, 32, 32, generator=g) * 2 - 1
+    eps = torch.randn(2, n, 8, 8, 8, generator=g)  # one draw per step
+    oh = torch.nn.functional.one_hot(torch.arange(n) % 12, 12).float()
+    return x, eps, oh
+
+
+def _cmodule(dev):
+    import medvae_disentangled_multimodal_amd as M
+    torch.manual_seed(5)
+    model = M.ConditionalVAE(**CKW).to(dev)
+    mod = M.VAELightningModule(model, {"type": "adamw", "lr": 1e-3, "weight_decay": 1e-5, "betas": [0.5, 0.999]},
+                               {"type": "none"}, {"type": "vae"}, gradient_clip_val=1.0)
+    mod.configure_optimizers()
+    return mod
+
+
+def _worker4(rank, world, init_file, out_file):
+    os.environ.update(WINO_ENV)  # (before the package is imported: its dispatch rules read them at import)
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    from medvae_disentangled_multimodal_amd import _lib, ddp, ops
+    dev = torch.device("cuda:0")
+    mod = _cmodule(dev)
+    dp = ddp.DataParallel(mod, bucket_bytes=256 << 10)
+    seen = set()
+    orig = _lib.call
+
+    def spy(name, *args):
+        seen.add(name)
+        return orig(name, *args)
+    _lib.call = spy
+    x, eps, oh = _cdata()
+    b = x.shape[0] // world
+    sl = slice(b * rank, b * rank + b)
+    batch = (x[sl].to(dev), torch.zeros(b, 1, dtype=torch.long, device=dev), oh[sl].to(dev))
+    mod.fit_step(batch, 0, eps=eps[0, sl].to(dev))
+    grad = (mod.flat.grad * mod.optimizer.grad_scale).cpu()
+    p1 = mod.flat.data.cpu()
+    mod.fit_step(batch, 1, eps=eps[1, sl].to(dev))
+    torch.cuda.synchronize()
+    _lib.call = orig
+    torch.save({"grad": grad, "p1": p1, "p2": mod.flat.data.cpu(), "scale": float(mod.optimizer.grad_scale),
+                "nb": len(dp.buckets), "wino": "mvae_winograd_wgrad_gemm" in seen,
+                "steps": mod.optimizer.steps.cpu()}, f"{out_file}.{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_four_ranks_real_hip_step(monkeypatch):
+    """4 data-parallel ranks on the one card (gloo collectives, the HIP step of a c4-family ConditionalVAE with its 3x3
+    convs on the Winograd form): the gradient scale is 1/4, the replicas stay bitwise identical over two fused AdamW
+    steps, the averaged gradient of 4 x 2 images equals the single-process gradient of the concatenated 8 within 1e-3,
+    and the parameters after each step equal the single-process steps' (elements with a real gradient to 1e-4 of the
+    update; Adam's sign-noise elements within one step size -- see the 2-rank test)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    world = 4
+    with tempfile.TemporaryDirectory() as d:
+        init_file, out = os.path.join(d, "init"), os.path.join(d, "out")
+        ctx = mp.get_context("spawn")
+        procs = [ctx.Process(target=_worker4, args=(r, world, init_file, out)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=300)
+        assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+        rs = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    assert all(r["scale"] == 0.25 and r["wino"] and r["nb"] > 1 for r in rs)
+    for r in rs[1:]:
+        assert torch.equal(r["p1"], rs[0]["p1"]) and torch.equal(r["p2"], rs[0]["p2"])
+        assert torch.equal(r["steps"], rs[0]["steps"])
+
+    from medvae_disentangled_multimodal_amd import ops
+    for k, v in WINO_ENV.items():
+        monkeypatch.setattr(ops, k[5:], float(v) if "MACS" in k else int(v))
+    dev = torch.device("cuda:0")
+    mod = _cmodule(dev)
+    x, eps, oh = _cdata()
+    batch = (x.to(dev), torch.zeros(8, 1, dtype=torch.long, device=dev), oh.to(dev))
+    p0 = mod.flat.data.cpu().double()
+    mod.fit_step(batch, 0, eps=eps[0].to(dev))
+    ref = mod.flat.grad.cpu().double()
+    assert float((rs[0]["grad"].double() - ref).norm() / ref.norm()) < 1e-3
+    single1 = mod.flat.data.cpu().double()
+    mod.fit_step(batch, 1, eps=eps[1].to(dev))
+    torch.cuda.synchronize()
+    single2 = mod.flat.data.cpu().double()
+    lr = mod.optimizer.param_groups[0]["lr"]
+    signal = torch.zeros_like(ref, dtype=torch.bool)
+    for prm, off in zip(mod.flat.params, mod.flat.offsets):
+        gg = ref[off:off + prm.numel()]
+        signal[off:off + prm.numel()] = gg.abs() > 1e-3 * gg.abs().max()
+    assert float(signal.double().mean()) > 0.9
+    for dp_p, single, base, steps in ((rs[0]["p1"].double(), single1, p0, 1), (rs[0]["p2"].double(), single2, p0, 2)):
+        upd = single - base
+        assert float((dp_p - single)[signal].norm() / upd[signal].norm()) < 1e-4 * 10 ** (steps - 1)
+        assert float((dp_p - single).abs().max()) <= 2 * steps * lr * 1.001

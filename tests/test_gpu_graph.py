@@ -130,3 +130,34 @@ def test_graph_key_covers_optimizer_hyperparameters(dev):
     mod.optimizer.max_grad_norm = 2.0
     mod.fit_step_graphed(batch, 4)
     assert mod._graph["graph"] is not g2
+
+
+def test_failed_capture_falls_back_with_the_step_count_intact(dev, monkeypatch):
+    """A capture that fails after the recorded fit_step advanced the host step counter (here: at capture_end) leaves
+    the counter where it was, runs the step eagerly and stays eager for that key; an error of the step itself (not a
+    capture error) propagates."""
+    cls, kw, loss = CASES[1]
+    mod = _module(cls, kw, loss, dev)
+    batch = _batch(cls, dev)
+    mod.fit_step(batch, 0)
+    assert mod.global_step_count == 1
+
+    orig = torch.cuda.CUDAGraph.capture_end
+
+    def boom(self, *a, **k):  # (the capture itself ends, so the stream leaves capture mode, then the failure)
+        orig(self, *a, **k)
+        raise RuntimeError("hipErrorStreamCaptureInvalidated: capture failed (test)")
+
+    monkeypatch.setattr(torch.cuda.CUDAGraph, "capture_end", boom)
+    with pytest.warns(UserWarning, match="capture failed"):
+        mod.fit_step_graphed(batch, 1)
+    assert mod.global_step_count == 2  # one eager step, not one plus the recorded one
+    assert getattr(mod, "_graph", None) is None
+    mod.fit_step_graphed(batch, 2)  # (same key: eager without another capture attempt)
+    assert mod.global_step_count == 3
+    monkeypatch.undo()
+    torch.cuda.synchronize()
+
+    from medvae_disentangled_multimodal_amd import lightning_module as LM
+    assert LM._is_capture_error(RuntimeError("operation not permitted when stream is capturing"))
+    assert not LM._is_capture_error(RuntimeError("conv2d: a pre-split input needs cin % 4 == 0"))

@@ -188,16 +188,29 @@ def test_state_dict_roundtrip_and_names():
         assert torch.equal(sd[k], ref[k]), k
 
 
+@pytest.mark.parametrize("wino", [False, True], ids=["direct", "winograd"])
 @pytest.mark.parametrize("name", ["cvae_c4_full", "beta_c2_full", "dis_c3_b16", "base_c1_full"])
-def test_training_step_exact_fp32_matches_reference(name):
+def test_training_step_exact_fp32_matches_reference(name, wino, monkeypatch):
     """The trainer's "32-exact" precision (every conv / bmm on the f32-input MFMA, no operand rounding -- the
     arithmetic of the bench's c4x line) against the reference at the exact BASELINE architectures: outputs, loss
     terms, the global gradient norm and the selected full gradients, 1e-4 relative (only the summation order
-    differs from the reference's CPU fp32)."""
+    differs from the reference's CPU fp32). winograd: the F(4x4, 3x3) convs the c4x bench runs at B = 256 forced on at
+    the golden B = 2 (fp32 transforms, bit-split GEMM operands: ~5e-7 per conv)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import medvae_disentangled_multimodal_amd as M
-    from medvae_disentangled_multimodal_amd import ops
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    seen = set()
+    if wino:
+        if name not in ("cvae_c4_full", "beta_c2_full", "base_c1_full"):
+            pytest.skip("no Winograd-eligible conv (the channel floor) in this architecture")
+        monkeypatch.setattr(ops, "WINOGRAD_MIN_MACS", 0.0)
+        orig = _lib.call
+
+        def spy(fn, *args):
+            seen.add(fn)
+            return orig(fn, *args)
+        monkeypatch.setattr(_lib, "call", spy)
     dev = torch.device("cuda:0")
     meta, data = load_case(name)
     case = CASES[name]
@@ -231,3 +244,5 @@ def test_training_step_exact_fp32_matches_reference(name):
     for k in FULL_GRADS[name]:
         g = mod.flat.params[names.index(k)]._mvae_main_grad.cpu()
         assert rel_err(g, data[f"grad.{k}"]) < 10 * tol, (k, rel_err(g, data[f"grad.{k}"]))
+    if wino:
+        assert {"mvae_winograd_gemm", "mvae_winograd_wgrad_gemm", "mvae_winograd_input_transform_gn"} <= seen

@@ -437,3 +437,240 @@ def test_winograd_image_chunks(dev, monkeypatch, _wino_on):
     assert rel(part, _stats64(y.detach().double().cpu())) < 1e-9
     for a, ref in ((x.grad, xr.grad), (wt.grad, wr.grad), (b.grad, br.grad)):
         assert rel(a, ref) < CONV_TOL
+
+
+def _deferred_gn(dev, monkeypatch, n=2, c=64, co=64, h=16, w=16, seed=4):
+    from medvae_disentangled_multimodal_amd import ops
+    g = torch.Generator().manual_seed(seed)
+    x0 = torch.randn(n, c, h, w, generator=g)
+    g0, b0 = torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1
+    w0 = torch.randn(co, c, 3, 3, generator=g) / (3 * c ** 0.5)
+    dy0 = torch.randn(n, co, h, w, generator=g)
+    monkeypatch.setattr(ops, "WINOGRAD_GN", True)
+    x = cl(x0, dev).requires_grad_(True)
+    gam, bet = g0.to(dev).requires_grad_(True), b0.to(dev).requires_grad_(True)
+    wt = w0.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    hgn = ops.group_norm(x, gam, bet, 32, 1e-6, silu=True, for_conv=co)
+    assert isinstance(hgn, ops.DeferredGnOutput) and getattr(hgn, ops.GN_LAZY_ATTR, None) is not None
+    return (x0, g0, b0, w0, dy0), (x, gam, bet, wt, hgn)
+
+
+def _ref_grads(x0, g0, b0, w0, dy0):
+    import torch.nn.functional as F
+    xr, gr, br, wr = (t.double().requires_grad_() for t in (x0, g0, b0, w0))
+    yr = F.conv2d(F.silu(F.group_norm(xr, 32, gr, br, eps=1e-6)), wr, None, padding=1)
+    yr.backward(dy0.double())
+    return yr, xr.grad, gr.grad, wr.grad
+
+
+def test_deferred_groupnorm_output_refuses_reads(dev, monkeypatch, _wino_on):
+    """The deferred placeholder is not the GroupNorm's values: any torch op on it raises (a forward hook or user code
+    reading a Normalize output), metadata queries pass, and the consuming conv still runs on it."""
+    from medvae_disentangled_multimodal_amd import ops
+    _, (x, gam, bet, wt, hgn) = _deferred_gn(dev, monkeypatch)
+    assert tuple(hgn.shape) == tuple(x.shape) and hgn.device == x.device and hgn.dtype == torch.float32
+    for read in (lambda t: t.sum(), lambda t: t + 1, lambda t: t.clone(), lambda t: t.cpu(), lambda t: float(t[0, 0, 0, 0]),
+                 lambda t: torch.nn.functional.relu(t), repr):
+        with pytest.raises(RuntimeError, match="deferred"):
+            read(hgn)
+    y = ops.conv2d(hgn, wt, None, ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False))
+    assert not isinstance(y, ops.DeferredGnOutput) and torch.isfinite(y).all()
+
+
+def test_deferred_groupnorm_conv_second_backward(dev, monkeypatch, _wino_on):
+    """retain_graph: the second backward through a deferred-GroupNorm Winograd conv (whose kept V the first one released)
+    re-derives V from the GroupNorm input and gives the same gradients again."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    (x0, g0, b0, w0, dy0), (x, gam, bet, wt, hgn) = _deferred_gn(dev, monkeypatch)
+    y = ops.conv2d(hgn, wt, None, ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False))
+    dy = cl(dy0, dev)
+    y.backward(dy, retain_graph=True)
+    torch.cuda.synchronize()
+    first = [t.grad.clone() for t in (x, gam, wt)]
+    for t in (x, gam, bet, wt):
+        t.grad = None
+    seen = []
+    orig = _lib.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return orig(name, *args)
+    monkeypatch.setattr(_lib, "call", spy)
+    y.backward(dy)
+    torch.cuda.synchronize()
+    monkeypatch.setattr(_lib, "call", orig)
+    assert "mvae_winograd_input_transform_gn" in seen  # V re-derived, normalized on load
+    for a, b in zip((x.grad, gam.grad, wt.grad), first):
+        assert rel(a, b) < 1e-6
+    yr, xg, gg, wg = _ref_grads(x0, g0, b0, w0, dy0)
+    for a, b in ((y, yr), (x.grad, xg), (gam.grad, gg), (wt.grad, wg)):
+        assert rel(a, b) < CONV_TOL
+
+
+def test_deferred_groupnorm_weight_gradient_off_winograd(dev, monkeypatch, _wino_on):
+    """The Winograd weight gradient switched off between forward and backward: the weight gradient writes the
+    GroupNorm output (mvae_group_norm_apply_nhwc) and runs the implicit GEMM on it -- never on the placeholder."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    (x0, g0, b0, w0, dy0), (x, gam, bet, wt, hgn) = _deferred_gn(dev, monkeypatch)
+    y = ops.conv2d(hgn, wt, None, ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False))
+    monkeypatch.setattr(ops, "WINOGRAD_WGRAD", False)
+    seen = []
+    orig = _lib.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return orig(name, *args)
+    monkeypatch.setattr(_lib, "call", spy)
+    y.backward(cl(dy0, dev))
+    torch.cuda.synchronize()
+    monkeypatch.setattr(_lib, "call", orig)
+    assert "mvae_group_norm_apply_nhwc" in seen and "mvae_winograd_wgrad_gemm" not in seen
+    yr, xg, gg, wg = _ref_grads(x0, g0, b0, w0, dy0)
+    for a, b in ((y, yr), (x.grad, xg), (gam.grad, gg), (wt.grad, wg)):
+        assert rel(a, b) < CONV_TOL
+
+
+def test_no_kept_transform_under_no_grad(dev, monkeypatch, _wino_on):
+    """Under torch.no_grad (validation) a Winograd conv keeps no input transform for a backward that never comes."""
+    from medvae_disentangled_multimodal_amd import ops
+    g = torch.Generator().manual_seed(9)
+    x = cl(torch.randn(2, 64, 16, 16, generator=g), dev)
+    wt = (torch.randn(64, 64, 3, 3, generator=g) / 24).to(dev).contiguous(memory_format=torch.channels_last)
+    wt.requires_grad_(True)
+    kept = []
+    orig = ops._winograd
+
+    def spy(*a, **k):
+        kept.append(k.get("keep") if len(a) < 11 else a[10])
+        return orig(*a, **k)
+    monkeypatch.setattr(ops, "_winograd", spy)
+    with torch.no_grad():
+        ops.conv2d(x, wt, None, ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False))
+    assert kept and all(k is None for k in kept)
+    ops.conv2d(x, wt, None, ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False))
+    assert kept[-1] is not None
+
+
+ARITH_CASES = [(2, 64, 64, 8, 8), (3, 128, 64, 16, 16), (2, 64, 32, 8, 32), (3, 64, 64, 7, 7), (1, 32, 64, 12, 64),
+               (2, 512, 256, 8, 8)]
+
+
+def _conv_fwd_bwd(dev, x0, w0, b0, dy0, prec, monkeypatch, r0=None):
+    """ops.conv2d forward (+ bias, + residual) and backward in arithmetic `prec`, recording the library calls."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    seen = []
+    orig = _lib.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return orig(name, *args)
+    x = cl(x0, dev).requires_grad_(True)
+    wt = w0.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    b = b0.to(dev).requires_grad_(True)
+    monkeypatch.setattr(_lib, "call", spy)
+    prev = ops.set_precision(prec)
+    try:
+        y = ops.conv2d(x, wt, b, ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False),
+                       residual=cl(r0, dev) if r0 is not None else None)
+        y.backward(cl(dy0, dev))
+        torch.cuda.synchronize()
+    finally:
+        ops.restore_math_mode(prev)
+        monkeypatch.setattr(_lib, "call", orig)
+    assert {"mvae_winograd_gemm", "mvae_winograd_wgrad_gemm", "mvae_winograd_wgrad_output"} <= set(seen)
+    assert "mvae_conv2d_nhwc" not in seen and "mvae_conv2d_wgrad_nhwc" not in seen
+    return y.detach().cpu(), x.grad.cpu(), wt.grad.cpu(), b.grad.cpu()
+
+
+@pytest.mark.parametrize("n,ci,co,h,w", ARITH_CASES)
+def test_winograd_exact_fp32(dev, n, ci, co, h, w, monkeypatch, _wino_on):
+    """The exact-fp32 arithmetic ("32-exact", the c4x line) on the Winograd form: V / U / D' written as a bit split the
+    f32-input MFMA reassembles exactly, so the result differs from float64 only by the transforms' fp32 rounding
+    (simulated: F(4x4) ~5e-7, F(2x2) ~8e-8; the direct fp32 conv ~4e-8). Forward with bias and residual, input gradient,
+    weight gradient and bias gradient against float64 at 5e-6 -- 40x inside the 3xBF16 bar."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(n * ci + co + 7 * h + w)
+    x0 = torch.randn(n, ci, h, w, generator=g)
+    w0 = torch.randn(co, ci, 3, 3, generator=g) / (3 * ci ** 0.5)
+    b0, r0 = torch.randn(co, generator=g), torch.randn(n, co, h, w, generator=g)
+    dy0 = torch.randn(n, co, h, w, generator=g)
+    y, dx, dw, db = _conv_fwd_bwd(dev, x0, w0, b0, dy0, "32-exact", monkeypatch, r0)
+    xr, wr, br = (t.double().requires_grad_() for t in (x0, w0, b0))
+    yr = F.conv2d(xr, wr, br, padding=1) + r0.double()
+    yr.backward(dy0.double())
+    for a, ref in ((y, yr), (dx, xr.grad), (dw, wr.grad), (db, br.grad)):
+        assert rel(a, ref) < 5e-6
+
+
+@pytest.mark.parametrize("n,ci,co,h,w", ARITH_CASES)
+def test_winograd_bf16_matches_emulation(dev, n, ci, co, h, w, monkeypatch, _wino_on):
+    """The bf16-mixed arithmetic on the Winograd form (c5): the GEMM multiplies V, U (and D') rounded to bf16 in the
+    transform domain, so it is checked against the float64 emulation of exactly that algorithm (tests/wino_ref.py:
+    the same transforms, the GEMM operands rounded to bf16 RNE) -- only fp32 accumulation / transform rounding differ,
+    2e-4 -- and against the float64 conv at the algorithm's own bf16 error (m = 2 ~4e-3, m = 4 ~3e-2)."""
+    import torch.nn.functional as F
+    import wino_ref as W
+    from medvae_disentangled_multimodal_amd import ops
+    monkeypatch.setattr(ops, "WINOGRAD_TILE_BF16", _wino_on)
+    monkeypatch.setattr(ops, "WINOGRAD_BF16_MAX_W", 64)
+    g = torch.Generator().manual_seed(n * ci + co + 5 * h + w)
+    x0 = torch.randn(n, ci, h, w, generator=g)
+    w0 = torch.randn(co, ci, 3, 3, generator=g) / (3 * ci ** 0.5)
+    b0 = torch.randn(co, generator=g)
+    dy0 = torch.randn(n, co, h, w, generator=g)
+    y, dx, dw, db = _conv_fwd_bwd(dev, x0, w0, b0, dy0, "bf16-mixed", monkeypatch)
+    m = _wino_on
+    ye = W.conv(x0, w0, m, W.bf16) + b0.double().view(1, -1, 1, 1)
+    dxe = W.conv(dy0, W.dgrad_weights(w0), m, W.bf16)
+    dwe = W.wgrad(x0, dy0, m, W.bf16)
+    for a, ref in ((y, ye), (dx, dxe), (dw, dwe)):
+        assert rel(a, ref) < 2e-4
+    assert rel(db, dy0.double().sum((0, 2, 3))) < 1e-5
+    xr, wr = x0.double().requires_grad_(), w0.double().requires_grad_()
+    yr = F.conv2d(xr, wr, b0.double(), padding=1)
+    yr.backward(dy0.double())
+    bar = 1e-2 if m == 2 else 6e-2
+    for a, ref in ((y, yr), (dx, xr.grad), (dw, wr.grad)):
+        assert rel(a, ref) < bar
+
+
+def test_winograd_exact_fp32_groupnorm_on_load_and_chunks(dev, monkeypatch, _wino_on):
+    """The exact arithmetic through the GroupNorm-on-load transform and over image chunks (5 images in chunks of
+    2 / 2 / 1 under a small descriptor limit): every gradient against float64 at 5e-6."""
+    import torch.nn.functional as F
+    from medvae_disentangled_multimodal_amd import ops
+    n, c, co, h, w = 5, 64, 64, 8, 16
+    per_img = (_wino_on + 2) ** 2 * ops._wino_tiles(1, h, w) * c * 4
+    monkeypatch.setattr(ops, "_MAX_DESC_BYTES", 2 * per_img)
+    g = torch.Generator().manual_seed(77)
+    x0 = torch.randn(n, c, h, w, generator=g) * 1.3 + 0.2
+    g0, b0 = torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1
+    w0 = torch.randn(co, c, 3, 3, generator=g) / (3 * c ** 0.5)
+    cb0 = torch.randn(co, generator=g)
+    dy0 = torch.randn(n, co, h, w, generator=g)
+    prev = ops.set_precision("32-exact")
+    try:
+        fused, seen = _gn_conv_step(dev, x0, g0, b0, w0, cb0, dy0, 32, monkeypatch, WINOGRAD_GN=True)
+    finally:
+        ops.restore_math_mode(prev)
+    assert seen.count("mvae_winograd_input_transform_gn") == 3 and "mvae_group_norm_apply_nhwc" not in seen
+    xr = x0.double().requires_grad_()
+    gr, br = g0.double().requires_grad_(), b0.double().requires_grad_()
+    wr, cbr = w0.double().requires_grad_(), cb0.double().requires_grad_()
+    yr = F.conv2d(F.silu(F.group_norm(xr, 32, gr, br, eps=1e-6)), wr, cbr, padding=1)
+    yr.backward(dy0.double())
+    for a, b in zip(fused, (yr, xr.grad, gr.grad, br.grad, wr.grad, cbr.grad)):
+        assert rel(a, b) < 5e-6
+
+
+def test_winograd_exact_rejects_split_inputs(dev):
+    """A pre-split input is a 3xBF16 value split; the exact mode's transforms refuse one instead of reading it as bits."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    x = torch.zeros(1, 8, 8, 8, device=dev).contiguous(memory_format=torch.channels_last)
+    v = torch.empty(36 * 4 * 8 * 4, dtype=torch.uint8, device=dev)
+    prev = ops.set_precision("32-exact")
+    try:
+        with pytest.raises(RuntimeError, match="exact"):
+            _lib.call("mvae_winograd_input_transform", x.data_ptr(), v.data_ptr(), 1, 8, 8, 8, 1, 4, ops._stream(x))
+    finally:
+        ops.restore_math_mode(prev)

@@ -39,9 +39,19 @@ def test_c4_levels(rules):
 def test_small_batches_and_math_modes(rules):
     assert ops._wino_ok(G3, 256, 7, 7, 512, 512)              # c2's 7x7 level (29.6 GMAC)
     assert not ops._wino_ok(G3, 32, 7, 7, 512, 512)           # c1 at B = 32 (3.7 GMAC): below MIN_MACS
-    ops._MATH[0] = 1                                          # bf16-mixed: never
+    rules.setattr(ops, "WINOGRAD_TILE_BF16", 2)
+    rules.setattr(ops, "WINOGRAD_BF16_MAX_W", 16)
+    ops._MATH[0] = 1                                          # bf16-mixed (c5): F(2x2) at the small wide levels only
+    assert ops._wtile() == 2 and ops._wino_alg(36.0) == pytest.approx(16.0)
+    assert ops._wino_ok(G3, 256, 8, 8, 2048, 2048) and ops._wino_ok(G3, 256, 16, 16, 1024, 1024)
+    assert not ops._wino_ok(G3, 256, 32, 32, 512, 512) and not ops._wino_ok(G3, 256, 64, 64, 256, 256)
+    assert ops._wino_chunks(256, 16, 16, 1024) == [(0, 256)]  # (F2: 16 x 16,384 tiles x 1024 x 4 B = 1.07 GB)
+    rules.setattr(ops, "WINOGRAD_BF16", False)
     assert not ops._wino_ok(G3, 256, 8, 8, 2048, 2048)
-    ops._MATH[0] = 2                                          # exact fp32: never
+    ops._MATH[0] = 2                                          # exact fp32 (c4x): F(4x4) at every c4 level
+    assert ops._wtile() == 4
+    assert ops._wino_ok(G3, 256, 8, 8, 2048, 2048) and ops._wino_ok(G3, 256, 64, 64, 512, 256)
+    rules.setattr(ops, "WINOGRAD_EXACT", False)
     assert not ops._wino_ok(G3, 256, 8, 8, 2048, 2048)
 
 
