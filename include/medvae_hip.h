@@ -345,6 +345,17 @@ int mvae_group_norm_bwd_part_nhwc(const float* x, const float* dy, const double*
                                   const float* beta, const float* mean, const float* rstd, float* dx,
                                   const float* dx_add, float* dgamma, float* dbeta, int nb, int hw, int c, int groups,
                                   int silu, void* workspace, size_t workspace_bytes, void* stream);
+/* ... with dx also written split4_bf16 and the producing conv's bias gradient (mvae_group_norm_bwd_split_nhwc's
+ * outputs; the partials from the Winograd input-gradient output transform, mvae_winograd_output_gnbwd). */
+int mvae_group_norm_bwd_part_split_nhwc(const float* x, const float* dy, const double* part, const float* gamma,
+                                        const float* beta, const float* mean, const float* rstd, float* dx,
+                                        const float* dx_add, float* dgamma, float* dbeta, int nb, int hw, int c,
+                                        int groups, int silu, void* workspace, size_t workspace_bytes, void* dx_split,
+                                        float* dbias, float bias_beta, void* cs_workspace, size_t cs_workspace_bytes,
+                                        void* stream);
+/* 1 when the GroupNorm backward of this geometry (with_dxp: its split / packed-output forms) runs the two-pass
+ * streaming chain, whose partial pass the consuming conv can supply; 0 for the one-pass resident / unit kernels. */
+int mvae_group_norm_bwd_streaming(int nb, int hw, int c, int groups, int with_dxp);
 /* mvae_group_norm_fwd_nhwc from the statistics the producing convolution emitted
  * (mvae_conv2d_gnstats_nhwc, part = [nb*hw/32][c/4][2] fp64): skips the statistics pass over x.
  * hw % 32 == 0, (c / groups) % 4 == 0. */

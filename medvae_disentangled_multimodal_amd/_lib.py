@@ -77,6 +77,9 @@ SIGNATURES = {
     "mvae_group_norm_fwd_part_nhwc": (I, [P, P, P, P, P, P, P, I, I, I, I, F, I, F, c_uint64, I, P, Z, P]),
     "mvae_group_norm_bwd_nhwc": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, c_uint64, P, Z, P]),
     "mvae_group_norm_bwd_part_nhwc": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P, Z, P]),
+    "mvae_group_norm_bwd_part_split_nhwc": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P, Z, P, P, F, P, Z,
+                                               P]),
+    "mvae_group_norm_bwd_streaming": (I, [I, I, I, I, I]),
     "mvae_group_norm_workspace_bytes": (Z, [I, I, I]),
     "mvae_group_norm_bwd_pack_nhwc": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, c_uint64, P, Z, P, P, F, P, Z,
                                           P]),

@@ -1010,8 +1010,9 @@ struct DmaColShape {
   static_assert(ROWS >= 64 && NI >= 1 && NI * NT * 8 == ROWS * KT, "DMA COL image shape");
 };
 
-// A = dY^T: element (m, k) at P[k * lda + m]
-template <int ROWS, int NT, int KT>
+// A = dY^T: element (m, k) at P[k * lda + m]; IS_A false: a k-major B operand, element (n, k) at P[k * ldb + n] (the
+// Winograd weight gradient's transformed input V, [tiles][cin])
+template <int ROWS, int NT, int KT, bool IS_A = true>
 struct DmaColK {
   using S = DmaColShape<ROWS, NT, KT>;
   __amdgpu_buffer_rsrc_t rs[2];
@@ -1019,15 +1020,15 @@ struct DmaColK {
   bool cv;
   int kr0, k, K, w;
   __device__ void init(const GemmArgs& a, const __bf16* p, int row0, int kb, int tid, int) {
-    plane_rsrc(rs, p, a.a_bytes, a.a_lo);
+    plane_rsrc(rs, p, IS_A ? a.a_bytes : a.b_bytes, IS_A ? a.a_lo : a.b_lo);
     const int lane = tid & 63;
     w = tid >> 6;
     kr0 = w * S::KPI + lane / S::CPR;
     const int lc = (lane % S::CPR) ^ (dcswz<ROWS>(kr0) >> 3);
     const int col = row0 + lc * 8;
-    cv = col < a.M;
+    cv = col < (IS_A ? a.M : a.N);
     colb = (unsigned)col * 2u;
-    ld2 = (unsigned)a.lda * 2u;
+    ld2 = (unsigned)(IS_A ? a.lda : a.ldb) * 2u;
     k = kb; K = a.K;
   }
   __device__ void prep(const GemmArgs&) {}
@@ -1182,6 +1183,8 @@ template <int ROWS, int NT, int KT>
 struct DmaLoader<A_CONV_SUBPIX, ROWS, NT, true, KT> : DmaConvA<ROWS, NT, MODE_SUBPIX, KT> {};
 template <int ROWS, int NT, int KT>
 struct DmaLoader<A_COLM, ROWS, NT, true, KT> : DmaColK<ROWS, NT, KT> {};
+template <int ROWS, int NT, int KT>
+struct DmaLoader<B_COLN, ROWS, NT, false, KT> : DmaColK<ROWS, NT, KT, false> {};
 // B operands (IS_A false): weights (ROW) and the weight gradient's im2col gathers (COL)
 template <int ROWS, int NT, int KT>
 struct DmaLoader<B_WGRAD_FWD, ROWS, NT, false, KT> : DmaWgradX<ROWS, NT, MODE_FWD, KT> {};
@@ -1350,7 +1353,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm3x_kernel(GemmArgs a) {
     // clock, which no issue order recovers.)
     constexpr int KT = PREC == 5 ? 32 : 64;
     constexpr int NPL = PREC == 5 ? 2 : 1;  // LDS images per operand (hi, lo)
-    constexpr bool ACOL = AK == A_COLM, BCOL = BKIND == B_WGRAD_FWD || BKIND == B_WGRAD_SUBPIX || BKIND == B_WGRAD_P2;
+    constexpr bool ACOL = AK == A_COLM,
+                   BCOL = BKIND == B_WGRAD_FWD || BKIND == B_WGRAD_SUBPIX || BKIND == B_WGRAD_P2 || BKIND == B_COLN;
     static_assert(ACOL == BCOL && MF == (ACOL ? 32 : 16), "DMA main loop: ROW x ROW (MF 16) or COL x COL (MF 32)");
     using DA = DmaLoader<AK == A_ROWK ? 0 : AK, BM, NT, true, KT>;
     using DB = DmaLoader<BKIND == B_ROWK ? 0 : BKIND, BN, NT, false, KT>;
@@ -2091,7 +2095,8 @@ void launch_dma(GemmArgs& a, hipStream_t st, int cfg) {
 // gemm_dma.hip: launch_dma for AK in {A_ROWK, A_CONV_FWD, A_CONV_DGRAD, A_CONV_SUBPIX} (own translation unit)
 // prec 4: packed bf16 operands; prec 5: planar 3xBF16 operands (hi plane, lo plane a_lo / b_lo bytes later)
 void conv_dma(int ak, GemmArgs& a, hipStream_t st, int cfg, int prec);
-// weight gradient on DMA-staged dY^T (COL) x im2col of X (B_WGRAD_FWD / B_WGRAD_SUBPIX)
+// weight gradient on DMA-staged dY^T (COL) x im2col of X (B_WGRAD_FWD / B_WGRAD_SUBPIX / B_WGRAD_P2), or x a k-major
+// packed operand (B_COLN: the Winograd weight gradient's V)
 void wgrad_dma(int bkind, GemmArgs& a, hipStream_t st, int cfg, int prec);
 
 template <int AK, int VA, int BKIND, int VB>

@@ -37,7 +37,8 @@ void wgrad_dma(int bkind, GemmArgs& a, hipStream_t st, int cfg, int prec) {
     else if (bkind == B_WGRAD_P2) wgrad_dma_cfg<B_WGRAD_P2, 5>(a, st, cfg);
     else wgrad_dma_cfg<B_WGRAD_FWD, 5>(a, st, cfg);
   } else {
-    if (bkind == B_WGRAD_SUBPIX) wgrad_dma_cfg<B_WGRAD_SUBPIX, 4>(a, st, cfg);
+    if (bkind == B_COLN) wgrad_dma_cfg<B_COLN, 4>(a, st, cfg);
+    else if (bkind == B_WGRAD_SUBPIX) wgrad_dma_cfg<B_WGRAD_SUBPIX, 4>(a, st, cfg);
     else if (bkind == B_WGRAD_P2) wgrad_dma_cfg<B_WGRAD_P2, 4>(a, st, cfg);
     else wgrad_dma_cfg<B_WGRAD_FWD, 4>(a, st, cfg);
   }

@@ -1398,10 +1398,62 @@ static int gn_bwd(const float* x, const float* dy, const float* gamma, const flo
 // Backward from the partials emitted by the input-gradient conv that consumed this GroupNorm's output
 // (mvae_conv2d_dgrad_gnbwd_nhwc, part = [nb*hw/32][c][2] fp64 {sum dyn, sum dyn*xhat}): no partial pass over
 // x and dy. No dropout (the fused conv epilogue does not apply a mask).
+static int gn_bwd_part(const float* x, const float* dy, const double* part, const float* gamma, const float* beta,
+                       const float* mean, const float* rstd, float* dx, const float* dx_add, float* dgamma,
+                       float* dbeta, int nb, int hw, int c, int groups, int silu, void* workspace,
+                       size_t workspace_bytes, void* dx_split, float* dbias, float bias_beta, void* cs_ws,
+                       void* stream);
+
 int mvae_group_norm_bwd_part_nhwc(const float* x, const float* dy, const double* part, const float* gamma,
                                   const float* beta, const float* mean, const float* rstd, float* dx,
                                   const float* dx_add, float* dgamma, float* dbeta, int nb, int hw, int c, int groups,
                                   int silu, void* workspace, size_t workspace_bytes, void* stream) {
+  return gn_bwd_part(x, dy, part, gamma, beta, mean, rstd, dx, dx_add, dgamma, dbeta, nb, hw, c, groups, silu,
+                     workspace, workspace_bytes, nullptr, nullptr, 0.f, nullptr, stream);
+}
+
+// as mvae_group_norm_bwd_part_nhwc, with dx also written as split4_bf16 groups and the producing conv's bias gradient
+// (dbias = bias_beta * dbias + column sums of dx) -- mvae_group_norm_bwd_split_nhwc's outputs without its partial pass
+int mvae_group_norm_bwd_part_split_nhwc(const float* x, const float* dy, const double* part, const float* gamma,
+                                        const float* beta, const float* mean, const float* rstd, float* dx,
+                                        const float* dx_add, float* dgamma, float* dbeta, int nb, int hw, int c,
+                                        int groups, int silu, void* workspace, size_t workspace_bytes, void* dx_split,
+                                        float* dbias, float bias_beta, void* cs_workspace, size_t cs_workspace_bytes,
+                                        void* stream) {
+  if (dx_split == nullptr || ((uintptr_t)dx_split & 15) || ((uintptr_t)dx & 15) || ((uintptr_t)x & 15) ||
+      ((uintptr_t)dy & 15) || (dx_add && ((uintptr_t)dx_add & 15)) || (dbias && cs_workspace == nullptr)) {
+    set_error("group_norm_bwd_part_split: 16-B aligned x / dy / dx / split output, a column-sum workspace");
+    return MVAE_EINVAL;
+  }
+  if (dbias && cs_workspace_bytes < mvae_group_norm_colsum_workspace_bytes(nb, hw, c)) {
+    set_error("group_norm_bwd_part_split: column-sum workspace too small");
+    return MVAE_EWORKSPACE;
+  }
+  return gn_bwd_part(x, dy, part, gamma, beta, mean, rstd, dx, dx_add, dgamma, dbeta, nb, hw, c, groups, silu,
+                     workspace, workspace_bytes, dx_split, dbias, bias_beta, cs_workspace, stream);
+}
+
+// 1 when mvae_group_norm_bwd_nhwc (with_dxp = 0) or its split / pack forms (with_dxp = 1) run the two-pass streaming
+// chain (a partial pass over x and dy, then the dx pass) -- the chain whose partial pass the consuming conv's
+// input-gradient epilogue can supply (mvae_group_norm_bwd_part*_nhwc); 0 for the one-pass resident / unit kernels
+int mvae_group_norm_bwd_streaming(int nb, int hw, int c, int groups, int with_dxp) {
+  if (nb <= 0 || hw <= 0 || c <= 0 || (c & 3) || groups <= 0 || c % groups) return 0;
+  static const int bwd_max_it = [] {
+    const char* e = getenv("MVAE_GN_RES_BWD_IT");
+    return e ? std::min(13, atoi(e)) : 13;
+  }();
+  int it = 0;
+  int sc = gn_resident_slab(nb, hw, c, groups, &it, bwd_max_it);
+  if (sc > 0 && sc < 32 && (long long)nb * hw * c * 4 > (64LL << 20)) sc = 0;
+  if (sc) return 0;
+  return (with_dxp || !gn_unit2_slab(hw, c, groups)) ? 1 : 0;
+}
+
+static int gn_bwd_part(const float* x, const float* dy, const double* part, const float* gamma, const float* beta,
+                       const float* mean, const float* rstd, float* dx, const float* dx_add, float* dgamma,
+                       float* dbeta, int nb, int hw, int c, int groups, int silu, void* workspace,
+                       size_t workspace_bytes, void* dx_split, float* dbias, float bias_beta, void* cs_ws,
+                       void* stream) {
   if (nb <= 0 || hw <= 0 || c <= 0 || (c & 3) || groups <= 0 || c % groups || hw % 32 || part == nullptr) {
     set_error("group_norm_bwd_part: needs hw %% 32 == 0 and C %% 4 == 0");
     return MVAE_EINVAL;
@@ -1416,6 +1468,9 @@ int mvae_group_norm_bwd_part_nhwc(const float* x, const float* dy, const double*
   a.nb = nb; a.hw = hw; a.C = c; a.G = groups; a.silu = silu; a.drop_p = 0.f; a.seed = 0;
   a.chunks = gn_chunks(nb, hw);
   a.rows_per_chunk = (hw + a.chunks - 1) / a.chunks;
+  a.dxp = (uint2*)dx_split;
+  a.dxp_split = 1;
+  a.csp = dbias ? (double*)cs_ws : nullptr;
   float* k1 = (float*)((char*)workspace + (size_t)nb * a.chunks * c * 2 * sizeof(double));
   float* k2 = k1 + (size_t)nb * c;
   float* k3 = k2 + (size_t)nb * c;
@@ -1432,6 +1487,9 @@ int mvae_group_norm_bwd_part_nhwc(const float* x, const float* dy, const double*
                        dbeta);
   }
   hipLaunchKernelGGL(gn_dx_kernel, dim3(a.chunks, nb), dim3(256), 0, st, a, k1, k2, k3, dx);
+  if (dbias)
+    hipLaunchKernelGGL(gn_colsum_final_kernel, dim3(cdiv(c, 16)), dim3(256), 0, st, (const double*)a.csp,
+                       nb * a.chunks, c, dbias, bias_beta);
   return launch_status();
 }
 

@@ -112,6 +112,34 @@ __device__ __forceinline__ void wstore(__amdgpu_buffer_rsrc_t r, unsigned off, u
   bstore4(r, off, float4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)});
 }
 
+// a 4-channel group of a transformed operand in format SF (0 split4_bf16, 1 split4_bits: 16 B; 2 packed bf16 -- the
+// bf16-mixed mode's LDS-DMA GEMM operand, round to nearest even: 8 B)
+template <int SF>
+constexpr unsigned wgb() { return SF == 2 ? 8u : 16u; }
+template <int SF>
+struct WGroup {
+  using T = uint4;
+};
+template <>
+struct WGroup<2> {
+  using T = uint2;
+};
+template <int SF>
+__device__ __forceinline__ typename WGroup<SF>::T wgroup(float4 v) {
+  if constexpr (SF == 2) return uint2{pk_bf16x2(v.x, v.y), pk_bf16x2(v.z, v.w)};
+  else return split4_fmt<SF>(v);
+}
+template <int SF>
+__device__ __forceinline__ void wstore_f(__amdgpu_buffer_rsrc_t r, unsigned off, float4 v) {
+  if constexpr (SF == 2) {
+    typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
+    const uint2 g = wgroup<2>(v);
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{g.x, g.y}, r, off, 0, 0);
+  } else {
+    wstore(r, off, split4_fmt<SF>(v));
+  }
+}
+
 __device__ __forceinline__ float4 split4_to_f32(float4 r) {  // split4_bf16 group (hi0..hi3 lo0..lo3) -> hi + lo
   const unsigned h01 = __float_as_uint(r.x), h23 = __float_as_uint(r.y);
   const unsigned l01 = __float_as_uint(r.z), l23 = __float_as_uint(r.w);
@@ -147,7 +175,7 @@ __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ 
   // one exec-masked branch -- and one wait -- per patch element
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(x, (unsigned)((long long)nb * H * W * C * 4));
   const unsigned cb = (unsigned)c4 * 16u;
-  const unsigned plane = (unsigned)(T * C4 * 16), base = (unsigned)(t * C4 + c4) * 16u;
+  const unsigned plane = (unsigned)(T * C4) * wgb<SF>(), base = (unsigned)(t * C4 + c4) * wgb<SF>();
   const __amdgpu_buffer_rsrc_t vr = make_rsrc(v, plane * (unsigned)(AL * AL));
   float4 d[AL][AL];
 #pragma unroll
@@ -189,7 +217,7 @@ __global__ void __launch_bounds__(256) wino_in_kernel(const float* __restrict__ 
 #pragma unroll
   for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < AL; ++j) wstore(vr, base + (unsigned)(i * AL + j) * plane, split4_fmt<SF>(d[i][j]));
+    for (int j = 0; j < AL; ++j) wstore_f<SF>(vr, base + (unsigned)(i * AL + j) * plane, d[i][j]);
 }
 
 // G g G^T of a 3x3 filter of float4 groups
@@ -223,7 +251,8 @@ __global__ void __launch_bounds__(256) wino_wt_fwd_kernel(const float* __restric
 #pragma unroll
   for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < AL; ++j) u[((long long)(i * AL + j) * cout + n) * K4 + k4] = split4_fmt<SF>(o[i][j]);
+    for (int j = 0; j < AL; ++j)
+      ((typename WGroup<SF>::T*)u)[((long long)(i * AL + j) * cout + n) * K4 + k4] = wgroup<SF>(o[i][j]);
 }
 
 // input-gradient filters U'[a^2][cin][cout] split4_bf16, g'(n = cin, k = cout)[r][s] = w[k][2-r][2-s][n]: the source is
@@ -243,7 +272,8 @@ __global__ void __launch_bounds__(256) wino_wt_dgrad_kernel(const float* __restr
                                                             int cout, int cin) {
   constexpr int AL = MT + 2, KQ = wdg_kq<MT, BIG>(), NT = WDG_N * KQ, PP = wdg_pp<MT, BIG>();
   static_assert((AL * AL) % PP == 0, "position passes");
-  __shared__ uint4 lds[PP][WDG_N][KQ];
+  using GT = typename WGroup<SF>::T;
+  __shared__ GT lds[PP][WDG_N][KQ];
   const int K4 = cout >> 2;
   const int n0 = blockIdx.x * WDG_N, kb = blockIdx.y * KQ;
   const int nl = threadIdx.x % WDG_N, kq = threadIdx.x / WDG_N;
@@ -270,13 +300,13 @@ __global__ void __launch_bounds__(256) wino_wt_dgrad_kernel(const float* __restr
       for (int i = 0; i < AL; ++i)
 #pragma unroll
         for (int j = 0; j < AL; ++j)
-          if (i * AL + j >= p0 && i * AL + j < p0 + PP) lds[i * AL + j - p0][nl][kq] = split4_fmt<SF>(o[i][j]);
+          if (i * AL + j >= p0 && i * AL + j < p0 + PP) lds[i * AL + j - p0][nl][kq] = wgroup<SF>(o[i][j]);
     }
     __syncthreads();
     for (int e = threadIdx.x; e < PP * WDG_N * KQ; e += NT) {
       const int xi = e / (WDG_N * KQ), rem = e % (WDG_N * KQ);
       const int nn = n0 + rem / KQ, kk = kb + rem % KQ;
-      if (nn < cin && kk < K4) u[((long long)(p0 + xi) * cin + nn) * K4 + kk] = lds[xi][rem / KQ][rem % KQ];
+      if (nn < cin && kk < K4) ((GT*)u)[((long long)(p0 + xi) * cin + nn) * K4 + kk] = lds[xi][rem / KQ][rem % KQ];
     }
     __syncthreads();
   }
@@ -472,7 +502,7 @@ __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ 
   const int k4 = (int)(idx - t * K4);
   const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
   const __amdgpu_buffer_rsrc_t dr = make_rsrc(dy, (unsigned)((long long)nb * H * W * K * 4));
-  const unsigned plane = (unsigned)(T * K4 * 16), base = (unsigned)(t * K4 + k4) * 16u;
+  const unsigned plane = (unsigned)(T * K4) * wgb<SF>(), base = (unsigned)(t * K4 + k4) * wgb<SF>();
   const __amdgpu_buffer_rsrc_t vr = make_rsrc(d, plane * (unsigned)(AL * AL));
   float4 v[MT][MT];
 #pragma unroll
@@ -493,7 +523,7 @@ __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ 
 #pragma unroll
   for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < AL; ++j) wstore(vr, base + (unsigned)(i * AL + j) * plane, split4_fmt<SF>(o[i][j]));
+    for (int j = 0; j < AL; ++j) wstore_f<SF>(vr, base + (unsigned)(i * AL + j) * plane, o[i][j]);
 }
 
 // dy -> both backward operands in one pass over dy (a conv whose input and weight gradients both run the Winograd
@@ -514,7 +544,7 @@ __global__ void __launch_bounds__(256) wino_dy2_kernel(const float* __restrict__
   const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(dy, (unsigned)((long long)nb * H * W * K * 4));
   const unsigned kb = (unsigned)k4 * 16u;
-  const unsigned plane = (unsigned)(T * K4 * 16), base = (unsigned)(t * K4 + k4) * 16u;
+  const unsigned plane = (unsigned)(T * K4) * wgb<SF>(), base = (unsigned)(t * K4 + k4) * wgb<SF>();
   const __amdgpu_buffer_rsrc_t vr = make_rsrc(v, plane * (unsigned)(AL * AL));
   const __amdgpu_buffer_rsrc_t dr = make_rsrc(d, plane * (unsigned)(AL * AL));
   float4 p[AL][AL];
@@ -545,7 +575,7 @@ __global__ void __launch_bounds__(256) wino_dy2_kernel(const float* __restrict__
       for (int e = 0; e < MT; ++e) wmadd(o[j], first, wino_at<MT>(e, j), ci[e]);
     }
 #pragma unroll
-    for (int j = 0; j < AL; ++j) wstore(dr, base + (unsigned)(i * AL + j) * plane, split4_fmt<SF>(o[j]));
+    for (int j = 0; j < AL; ++j) wstore_f<SF>(dr, base + (unsigned)(i * AL + j) * plane, o[j]);
   }
   constexpr auto bt = [](int i, int k) { return wino_bt<MT>(i, k); };
 #pragma unroll
@@ -555,7 +585,7 @@ __global__ void __launch_bounds__(256) wino_dy2_kernel(const float* __restrict__
 #pragma unroll
   for (int i = 0; i < AL; ++i)
 #pragma unroll
-    for (int j = 0; j < AL; ++j) wstore(vr, base + (unsigned)(i * AL + j) * plane, split4_fmt<SF>(p[i][j]));
+    for (int j = 0; j < AL; ++j) wstore_f<SF>(vr, base + (unsigned)(i * AL + j) * plane, p[i][j]);
 }
 
 // dw [cout][3][3][cin] = beta * dw + G^T M G, M [a^2][cout][cin] fp32: one thread per (k, 4-group of c)
@@ -614,13 +644,21 @@ static int egrid256(long long n) { return (int)std::min<long long>((n + 255) / 2
 
 // every GEMM arithmetic: 3xBF16 (V / U value-split into split4_bf16), bf16 (the same groups; the GEMM stages the hi
 // halves) and exact fp32 (bit split, split4_bits: the f32-input MFMA reassembles the transforms' fp32 words exactly)
-static int wino_sf() { return math_mode() == MATH_FP32 ? 1 : 0; }
+static int wino_sf() { return math_mode() == MATH_FP32 ? 1 : math_mode() == MATH_BF16 ? 2 : 0; }
 // a pre-split INPUT is a 3xBF16 value split: there is none in the exact mode
 static bool wino_split_in_ok(int split) {
-  if (!split || wino_sf() == 0) return true;
+  if (!split || wino_sf() != 1) return true;
   set_error("winograd: pre-split (3xBF16) inputs are not used in the exact fp32 arithmetic");
   return false;
 }
+
+// FN<MT, SF>(args...) for the transform layout of the current arithmetic (sf: wino_sf())
+#define WINO_GO(FN, MT, ...)                        \
+  do {                                              \
+    if (sf == 1) FN<MT, 1>(__VA_ARGS__);            \
+    else if (sf == 2) FN<MT, 2>(__VA_ARGS__);       \
+    else FN<MT, 0>(__VA_ARGS__);                    \
+  } while (0)
 
 template <int MT, int SF>
 static void wt_go(const float* w, void* u, int cin, int cout, int dgrad, hipStream_t st) {
@@ -644,9 +682,9 @@ static void wt_go(const float* w, void* u, int cin, int cout, int dgrad, hipStre
 template <int MT, int SF>
 static void in_go(const float* x, void* v, int nb, int h, int w, int c, int xs, int gn, WinoGn p, hipStream_t st) {
   const dim3 g(egrid256(wino_tiles(nb, h, w, MT) * (c / 4)));
-  if constexpr (SF == 0) {
+  if constexpr (SF != 1) {
     if (xs) {
-      hipLaunchKernelGGL((wino_in_kernel<MT, true, 0, 0>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, p);
+      hipLaunchKernelGGL((wino_in_kernel<MT, true, 0, SF>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, p);
       return;
     }
   }
@@ -660,10 +698,10 @@ template <int MT, int SF>
 static void dy_go(const float* dy, void* v, void* d, int nb, int h, int w, int k, int xs, bool both, hipStream_t st) {
   const dim3 g(egrid256(wino_tiles(nb, h, w, MT) * (k / 4)));
   uint4 *vv = (uint4*)v, *dd = (uint4*)d;
-  if constexpr (SF == 0) {
+  if constexpr (SF != 1) {
     if (xs) {
-      if (both) hipLaunchKernelGGL((wino_dy2_kernel<MT, true, 0>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
-      else hipLaunchKernelGGL((wino_dy_kernel<MT, true, 0>), g, dim3(256), 0, st, dy, dd, nb, h, w, k);
+      if (both) hipLaunchKernelGGL((wino_dy2_kernel<MT, true, SF>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
+      else hipLaunchKernelGGL((wino_dy_kernel<MT, true, SF>), g, dim3(256), 0, st, dy, dd, nb, h, w, k);
       return;
     }
   }
@@ -717,8 +755,8 @@ int mvae_winograd_weight_transform(const float* w, void* u, int cin, int cout, i
   }
   hipStream_t st = (hipStream_t)stream;
   const int sf = wino_sf();
-  if (tile == 2) (sf ? wt_go<2, 1> : wt_go<2, 0>)(w, u, cin, cout, dgrad, st);
-  else (sf ? wt_go<4, 1> : wt_go<4, 0>)(w, u, cin, cout, dgrad, st);
+  if (tile == 2) WINO_GO(wt_go, 2, w, u, cin, cout, dgrad, st);
+  else WINO_GO(wt_go, 4, w, u, cin, cout, dgrad, st);
   return launch_status();
 }
 
@@ -732,8 +770,8 @@ int mvae_winograd_input_transform(const float* x, void* v, int nb, int h, int w,
   if (!wino_split_in_ok(x_split)) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   const int sf = wino_sf();
-  if (tile == 2) (sf ? in_go<2, 1> : in_go<2, 0>)(x, v, nb, h, w, c, x_split, 0, WinoGn{}, st);
-  else (sf ? in_go<4, 1> : in_go<4, 0>)(x, v, nb, h, w, c, x_split, 0, WinoGn{}, st);
+  if (tile == 2) WINO_GO(in_go, 2, x, v, nb, h, w, c, x_split, 0, WinoGn{}, st);
+  else WINO_GO(in_go, 4, x, v, nb, h, w, c, x_split, 0, WinoGn{}, st);
   return launch_status();
 }
 
@@ -749,8 +787,8 @@ int mvae_winograd_input_transform_gn(const float* x, const float* scale, const f
   hipStream_t st = (hipStream_t)stream;
   const WinoGn gn{scale, shift, silu};
   const int sf = wino_sf(), mode = silu ? 2 : 1;
-  if (tile == 2) (sf ? in_go<2, 1> : in_go<2, 0>)(x, v, nb, h, w, c, 0, mode, gn, st);
-  else (sf ? in_go<4, 1> : in_go<4, 0>)(x, v, nb, h, w, c, 0, mode, gn, st);
+  if (tile == 2) WINO_GO(in_go, 2, x, v, nb, h, w, c, 0, mode, gn, st);
+  else WINO_GO(in_go, 4, x, v, nb, h, w, c, 0, mode, gn, st);
   return launch_status();
 }
 
@@ -764,15 +802,26 @@ int mvae_winograd_gemm(const void* v, const void* u, float* m, long long tiles, 
     set_error("winograd_gemm: k_in, n_out multiples of 4, 16-B aligned, one position < 4 GiB, tile 2 or 4");
     return MVAE_EINVAL;
   }
+  // (bf16-mixed: V and U packed bf16, 2 B per element, through the LDS-DMA main loop -- 16-B rows need k_in % 8)
+  const bool pk = wino_sf() == 2;
+  if (pk && k_in % 8) {
+    set_error("winograd_gemm: the bf16 (packed) operands need k_in %% 8 == 0");
+    return MVAE_EINVAL;
+  }
+  const unsigned eb = pk ? 2u : 4u;
   GemmArgs a{};
   a.M = (int)tiles; a.N = n_out; a.K = k_in; a.batch = (tile + 2) * (tile + 2);
   a.A = (const float*)v; a.lda = k_in; a.sA = tiles * k_in;
   a.B = (const float*)u; a.ldb = k_in; a.sB = (long long)n_out * k_in;
   a.C = m; a.ldc = n_out; a.sC = tiles * n_out;
   a.alpha = 1.f; a.beta = 0.f;
-  a.a_bytes = (unsigned)(tiles * k_in * 4); a.b_bytes = (unsigned)((long long)n_out * k_in * 4);
+  a.a_bytes = (unsigned)(tiles * k_in * eb); a.b_bytes = (unsigned)((long long)n_out * k_in * eb);
   a.c_bytes = (unsigned)(tiles * n_out * 4);
   set_splits(a, 1);
+  auto go = [&](GemmArgs& g, int c) {
+    if (pk) conv_dma(A_ROWK, g, (hipStream_t)stream, c, 4);
+    else launch_big<A_ROWK_SPLIT, 4, B_ROWK_SPLIT, 4>(g, (hipStream_t)stream, c);
+  };
   const int cfg = choose_tile(a, true, false);
   // wave-quantization tail (as conv2d_impl's): positions whose tiles would leave a nearly empty last round (c2's 7x7x512
   // level: 16 tiles of 256x128 per position x 36 = 2.25 rounds) go in a second launch the cost model tiles finely
@@ -787,17 +836,18 @@ int mvae_winograd_gemm(const void* v, const void* u, float* m, long long tiles, 
     if (full >= 1 && rem > 0 && rem * 2 <= slots) b_main = (int)std::max<long long>(1, full * slots / tp);
   }
   if (b_main >= a.batch) {
-    launch_big<A_ROWK_SPLIT, 4, B_ROWK_SPLIT, 4>(a, (hipStream_t)stream, cfg);
+    go(a, cfg);
     return launch_status();
   }
   GemmArgs t = a;
   a.batch = b_main;
-  launch_big<A_ROWK_SPLIT, 4, B_ROWK_SPLIT, 4>(a, (hipStream_t)stream, cfg);
+  go(a, cfg);
   t.batch -= b_main;
-  t.A += (long long)b_main * t.sA;
-  t.B += (long long)b_main * t.sB;
+  // (the A / B pointers are float-typed: a packed operand's element offset is half as many floats)
+  t.A = (const float*)((const char*)t.A + (long long)b_main * t.sA * eb);
+  t.B = (const float*)((const char*)t.B + (long long)b_main * t.sB * eb);
   t.C += (long long)b_main * t.sC;
-  launch_big<A_ROWK_SPLIT, 4, B_ROWK_SPLIT, 4>(t, (hipStream_t)stream, choose_tile(t, true, false));
+  go(t, choose_tile(t, true, false));
   return launch_status();
 }
 
@@ -847,8 +897,8 @@ int mvae_winograd_dy_transform(const float* dy, void* d, int nb, int h, int w, i
   if (!wino_split_in_ok(dy_split)) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   const int sf = wino_sf();
-  if (tile == 2) (sf ? dy_go<2, 1> : dy_go<2, 0>)(dy, nullptr, d, nb, h, w, k, dy_split, false, st);
-  else (sf ? dy_go<4, 1> : dy_go<4, 0>)(dy, nullptr, d, nb, h, w, k, dy_split, false, st);
+  if (tile == 2) WINO_GO(dy_go, 2, dy, nullptr, d, nb, h, w, k, dy_split, false, st);
+  else WINO_GO(dy_go, 4, dy, nullptr, d, nb, h, w, k, dy_split, false, st);
   return launch_status();
 }
 
@@ -863,8 +913,8 @@ int mvae_winograd_dy_transforms(const float* dy, void* v, void* d, int nb, int h
   if (!wino_split_in_ok(dy_split)) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   const int sf = wino_sf();
-  if (tile == 2) (sf ? dy_go<2, 1> : dy_go<2, 0>)(dy, v, d, nb, h, w, k, dy_split, true, st);
-  else (sf ? dy_go<4, 1> : dy_go<4, 0>)(dy, v, d, nb, h, w, k, dy_split, true, st);
+  if (tile == 2) WINO_GO(dy_go, 2, dy, v, d, nb, h, w, k, dy_split, true, st);
+  else WINO_GO(dy_go, 4, dy, v, d, nb, h, w, k, dy_split, true, st);
   return launch_status();
 }
 
@@ -878,17 +928,24 @@ int mvae_winograd_wgrad_gemm(const void* d, const void* v, float* m, long long t
     set_error("winograd_wgrad_gemm: cout, cin multiples of 4, 16-B aligned, one position < 4 GiB, tile 2 or 4");
     return MVAE_EINVAL;
   }
+  const bool pk = wino_sf() == 2;  // (bf16-mixed: packed D' / V through the LDS-DMA COL x COL loop)
+  if (pk && (cout % 8 || cin % 8)) {
+    set_error("winograd_wgrad_gemm: the bf16 (packed) operands need cout, cin %% 8 == 0");
+    return MVAE_EINVAL;
+  }
+  const unsigned eb = pk ? 2u : 4u;
   GemmArgs a{};
   a.M = cout; a.N = cin; a.K = (int)tiles; a.batch = (tile + 2) * (tile + 2);
   a.A = (const float*)d; a.lda = cout; a.sA = tiles * cout;
   a.B = (const float*)v; a.ldb = cin; a.sB = tiles * cin;
   a.C = m; a.ldc = cin; a.sC = (long long)cout * cin;
   a.alpha = 1.f; a.beta = 0.f;
-  a.a_bytes = (unsigned)(tiles * cout * 4); a.b_bytes = (unsigned)(tiles * cin * 4);
+  a.a_bytes = (unsigned)(tiles * cout * eb); a.b_bytes = (unsigned)(tiles * cin * eb);
   a.c_bytes = (unsigned)((long long)cout * cin * 4);
   const int cfg = choose_tile(a, true, workspace != nullptr);
   plan_splits(a, cfg, workspace, workspace_bytes);
-  launch_big<A_COLM_SPLIT, 4, B_COLN_SPLIT, 4>(a, (hipStream_t)stream, cfg);
+  if (pk) wgrad_dma(B_COLN, a, (hipStream_t)stream, cfg, 4);
+  else launch_big<A_COLM_SPLIT, 4, B_COLN_SPLIT, 4>(a, (hipStream_t)stream, cfg);
   return gemm_finish(a, (hipStream_t)stream);
 }
 

@@ -247,7 +247,9 @@ if WINOGRAD_TILE not in (2, 4):
 # transform domain amplify the rounding -- simulated against float64 at 16x16x256 the direct bf16 conv errs 2.4e-3, F(2x2)
 # 4.0e-3, F(4x4) 2.7e-2 -- so that mode uses m = 2 (MVAE_WINOGRAD_TILE_BF16), at 4x the input / output transform traffic
 # for 4/9 of the MACs: only where the images are small and the channels wide (MVAE_WINOGRAD_BF16_MAX_W, default 16: c5's
-# 8x8x2048 and 16x16x1024 levels). MVAE_NO_WINOGRAD_BF16=1 keeps its convs on the LDS-DMA implicit GEMM.
+# 8x8x2048 and 16x16x1024 levels). The transforms write V, U and D' as packed bf16 (2 B per element: half the transform
+# write traffic) and the position / weight-gradient GEMMs run on the LDS-DMA main loop like the mode's other convs.
+# MVAE_NO_WINOGRAD_BF16=1 keeps its convs on the LDS-DMA implicit GEMM.
 WINOGRAD_EXACT = os.environ.get("MVAE_NO_WINOGRAD_EXACT") is None
 WINOGRAD_BF16 = os.environ.get("MVAE_NO_WINOGRAD_BF16") is None
 WINOGRAD_TILE_BF16 = int(os.environ.get("MVAE_WINOGRAD_TILE_BF16", "2"))
@@ -257,6 +259,12 @@ WINOGRAD_BF16_MAX_W = int(os.environ.get("MVAE_WINOGRAD_BF16_MAX_W", "16"))
 def _wtile() -> int:
     """The output tile m of F(m x m, 3x3) in the current GEMM arithmetic."""
     return WINOGRAD_TILE_BF16 if _MATH[0] == 1 else WINOGRAD_TILE
+
+
+def _wel() -> int:
+    """bytes per element of the transformed operands (V, U, D'): the 16-B-per-4 pre-split layouts, or packed bf16 in the
+    bf16-mixed mode (the LDS-DMA GEMM's operand)."""
+    return 2 if _MATH[0] == 1 else 4
 
 
 def _wino_alg(ref: float) -> float:
@@ -286,7 +294,7 @@ def _wino_ok(g, n: int, h: int, wd: int, cin: int, cout: int) -> bool:
         on, maxw = WINOGRAD_BF16, min(WINOGRAD_MAX_W, WINOGRAD_BF16_MAX_W)
     return (WINOGRAD and on and g.kh == 3 and g.kw == 3 and g.stride == 1 and
             not g.upsample and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and wd <= maxw and
-            cin % 4 == 0 and cout % 4 == 0 and
+            cin % (8 if mode == 1 else 4) == 0 and cout % (8 if mode == 1 else 4) == 0 and
             min(cin, cout) >= (WINOGRAD_MIN_C_WIDE if wd >= 32 else WINOGRAD_MIN_C) and
             9.0 * n * h * wd * cin * cout >= WINOGRAD_MIN_MACS and
             # (each transformed operand is addressed through one buffer descriptor, < 4 GiB: batches whose operands
@@ -343,6 +351,9 @@ WINOGRAD_DY2 = os.environ.get("MVAE_NO_WINOGRAD_DY2") is None
 # runs at the plain one's speed and c4 gains 2 % (704-706 -> 717-721 img/s, GroupNorm family 40.5 -> 31.9 ms; same box,
 # interleaved, profiles/r05_winograd_gn_ab.txt). MVAE_NO_WINOGRAD_GN=1 writes the GroupNorm output as before.
 WINOGRAD_GN = os.environ.get("MVAE_NO_WINOGRAD_GN") is None
+# ... and where that GroupNorm's backward streams (the large levels), its partial pass over x and dy comes from the
+# conv's Winograd input-gradient output transform instead; MVAE_NO_WINOGRAD_GN_LINK=1: the pass
+WINOGRAD_GN_LINK = os.environ.get("MVAE_NO_WINOGRAD_GN_LINK") is None
 GN_LAZY_ATTR = "_mvae_gn_lazy"
 G3 = ConvGeom(3, 3, 1, 1, 1, 1, 1, False)  # the GroupNorm-fed convs' geometry (ResnetBlock conv1 / conv2, conv_out)
 
@@ -417,18 +428,18 @@ def _winograd(src, w, n: int, h: int, wd: int, k_in: int, n_out: int, src_split:
     pos = (mt + 2) ** 2
     dev = src.device
     if keep is not None:
-        v = torch.empty(4 * pos * t * k_in, dtype=torch.uint8, device=dev)
+        v = torch.empty(_wel() * pos * t * k_in, dtype=torch.uint8, device=dev)
         kt = src if key is None else key
         keep.append((v, mt, kt.data_ptr(), kt._version, tuple(chunk)))
     else:
-        v = ARENA.get("wino_v", 4 * pos * t * k_in, dev)
+        v = ARENA.get("wino_v", _wel() * pos * t * k_in, dev)
     m = ARENA.get("wino_m", 4 * pos * t * n_out, dev)
     if u is None:
-        u = ARENA.get("wino_u", 4 * pos * k_in * n_out, dev)
+        u = ARENA.get("wino_u", _wel() * pos * k_in * n_out, dev)
         cin, cout = (n_out, k_in) if dgrad else (k_in, n_out)
         _lib.call("mvae_winograd_weight_transform", w.data_ptr(), u.data_ptr(), cin, cout, int(dgrad), mt, st)
     if dkeep is not None:
-        d = torch.empty(4 * pos * t * k_in, dtype=torch.uint8, device=dev)
+        d = torch.empty(_wel() * pos * t * k_in, dtype=torch.uint8, device=dev)
         kt = src if key is None else key
         dkeep.append((d, mt, kt.data_ptr(), kt._version, tuple(chunk)))
         _lib.call("mvae_winograd_dy_transforms", src.data_ptr(), v.data_ptr(), d.data_ptr(), n, h, wd, k_in,
@@ -1003,7 +1014,11 @@ def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool
 def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_split=False, dys=None, wino_v=None,
                        wino_d=None, lazy=None):
     st = _stream(dy)
-    if isinstance(x, DeferredGnOutput) and (lazy is None or not _wino_wgrad_ok(g, lazy.x, dy, dw, dys)):
+    # a deferred GroupNorm output has no values to read: its weight gradient is the Winograd one, on the kept (or
+    # re-derived) V, ahead of the kernels below that read x -- the direct cout-32 kernel would otherwise take a 32-channel
+    # conv and read n*h*w*c floats from the placeholder's one-element allocation
+    deferred = isinstance(x, DeferredGnOutput)
+    if deferred and (lazy is None or not _wino_wgrad_ok(g, lazy.x, dy, dw, dys)):
         # (conv2d_wgrad_raw materializes such an x for every other path: reaching here would read the placeholder)
         raise RuntimeError("conv2d wgrad: a deferred GroupNorm output reached a weight-gradient kernel that reads x")
     if x_split and (g.pointwise or g.upsample):
@@ -1016,7 +1031,7 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         _lib.call("mvae_gemm_strided_batched", 1, 0, co, c, m, 1.0, dy.data_ptr(), co, 0, x.data_ptr(), c, 0,
                   float(beta), dw.data_ptr(), c, 0, 1, None, None, 0, 0, ws.data_ptr(), ws.numel(), st)
         return False
-    if (SMALL_COUT_WGRAD and co <= 4 and c % 4 == 0 and not g.upsample and g.kh == 3 and g.kw == 3 and g.stride == 1
+    if (not deferred and SMALL_COUT_WGRAD and co <= 4 and c % 4 == 0 and not g.upsample and g.kh == 3 and g.kw == 3 and g.stride == 1
             and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and _al16(x)):
         # Decoder.conv_out (cout 3): x read once, scattered into its 9 taps (no 9x im2col stream)
         nbytes = _lib.query("mvae_conv2d_wgrad_small_cout_workspace_bytes", n, c)
@@ -1024,7 +1039,7 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         _lib.call("mvae_conv2d_wgrad_small_cout_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db),
                   float(beta), n, h, wd, c, co, int(x_split), ws.data_ptr(), ws.numel(), st)
         return db is not None
-    if (DIRECT_WGRAD and dys is None and c in (32, 64) and co in DIRECT_WGRAD_COUT and _MATH[0] != 2 and
+    if (not deferred and DIRECT_WGRAD and dys is None and c in (32, 64) and co in DIRECT_WGRAD_COUT and _MATH[0] != 2 and
             not g.upsample and g.kh == 3 and g.kw == 3 and g.stride == 1 and (g.pad_t, g.pad_l, g.pad_b, g.pad_r) == (1, 1, 1, 1) and
             _al16(x, dy)):
         # cout 32 (c3's 28x28 / 14x14 levels): per-tap MFMA products over LDS-resident row bands; 28x28x32 at bs 512
@@ -1034,7 +1049,7 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         _lib.call("mvae_conv2d_wgrad_direct_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db), float(beta),
                   n, h, wd, c, co, int(x_split), ws.data_ptr(), ws.numel(), st)
         return db is not None
-    if _subpixel_upsample(g):
+    if not deferred and _subpixel_upsample(g):
         nbytes = _lib.query("mvae_conv2d_wgrad_upsample_workspace_bytes", n, h, wd, c, co)
         ws = ARENA.get("ws", nbytes, dy.device)
         _lib.call("mvae_conv2d_wgrad_upsample_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db),
@@ -1063,15 +1078,15 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
             m = ARENA.get("wino_mw", 4 * pos * co * c, dev)
             ws = ARENA.get("ws", _lib.query("mvae_gemm_workspace_bytes", co, c, t, pos), dev)
             if dt is None:
-                dt = ARENA.get("wino_d", 4 * pos * t * co, dev)
+                dt = ARENA.get("wino_d", _wel() * pos * t * co, dev)
                 _lib.call("mvae_winograd_dy_transform", dya[b0:b1].data_ptr(), dt.data_ptr(), nb, h, wd, co,
                           int(dys is not None), mt, st)
             if v is None and lazy is not None:  # (the kept V is gone -- a second backward: re-derived, normalized on load)
-                v = ARENA.get("wino_v", 4 * pos * t * c, dev)
+                v = ARENA.get("wino_v", _wel() * pos * t * c, dev)
                 _lib.call("mvae_winograd_input_transform_gn", lazy.x[b0:b1].data_ptr(), lazy.scale[b0 * c:].data_ptr(),
                           lazy.shift[b0 * c:].data_ptr(), lazy.silu, v.data_ptr(), nb, h, wd, c, mt, st)
             elif v is None:
-                v = ARENA.get("wino_v", 4 * pos * t * c, dev)
+                v = ARENA.get("wino_v", _wel() * pos * t * c, dev)
                 _lib.call("mvae_winograd_input_transform", x[b0:b1].data_ptr(), v.data_ptr(), nb, h, wd, c,
                           int(x_split), mt, st)
             _lib.call("mvae_winograd_wgrad_gemm", dt.data_ptr(), v.data_ptr(), m.data_ptr(), t, co, c, mt,
@@ -1513,40 +1528,50 @@ class GroupNormFn(torch.autograd.Function):
                 raise RuntimeError("group_norm backward: parked branch gradient has the wrong shape")
         gpart = ctx.link.take(dy) if ctx.link is not None and drop_p == 0.0 else None
         # algorithmic HBM bytes: read x, dy (and the residual branch's gradient when it is summed here); write dx
+        req = ctx.dypack if ctx.dypack is not None and _al16(dy, dx) and (add is None or _al16(add)) else None
+        if req is not None and gpart is not None and not req.split:
+            req = None  # (the backward from the conv's partials writes split4 dy only)
+        packed = tgt = cs = None
+        if req is not None:
+            # also dx as packed bf16 / split4 and the producing conv's bias gradient (DyPack)
+            # packed bf16: 2 B per element; split4_bf16: 4 B per element, dx's layout (an fp32-sized buffer)
+            packed = (torch.empty_like(x, memory_format=CL) if req.split else
+                      torch.empty(x.numel() * 2, device=x.device, dtype=torch.uint8))
+            bref = req.bias_ref
+            if bref is not None and bref.requires_grad:
+                # a private buffer, never the flat gradient slot: the conv adds it there only if DyPack.take()
+                # accepts dy (a rejected dy -- another branch summed in by autograd -- gets its bias gradient from
+                # the real dy instead, and nothing partial is left in the slot)
+                tgt = req.db = torch.empty(c, device=x.device, dtype=torch.float32)
+            csb = _lib.query("mvae_group_norm_colsum_workspace_bytes", n, h * w, c)
+            cs = ARENA.get("gncs", csb, x.device) if tgt is not None else None
         with _timed("gn_bwd", (12.0 + (4.0 if add is not None else 0.0)) * x.numel(), (n, c, h * w)):
-            if gpart is not None:  # reduction half emitted by the consuming conv's input-gradient GEMM
+            if gpart is not None and req is not None:  # reduction half from the conv + the conv's split dy / bias
+                _lib.call("mvae_group_norm_bwd_part_split_nhwc", x.data_ptr(), dy.data_ptr(), gpart.data_ptr(),
+                          gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                          _ptr(add), _ptr(dg), _ptr(db), n, h * w, c, groups, silu, ws.data_ptr(), ws.numel(),
+                          packed.data_ptr(), _ptr(tgt), 0.0, _ptr(cs), cs.numel() if cs is not None else 0,
+                          _stream(x))
+            elif gpart is not None:  # reduction half emitted by the consuming conv's input-gradient GEMM
                 _lib.call("mvae_group_norm_bwd_part_nhwc", x.data_ptr(), dy.data_ptr(), gpart.data_ptr(),
                           gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
                           _ptr(add), _ptr(dg), _ptr(db), n, h * w, c, groups, silu, ws.data_ptr(), ws.numel(),
                           _stream(x))
-            elif ctx.dypack is not None and _al16(dy, dx) and (add is None or _al16(add)):
-                # also dx as packed bf16 and the producing conv's bias gradient (DyPack)
-                req = ctx.dypack
-                # packed bf16: 2 B per element; split4_bf16: 4 B per element, dx's layout (an fp32-sized buffer)
-                packed = (torch.empty_like(x, memory_format=CL) if req.split else
-                          torch.empty(x.numel() * 2, device=x.device, dtype=torch.uint8))
-                bref = req.bias_ref
-                tgt, bbeta = None, 0.0
-                if bref is not None and bref.requires_grad:
-                    # a private buffer, never the flat gradient slot: the conv adds it there only if DyPack.take()
-                    # accepts dy (a rejected dy -- another branch summed in by autograd -- gets its bias gradient from
-                    # the real dy instead, and nothing partial is left in the slot)
-                    tgt = req.db = torch.empty(c, device=x.device, dtype=torch.float32)
-                csb = _lib.query("mvae_group_norm_colsum_workspace_bytes", n, h * w, c)
-                cs = ARENA.get("gncs", csb, x.device) if tgt is not None else None
+            elif req is not None:
                 _lib.call("mvae_group_norm_bwd_split_nhwc" if req.split else "mvae_group_norm_bwd_pack_nhwc",
                           x.data_ptr(), dy.data_ptr(), gamma.data_ptr(),
                           beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(add), _ptr(dg),
                           _ptr(db), n, h * w, c, groups, silu, drop_p, seed, ws.data_ptr(), ws.numel(),
-                          packed.data_ptr(), _ptr(tgt), float(bbeta), _ptr(cs), cs.numel() if cs is not None else 0,
+                          packed.data_ptr(), _ptr(tgt), 0.0, _ptr(cs), cs.numel() if cs is not None else 0,
                           _stream(x))
-                req.packed, req.dx_ref, req.dx_version, req.dx_shape = packed, weakref.ref(dx), dx._version, \
-                    tuple(dx.shape)
-                req.bias_done = tgt is not None
             else:
                 _lib.call("mvae_group_norm_bwd_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
                           mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(add), _ptr(dg), _ptr(db), n, h * w,
                           c, groups, silu, drop_p, seed, ws.data_ptr(), ws.numel(), _stream(x))
+        if req is not None:
+            req.packed, req.dx_ref, req.dx_version, req.dx_shape = packed, weakref.ref(dx), dx._version, \
+                tuple(dx.shape)
+            req.bias_done = tgt is not None
         if ctx.needs_input_grad[1] and dg_ret is None:
             _grad_done(ctx.gamma_ref)
         if ctx.needs_input_grad[2] and db_ret is None:
@@ -1582,16 +1607,23 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
             x.shape[1] % groups == 0 and x.is_contiguous(memory_format=CL)
         part = part[0] if ok else None
     link = GnBwdLink(groups, silu) if (for_conv and GN_BWD_FUSED and drop_p == 0.0 and x.requires_grad) else None
-    lazy = None
-    if (WINOGRAD_GN and for_conv and not isinstance(for_conv, bool) and drop_p == 0.0 and not packed and
-            link is None and x.dim() == 4 and _al16(x) and WINOGRAD_WGRAD):
-        n, c, h, w = x.shape
-        if _wino_ok(G3, n, h, w, c, int(for_conv)):  # (the consuming conv is 3x3 / stride 1 / pad 1: for_conv callers)
-            lazy, split = LazyGn(x, silu), 0
     dyp = getattr(x, DYPACK_ATTR, None)
     if dyp is not None:
         delattr(x, DYPACK_ATTR)  # one GroupNorm per conv output
         dyp = dyp[0] if dyp[1] == x._version and x.is_contiguous(memory_format=CL) and _al16(x) else None
+    lazy = None
+    if (WINOGRAD_GN and for_conv and not isinstance(for_conv, bool) and drop_p == 0.0 and not packed and
+            x.dim() == 4 and _al16(x) and WINOGRAD_WGRAD):
+        n, c, h, w = x.shape
+        if _wino_ok(G3, n, h, w, c, int(for_conv)):  # (the consuming conv is 3x3 / stride 1 / pad 1: for_conv callers)
+            lazy, split = LazyGn(x, silu), 0
+            # the conv's Winograd input-gradient output transform also emits this GroupNorm's backward partials
+            # (mvae_winograd_output_gnbwd: one extra read of x there) where the backward would otherwise make a partial
+            # pass over x and dy (its streaming chain: the large levels, whose producing conv takes dy pre-split)
+            if (link is None and WINOGRAD_GN_LINK and x.requires_grad and dyp is not None and dyp.split and
+                    _wino_blocks(h, w) and c % groups == 0 and (c // groups) % 4 == 0 and
+                    _lib.query("mvae_group_norm_bwd_streaming", n, h * w, c, groups, 1)):
+                link = GnBwdLink(groups, silu)
     y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink, part, link, dyp, lazy)
     if lazy is not None:
         y = y.as_subclass(DeferredGnOutput)  # (same autograd node; any read of its values raises)

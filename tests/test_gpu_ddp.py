@@ -272,7 +272,7 @@ def _worker4(rank, world, init_file, out_file):
     sl = slice(b * rank, b * rank + b)
     batch = (x[sl].to(dev), torch.zeros(b, 1, dtype=torch.long, device=dev), oh[sl].to(dev))
     mod.fit_step(batch, 0, eps=eps[0, sl].to(dev))
-    grad = (mod.flat.grad * mod.optimizer.grad_scale).cpu()
+    grad = mod.flat.grad.cpu()  # (the fused step leaves the exchanged gradient scaled by 1/world -- and clipped -- in place)
     p1 = mod.flat.data.cpu()
     mod.fit_step(batch, 1, eps=eps[1, sl].to(dev))
     torch.cuda.synchronize()
@@ -317,7 +317,7 @@ def test_dp_four_ranks_real_hip_step(monkeypatch):
     batch = (x.to(dev), torch.zeros(8, 1, dtype=torch.long, device=dev), oh.to(dev))
     p0 = mod.flat.data.cpu().double()
     mod.fit_step(batch, 0, eps=eps[0].to(dev))
-    ref = mod.flat.grad.cpu().double()
+    ref = mod.flat.grad.cpu().double()  # (the same in-place clip)
     assert float((rs[0]["grad"].double() - ref).norm() / ref.norm()) < 1e-3
     single1 = mod.flat.data.cpu().double()
     mod.fit_step(batch, 1, eps=eps[1].to(dev))
