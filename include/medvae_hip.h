@@ -211,6 +211,22 @@ int mvae_winograd_dy_transforms(const float* dy, void* v, void* d, int nb, int h
 int mvae_winograd_wgrad_gemm(const void* d, const void* v, float* m, long long tiles, int cout, int cin, int tile,
                              float* workspace, size_t workspace_bytes, void* stream);
 int mvae_winograd_wgrad_output(const float* m, float* dw, float beta, int cout, int cin, int tile, void* stream);
+/* The Upsample conv (nearest x2, then 3x3 / pad 1: encoder_decoder.py:194-209, Upsample) on the Winograd form: four 3x3 /
+ * pad-1 class convs on the low-resolution input x [nb][h][w][cin], one per output parity class (p, q) -- class kernel
+ * K_pq = the sub-pixel form's tap sums embedded in a 3x3 support -- sharing x's input transform:
+ *   upsample_weights: w [cout][3][3][cin] -> kc [4 cout][3][3][cin] (row pq * cout + k); weight_transform(kc, 4 cout)
+ *                     then gives U (forward, dgrad 0) or U' (input gradient, dgrad 1)
+ *   gemm(V of x, U, n_out = 4 cout) -> output_transform_upsample -> y [nb][2h][2w][cout] (+ bias)
+ *   dy_transforms_upsample: dy [nb][2h][2w][cout] -> V' (nullable) and D', each [a^2][T][4 cout] from the four class
+ *                     sub-images dy[2i + p][2j + q]; gemm(V', U', k_in = 4 cout, n_out = cin) -> output_transform -> dx
+ *   wgrad_gemm(D', V of x, cout = 4 cout) -> wgrad_output -> dkc [4 cout][3][3][cin]; upsample_fold: dw = beta * dw +
+ *                     each class kernel's gradient summed onto the taps it was built from */
+int mvae_winograd_upsample_weights(const float* w, float* kc, int cin, int cout, void* stream);
+int mvae_winograd_upsample_fold(const float* dkc, float* dw, float beta, int cin, int cout, void* stream);
+int mvae_winograd_output_transform_upsample(const float* m, const float* bias, float* y, int nb, int h, int w, int cout,
+                                            int tile, void* stream);
+int mvae_winograd_dy_transforms_upsample(const float* dy, void* v, void* d, int nb, int h, int w, int cout, int tile,
+                                         void* stream);
 
 /* 3xBF16 operand pre-split (same bytes as the fp32 tensor): per 4 values hi0..hi3 lo0..lo3 bf16,
  * hi = bf16(x) (round to nearest even), lo = bf16(x - hi). The weight-prep entry points below take

@@ -45,6 +45,10 @@ SIGNATURES = {
     "mvae_winograd_dy_transforms": (I, [P, P, P, I, I, I, I, I, I, P]),
     "mvae_winograd_wgrad_gemm": (I, [P, P, P, L, I, I, I, P, Z, P]),
     "mvae_winograd_wgrad_output": (I, [P, P, F, I, I, I, P]),
+    "mvae_winograd_upsample_weights": (I, [P, P, I, I, P]),
+    "mvae_winograd_upsample_fold": (I, [P, P, F, I, I, P]),
+    "mvae_winograd_output_transform_upsample": (I, [P, P, P, I, I, I, I, I, P]),
+    "mvae_winograd_dy_transforms_upsample": (I, [P, P, P, I, I, I, I, I, P]),
     "mvae_conv2d_wgrad_workspace_bytes": (Z, [I, I, I, I, I, I, I]),
     "mvae_conv2d_wgrad_small_cout_nhwc": (I, [P, P, P, P, F, I, I, I, I, I, I, P, Z, P]),
     "mvae_conv2d_wgrad_small_cout_workspace_bytes": (Z, [I, I]),

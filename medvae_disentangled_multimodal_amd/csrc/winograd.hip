@@ -488,9 +488,34 @@ __global__ void __launch_bounds__(256) wino_out_any_kernel(WinoOut p) {
   }
 }
 
-// dy [nb][H][W][K] (fp32, or split4_bf16 groups when XS) -> D' = A D A^T [a^2][T][K] split4_bf16: one thread per
-// (tile, 4-group)
-template <int MT, bool XS, int SF = 0>
+// Where the output-gradient 4-group k4 of low-resolution pixel (h, w) of image b lives (byte offset): the dy [nb][H][W][K]
+// of a conv; or, UPS (the Upsample conv run as 4 class convs on its low-resolution input, K = 4 cout, k4 = class pq x
+// cout / 4 + c4), the class-pq sub-image of the full-resolution dy [nb][2H][2W][cout] -- pixel (2h + p, 2w + q)
+template <bool UPS>
+struct DySrc {
+  unsigned pix0, chan, rowb;  // per image / class: base pixel, byte offset of the 4-group, bytes per pixel
+  int H, W;
+  __device__ DySrc(int b, int k4, int H_, int W_, int K) : H(H_), W(W_) {
+    if constexpr (UPS) {
+      const int cq4 = K >> 4, pq = k4 / cq4, c4 = k4 - pq * cq4;  // (K / 4 = cout: 4-groups per class = K / 16)
+      pix0 = (unsigned)((b * 2 * H + (pq >> 1)) * 2 * W + (pq & 1));
+      chan = (unsigned)c4 * 16u;
+      rowb = (unsigned)(K >> 2) * 4u;
+    } else {
+      pix0 = (unsigned)(b * H * W);
+      chan = (unsigned)k4 * 16u;
+      rowb = (unsigned)K * 4u;
+    }
+  }
+  __device__ unsigned off(int h, int w) const {  // (h, w) inside the low-resolution image
+    if constexpr (UPS) return (pix0 + (unsigned)(2 * h * 2 * W + 2 * w)) * rowb + chan;
+    else return (pix0 + (unsigned)(h * W + w)) * rowb + chan;
+  }
+};
+
+// dy [nb][H][W][K] (fp32, or split4_bf16 groups when XS; UPS: the Upsample conv's class sub-images, DySrc) -> D' =
+// A D A^T [a^2][T][K] split4_bf16: one thread per (tile, 4-group)
+template <int MT, bool XS, int SF = 0, bool UPS = false>
 __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ dy, uint4* __restrict__ d, int nb, int H,
                                                       int W, int K) {
   constexpr int AL = MT + 2;
@@ -502,6 +527,7 @@ __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ 
   const int k4 = (int)(idx - t * K4);
   const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
   const __amdgpu_buffer_rsrc_t dr = make_rsrc(dy, (unsigned)((long long)nb * H * W * K * 4));
+  const DySrc<UPS> src(b, k4, H, W, K);
   const unsigned plane = (unsigned)(T * K4) * wgb<SF>(), base = (unsigned)(t * K4 + k4) * wgb<SF>();
   const __amdgpu_buffer_rsrc_t vr = make_rsrc(d, plane * (unsigned)(AL * AL));
   float4 v[MT][MT];
@@ -510,8 +536,7 @@ __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ 
 #pragma unroll
     for (int e = 0; e < MT; ++e) {
       const int h = MT * ti + a, w = MT * tj + e;  // (pixels past the image edge carry no gradient: zero)
-      const float4 r = bload4(dr, (h < H && w < W) ? ((unsigned)((b * H + h) * W + w) * (unsigned)K) * 4u +
-                                                         (unsigned)k4 * 16u : OOB);
+      const float4 r = bload4(dr, (h < H && w < W) ? src.off(h, w) : OOB);
       v[a][e] = XS ? split4_to_f32(r) : r;
     }
   constexpr auto ac = [](int i, int k) { return wino_at<MT>(k, i); };  // A = (A^T)^T
@@ -531,7 +556,7 @@ __global__ void __launch_bounds__(256) wino_dy_kernel(const float* __restrict__ 
 // D' = A D A^T of the m x m tile D = P[1..m][1..m] inside it (the weight gradient's transformed output gradient, as
 // wino_dy_kernel) -- the separate kernels each read all of dy. One thread per (tile, 4-group); D' one output row at a
 // time (181-215 VGPRs: the patch plus one row; 2 waves per SIMD, as the input transform).
-template <int MT, bool XS, int SF = 0>
+template <int MT, bool XS, int SF = 0, bool UPS = false>
 __global__ void __launch_bounds__(256) wino_dy2_kernel(const float* __restrict__ dy, uint4* __restrict__ v,
                                                        uint4* __restrict__ d, int nb, int H, int W, int K) {
   constexpr int AL = MT + 2;
@@ -543,7 +568,7 @@ __global__ void __launch_bounds__(256) wino_dy2_kernel(const float* __restrict__
   const int k4 = (int)(idx - t * K4);
   const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(dy, (unsigned)((long long)nb * H * W * K * 4));
-  const unsigned kb = (unsigned)k4 * 16u;
+  const DySrc<UPS> src(b, k4, H, W, K);
   const unsigned plane = (unsigned)(T * K4) * wgb<SF>(), base = (unsigned)(t * K4 + k4) * wgb<SF>();
   const __amdgpu_buffer_rsrc_t vr = make_rsrc(v, plane * (unsigned)(AL * AL));
   const __amdgpu_buffer_rsrc_t dr = make_rsrc(d, plane * (unsigned)(AL * AL));
@@ -554,7 +579,7 @@ __global__ void __launch_bounds__(256) wino_dy2_kernel(const float* __restrict__
     for (int j = 0; j < AL; ++j) {
       const int h = MT * ti - 1 + i, w = MT * tj - 1 + j;
       const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-      const float4 r = bload4(xr, ok ? ((unsigned)((b * H + h) * W + w) * (unsigned)K) * 4u + kb : OOB);
+      const float4 r = bload4(xr, ok ? src.off(h, w) : OOB);
       p[i][j] = XS ? split4_to_f32(r) : r;
     }
 #pragma unroll
@@ -586,6 +611,110 @@ __global__ void __launch_bounds__(256) wino_dy2_kernel(const float* __restrict__
   for (int i = 0; i < AL; ++i)
 #pragma unroll
     for (int j = 0; j < AL; ++j) wstore_f<SF>(vr, base + (unsigned)(i * AL + j) * plane, p[i][j]);
+}
+
+// The Upsample conv (nearest x2, then a 3x3 / pad-1 conv: encoder_decoder.py:194-209) as four 3x3 / pad-1 convs on the
+// LOW-resolution input, one per output parity class (p, q): output pixel (2i + p, 2j + q) = sum over taps (r, s) of
+// w[r][s] x[i + floor((p + r - 1) / 2)][j + floor((q + s - 1) / 2)], i.e. class kernel K_pq[a][b] = sum of the taps
+// (r, s) with e_p(r) = a, e_q(s) = b, e_0 = (0, 1, 1), e_1 = (1, 1, 2) (the sub-pixel form's tap sums, embedded in a
+// 3x3 support). The four classes share the input transform V of x: one position GEMM over N = 4 cout, (m+2)^2 / (4 m^2)
+// MACs per output pixel per channel pair instead of the sub-pixel form's 4 (0.56x at m = 4).
+__host__ __device__ constexpr int ups_tap(int p, int r) { return p == 0 ? (r == 0 ? 0 : 1) : (r == 2 ? 2 : 1); }
+
+// kc [4 cout][3][3][cin] (row pq * cout + k) from w [cout][3][3][cin]: one thread per (class, k, 4-group of cin)
+__global__ void __launch_bounds__(256) wino_ups_weights_kernel(const float* __restrict__ w, float* __restrict__ kc,
+                                                               int cout, int cin) {
+  const int C4 = cin >> 2;
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 4LL * cout * C4) return;
+  const int c4 = (int)(idx % C4);
+  const long long kq = idx / C4;
+  const int k = (int)(kq % cout), pq = (int)(kq / cout), p = pq >> 1, q = pq & 1;
+  float4 o[3][3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int bb = 0; bb < 3; ++bb) o[a][bb] = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int s2 = 0; s2 < 3; ++s2) {
+      const float4 v = *(const float4*)(w + (((long long)k * 3 + r) * 3 + s2) * cin + c4 * 4);
+      o[ups_tap(p, r)][ups_tap(q, s2)] = f4add(o[ups_tap(p, r)][ups_tap(q, s2)], v);
+    }
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int bb = 0; bb < 3; ++bb) *(float4*)(kc + ((kq * 3 + a) * 3 + bb) * cin + c4 * 4) = o[a][bb];
+}
+
+// dw [cout][3][3][cin] = beta * dw + sum over the classes of the class kernels' gradients dkc [4 cout][3][3][cin] at the
+// taps each original tap feeds (the transpose of wino_ups_weights_kernel), fixed class order
+__global__ void __launch_bounds__(256) wino_ups_fold_kernel(const float* __restrict__ dkc, float* __restrict__ dw,
+                                                            float beta, int cout, int cin) {
+  const int C4 = cin >> 2;
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)cout * C4) return;
+  const int k = (int)(idx / C4), c4 = (int)(idx - (long long)k * C4);
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int s2 = 0; s2 < 3; ++s2) {
+      float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int pq = 0; pq < 4; ++pq) {
+        const long long row = (long long)pq * cout + k;
+        acc = f4add(acc, *(const float4*)(dkc + ((row * 3 + ups_tap(pq >> 1, r)) * 3 + ups_tap(pq & 1, s2)) * cin +
+                                          c4 * 4));
+      }
+      float4* q = (float4*)(dw + (((long long)k * 3 + r) * 3 + s2) * cin + c4 * 4);
+      if (beta != 0.f) {
+        const float4 old = *q;
+        acc = float4{fmaf(beta, old.x, acc.x), fmaf(beta, old.y, acc.y), fmaf(beta, old.z, acc.z),
+                     fmaf(beta, old.w, acc.w)};
+      }
+      *q = acc;
+    }
+}
+
+// M [a^2][T][4 cout] (class-major columns) -> y [nb][2H][2W][cout] = A^T M_pq A at pixels (2i + p, 2j + q) (+ bias):
+// one thread per (low-resolution tile, class, 4-channel group)
+template <int MT>
+__global__ void __launch_bounds__(256) wino_out_ups_kernel(WinoOut p) {
+  constexpr int AL = MT + 2;
+  const int N = p.N, N4 = N >> 2, K4 = N, th = (p.H + MT - 1) / MT, tw = (p.W + MT - 1) / MT;  // (K4: 4 N / 4)
+  const long long T = (long long)p.nb * th * tw;
+  const unsigned mplane = (unsigned)(T * K4 * 16);
+  const __amdgpu_buffer_rsrc_t mr = make_rsrc(p.m, mplane * (unsigned)(AL * AL));
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= T * K4) return;
+  const long long t = idx / K4;
+  const int k4 = (int)(idx - t * K4), pq = k4 / N4, c4 = k4 - pq * N4;
+  const int tj = (int)(t % tw), ti = (int)((t / tw) % th), b = (int)(t / ((long long)tw * th));
+  const float4 bv = p.bias ? *(const float4*)(p.bias + c4 * 4) : float4{0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t yr = make_rsrc(p.y, (unsigned)((long long)p.nb * 4 * p.H * p.W * N * 4));
+  float4 mv[AL][AL];
+#pragma unroll
+  for (int i = 0; i < AL; ++i)
+#pragma unroll
+    for (int j = 0; j < AL; ++j) mv[i][j] = bload4(mr, (unsigned)(t * K4 + k4) * 16u + (unsigned)(i * AL + j) * mplane);
+  constexpr auto at = [](int i, int k) { return wino_at<MT>(i, k); };
+  float4 r[MT][AL];
+#pragma unroll
+  for (int j = 0; j < AL; ++j) wlin<MT, AL>(&r[0][j], AL, &mv[0][j], AL, at);
+#pragma unroll
+  for (int a = 0; a < MT; ++a) {
+    float4 o[MT];
+    wlin<MT, AL>(o, 1, &r[a][0], 1, at);
+    const int row = ti * MT + a;
+#pragma unroll
+    for (int e = 0; e < MT; ++e) {
+      const int col = tj * MT + e;
+      const unsigned off =
+          ((unsigned)((b * 2 * p.H + 2 * row + (pq >> 1)) * 2 * p.W + 2 * col + (pq & 1)) * (unsigned)N + c4 * 4) * 4u;
+      bstore4(yr, (row < p.H && col < p.W) ? off : OOB, f4add(o[e], bv));
+    }
+  }
 }
 
 // dw [cout][3][3][cin] = beta * dw + G^T M G, M [a^2][cout][cin] fp32: one thread per (k, 4-group of c)
@@ -693,11 +822,18 @@ static void in_go(const float* x, void* v, int nb, int h, int w, int c, int xs, 
   else hipLaunchKernelGGL((wino_in_kernel<MT, false, 0, SF>), g, dim3(256), 0, st, x, (uint4*)v, nb, h, w, c, p);
 }
 
-// both = 0: D' only (wino_dy_kernel); 1: V' and D' in one pass (wino_dy2_kernel)
+// both = 0: D' only (wino_dy_kernel); 1: V' and D' in one pass (wino_dy2_kernel); ups: the Upsample conv's class
+// sub-images of the full-resolution dy (k = 4 cout)
 template <int MT, int SF>
-static void dy_go(const float* dy, void* v, void* d, int nb, int h, int w, int k, int xs, bool both, hipStream_t st) {
+static void dy_go(const float* dy, void* v, void* d, int nb, int h, int w, int k, int xs, bool both, hipStream_t st,
+                  bool ups = false) {
   const dim3 g(egrid256(wino_tiles(nb, h, w, MT) * (k / 4)));
   uint4 *vv = (uint4*)v, *dd = (uint4*)d;
+  if (ups) {  // (no pre-split form: the Upsample conv's dy is never split)
+    if (both) hipLaunchKernelGGL((wino_dy2_kernel<MT, false, SF, true>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
+    else hipLaunchKernelGGL((wino_dy_kernel<MT, false, SF, true>), g, dim3(256), 0, st, dy, dd, nb, h, w, k);
+    return;
+  }
   if constexpr (SF != 1) {
     if (xs) {
       if (both) hipLaunchKernelGGL((wino_dy2_kernel<MT, true, SF>), g, dim3(256), 0, st, dy, vv, dd, nb, h, w, k);
@@ -947,6 +1083,64 @@ int mvae_winograd_wgrad_gemm(const void* d, const void* v, float* m, long long t
   if (pk) wgrad_dma(B_COLN, a, (hipStream_t)stream, cfg, 4);
   else launch_big<A_COLM_SPLIT, 4, B_COLN_SPLIT, 4>(a, (hipStream_t)stream, cfg);
   return gemm_finish(a, (hipStream_t)stream);
+}
+
+// The Upsample conv on the Winograd form (see wino_ups_weights_kernel): kc [4 cout][3][3][cin] = the four class kernels
+// of w [cout][3][3][cin], row pq * cout + k -- the forward / input-gradient "weights" of a 3x3 conv with 4 cout outputs
+int mvae_winograd_upsample_weights(const float* w, float* kc, int cin, int cout, void* stream) {
+  if (!w || !kc || cin <= 0 || cout <= 0 || cin % 4 || !al16(w) || !al16(kc)) {
+    set_error("winograd_upsample_weights: cin %% 4 == 0, 16-B aligned");
+    return MVAE_EINVAL;
+  }
+  hipLaunchKernelGGL(wino_ups_weights_kernel, dim3(egrid256(4LL * cout * (cin / 4))), dim3(256), 0, (hipStream_t)stream,
+                     w, kc, cout, cin);
+  return launch_status();
+}
+
+// dw = beta * dw + the class kernels' gradients dkc [4 cout][3][3][cin] folded back onto the 3x3 taps
+int mvae_winograd_upsample_fold(const float* dkc, float* dw, float beta, int cin, int cout, void* stream) {
+  if (!dkc || !dw || cin <= 0 || cout <= 0 || cin % 4 || !al16(dkc) || !al16(dw)) {
+    set_error("winograd_upsample_fold: cin %% 4 == 0, 16-B aligned");
+    return MVAE_EINVAL;
+  }
+  hipLaunchKernelGGL(wino_ups_fold_kernel, dim3(egrid256((long long)cout * (cin / 4))), dim3(256), 0,
+                     (hipStream_t)stream, dkc, dw, beta, cout, cin);
+  return launch_status();
+}
+
+// m [a^2][T][4 cout] (the position GEMM of V of the low-resolution x [nb][h][w][cin] with the class kernels' U) ->
+// y [nb][2h][2w][cout] (+ bias)
+int mvae_winograd_output_transform_upsample(const float* m, const float* bias, float* y, int nb, int h, int w, int cout,
+                                            int tile, void* stream) {
+  if (!m || !y || cout % 4 || !wino_geom_ok(tile, nb, h, w, 4 * cout, 4 * cout) || !al16(m) || !al16(y) ||
+      (bias && !al16(bias)) || (long long)nb * 4 * h * w * cout * 4 > MAX_DESC_BYTES) {
+    set_error("winograd_output_transform_upsample: tile 2 or 4, cout %% 4 == 0, 16-B aligned, operands < 4 GiB");
+    return MVAE_EINVAL;
+  }
+  WinoOut p{};
+  p.m = m; p.bias = bias; p.y = y;
+  p.groups = 1; p.nb = nb; p.H = h; p.W = w; p.N = cout;
+  const dim3 g(egrid256(wino_tiles(nb, h, w, tile) * cout));
+  if (tile == 2) hipLaunchKernelGGL(wino_out_ups_kernel<2>, g, dim3(256), 0, (hipStream_t)stream, p);
+  else hipLaunchKernelGGL(wino_out_ups_kernel<4>, g, dim3(256), 0, (hipStream_t)stream, p);
+  return launch_status();
+}
+
+// The Upsample conv's backward transforms of its full-resolution dy [nb][2h][2w][cout]: for each class pq the sub-image
+// dy[2i + p][2j + q] (an h x w image) -> v = V' [a^2][T][4 cout] (the input gradient's transformed input; null: not
+// wanted) and d = D' [a^2][T][4 cout] (the weight gradient's), columns class-major as the class kernels' rows
+int mvae_winograd_dy_transforms_upsample(const float* dy, void* v, void* d, int nb, int h, int w, int cout, int tile,
+                                         void* stream) {
+  if (!dy || !d || cout % 4 || !wino_geom_ok(tile, nb, h, w, 4 * cout, 4 * cout) || !al16(dy) || !al16(d) ||
+      (v && !al16(v))) {
+    set_error("winograd_dy_transforms_upsample: tile 2 or 4, cout %% 4 == 0, 16-B aligned, operands < 4 GiB");
+    return MVAE_EINVAL;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int sf = wino_sf(), k = 4 * cout;
+  if (tile == 2) WINO_GO(dy_go, 2, dy, v, d, nb, h, w, k, 0, v != nullptr, st, true);
+  else WINO_GO(dy_go, 4, dy, v, d, nb, h, w, k, 0, v != nullptr, st, true);
+  return launch_status();
 }
 
 // dw [cout][3][3][cin] = beta * dw + G^T M G

@@ -304,6 +304,20 @@ def _wino_ok(g, n: int, h: int, wd: int, cin: int, cout: int) -> bool:
 
 _MAX_DESC_BYTES = 0xFFFFFF00  # csrc/gemm_core.h MAX_DESC_BYTES
 
+# The Upsample conv (nearest x2 + 3x3 / pad 1, encoder_decoder.py:194-209) on the Winograd form: four class convs on the
+# low-resolution input (the sub-pixel form's tap sums as 3x3 class kernels, csrc/winograd.hip wino_ups_weights_kernel)
+# sharing one input transform, a position GEMM over N = 4 cout: (m+2)^2 / m^2 MACs per output pixel per channel pair
+# instead of the sub-pixel form's 4 (0.56x at m = 4) for the class-interleaving output transform. Same size rules as the
+# plain Winograd conv on the low-resolution image. MVAE_NO_WINOGRAD_UPSAMPLE=1: the sub-pixel GEMM.
+WINOGRAD_UPSAMPLE = os.environ.get("MVAE_NO_WINOGRAD_UPSAMPLE") is None
+
+
+def _wino_ups_ok(g, n: int, h: int, wd: int, cin: int, cout: int) -> bool:
+    """g an Upsample conv geometry, (h, wd) its low-resolution input."""
+    return (WINOGRAD_UPSAMPLE and _subpixel_upsample(g) and cout % 8 == 0 and _wino_ok(G3, n, h, wd, cin, 4 * cout) and
+            min(cin, cout) >= (WINOGRAD_MIN_C_WIDE if wd >= 32 else WINOGRAD_MIN_C) and
+            4 * n * h * wd * cout * 4 <= _MAX_DESC_BYTES)
+
 
 def _lazy_wino(lazy, x, w, b, res, g, gn_part, wgrad: bool) -> bool:
     """A deferred GroupNorm output can stay deferred: its conv runs the Winograd forward (normalizing on load) and, when
@@ -400,6 +414,12 @@ _DEFERRED_META = {torch.Tensor.shape.__get__, torch.Tensor.size, torch.Tensor.di
                   torch.Tensor.requires_grad.__get__, torch.Tensor.grad_fn.__get__, torch.Tensor.numel,
                   torch.Tensor.layout.__get__, torch.Tensor.stride, torch.Tensor.is_leaf.__get__,
                   torch.Tensor.__hash__, torch.Tensor.element_size, torch.Tensor.get_device}
+
+
+def _wino_ups_wgrad_ok(g, x, dy, dw) -> bool:
+    n, c, h, wd = x.shape
+    return (WINOGRAD_WGRAD and _wino_ups_ok(g, n, h, wd, c, dy.shape[1]) and _al16(x, dy, dw) and
+            dy.is_contiguous(memory_format=CL) and dw.is_contiguous(memory_format=CL))
 
 
 def _wino_wgrad_ok(g, x, dy, dw, dys) -> bool:
@@ -755,6 +775,19 @@ def conv2d_forward_raw(x, w, b, res, g: ConvGeom, x_split: bool = False, gn_part
     # (the Winograd form first: in the bf16-mixed mode it takes the small wide levels off the LDS-DMA path)
     wino = not x_bf16 and _wino_ok(g, n, h, wd, c, co) and _al16(w) and (b is None or _al16(b)) and \
         (res is None or _al16(res)) and (gn_part is None or _wino_blocks(h, wd)) and _al16(lazy.x if lazy is not None else x)
+    wups = not x_bf16 and not x_split and lazy is None and res is None and gn_part is None and \
+        _wino_ups_ok(g, n, h, wd, c, co) and _al16(x, w) and (b is None or _al16(b))
+    if wups:
+        with _timed("conv_fwd", _wino_alg(ref), (n, c, h, wd, co, g.kh, g.stride, g.upsample), ref):
+            kc = ARENA.get("wups_k", 4 * co * 9 * c * 4, x.device)
+            _lib.call("mvae_winograd_upsample_weights", w.data_ptr(), kc.data_ptr(), c, co, st)
+            u = None
+            for b0, b1 in _wino_chunks(n, h, wd, max(c, 4 * co)):
+                m, u = _winograd(x[b0:b1], kc, b1 - b0, h, wd, c, 4 * co, False, False, st, keep_v, key=x, u=u,
+                                 chunk=(b0, b1))
+                _lib.call("mvae_winograd_output_transform_upsample", m.data_ptr(), _ptr(b), y[b0:b1].data_ptr(),
+                          b1 - b0, h, wd, co, _wtile(), st)
+        return y
     if not wino and _dma_ok(ref / 2) and c % 8 == 0 and not x_split and _al16(x) and not g.pointwise and \
             g.kh * g.kw <= 32 and (sub or not g.upsample):
         return _conv_fwd_bf16(x, w, b, res, g, y, n, c, h, wd, co, ho, wo, sub, alg, ref, gn_part, st, x_bf16)
@@ -837,7 +870,8 @@ def pack_dy(dy: torch.Tensor, g: ConvGeom, cin: int, bias_out=None, beta: float 
     (mvae_pack_bf16_colsum). Returns (packed dy or None, whether the bias gradient was produced)."""
     if not _bf16_dma() or g.pointwise or dy.dim() != 4 or dy.shape[1] % 8 or g.kh * g.kw > 32 or not _al16(dy) or \
             not dy.is_contiguous(memory_format=CL) or not _dma_ok(float(dy.numel()) * cin * g.kh * g.kw) or \
-            _wino_ok(g, dy.shape[0], dy.shape[2], dy.shape[3], cin, dy.shape[1]):  # (Winograd: both passes read fp32 dy)
+            _wino_ok(g, dy.shape[0], dy.shape[2], dy.shape[3], cin, dy.shape[1]) or \
+            _wino_ups_ok(g, dy.shape[0], dy.shape[2] // 2, dy.shape[3] // 2, cin, dy.shape[1]):  # (Winograd: fp32 dy)
         return None, False
     if bias_out is None:
         return pack_bf16(dy, "dybf"), False
@@ -874,6 +908,32 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
     st = _stream(dy)
     flops = 2.0 * n * ho * wo * co * c * g.kh * g.kw  # reference count
     shp = (n, c, h, wd, co, g.kh, g.stride, g.upsample)
+    if dyb is None and dys is None and _wino_ups_ok(g, n, h, wd, c, co) and _al16(dy, w) and \
+            dy.is_contiguous(memory_format=CL):
+        # the Upsample conv's input gradient on the Winograd form: sum over the classes of the class sub-images of dy
+        # convolved with the flipped, transposed class kernels -- one GEMM over K = 4 cout
+        mt = _wtile()
+        pos = (mt + 2) ** 2
+        with _timed("conv_dgrad", _wino_alg(flops), shp, flops):
+            kc = ARENA.get("wups_k", 4 * co * 9 * c * 4, dy.device)
+            _lib.call("mvae_winograd_upsample_weights", w.data_ptr(), kc.data_ptr(), c, co, st)
+            u = ARENA.get("wino_u", _wel() * pos * c * 4 * co, dy.device)
+            _lib.call("mvae_winograd_weight_transform", kc.data_ptr(), u.data_ptr(), c, 4 * co, 1, mt, st)
+            for b0, b1 in _wino_chunks(n, h, wd, max(c, 4 * co)):
+                nb, t = b1 - b0, _wino_tiles(b1 - b0, h, wd)
+                v = ARENA.get("wino_v", _wel() * pos * t * 4 * co, dy.device)
+                if dkeep is not None:
+                    d = torch.empty(_wel() * pos * t * 4 * co, dtype=torch.uint8, device=dy.device)
+                    dkeep.append((d, mt, dy.data_ptr(), dy._version, (b0, b1)))
+                else:
+                    d = ARENA.get("wino_d", _wel() * pos * t * 4 * co, dy.device)
+                _lib.call("mvae_winograd_dy_transforms_upsample", dy[b0:b1].data_ptr(), v.data_ptr(), d.data_ptr(), nb,
+                          h, wd, co, mt, st)
+                m = ARENA.get("wino_m", 4 * pos * t * c, dy.device)
+                _lib.call("mvae_winograd_gemm", v.data_ptr(), u.data_ptr(), m.data_ptr(), t, 4 * co, c, mt, st)
+                _lib.call("mvae_winograd_output_transform", m.data_ptr(), None, None, dx[b0:b1].data_ptr(), None, nb, h,
+                          wd, c, mt, st)
+        return dx
     if dyb is not None and (gn_link is None or not gn_link.usable(dx)):
         return _conv_dgrad_bf16(dyb, w, dx, g, n, c, h, wd, co, ho, wo, flops, shp, st)
     if dys is not None and (g.pointwise or co % 4):
@@ -991,7 +1051,7 @@ def conv2d_wgrad_raw(dy, x, dw, beta: float, g: ConvGeom, db=None, x_split: bool
         x, lazy = lazy.materialize(), None
     ref = 2.0 * n * ho * wo * co * c * g.kh * g.kw
     alg = ref * 4 / 9 if _subpixel_upsample(g) else ref
-    if dyb is None and _wino_wgrad_ok(g, x if lazy is None else lazy.x, dy, dw, dys):
+    if dyb is None and (_wino_wgrad_ok(g, x if lazy is None else lazy.x, dy, dw, dys) or _wino_ups_wgrad_ok(g, x, dy, dw)):
         alg = _wino_alg(ref)
     if dyb is not None and not x_split and not g.upsample and c % 8 == 0 and co % 8 == 0 and _al16(x):
         # bf16-mixed weight gradient on packed bf16 dy and x (LDS-DMA main loop); the bias gradient is summed from the
@@ -1049,6 +1109,33 @@ def _conv_wgrad_launch(dy, x, dw, beta, g, n, c, h, wd, co, ho, wo, db=None, x_s
         _lib.call("mvae_conv2d_wgrad_direct_nhwc", dy.data_ptr(), x.data_ptr(), dw.data_ptr(), _ptr(db), float(beta),
                   n, h, wd, c, co, int(x_split), ws.data_ptr(), ws.numel(), st)
         return db is not None
+    if not deferred and not x_split and _wino_ups_wgrad_ok(g, x, dy, dw):
+        # the Upsample conv's weight gradient on the Winograd form: the class kernels' gradients G^T [sum_t D'_pq (.) V] G
+        # (D' of the class sub-images of dy, kept by the input gradient's pass; V the forward's), folded onto the taps
+        mt = _wtile()
+        pos = (mt + 2) ** 2
+        dev = dy.device
+        kept = {e[4]: e[0] for e in wino_v or () if e[1] == mt and e[2] == x.data_ptr() and e[3] == x._version}
+        kept_d = {e[4]: e[0] for e in wino_d or () if e[1] == mt and e[2] == dy.data_ptr() and e[3] == dy._version}
+        dkc = ARENA.get("wups_dk", 4 * co * 9 * c * 4, dev)
+        for i, (b0, b1) in enumerate(_wino_chunks(n, h, wd, max(c, 4 * co))):
+            nb, t = b1 - b0, _wino_tiles(b1 - b0, h, wd)
+            v, dt = kept.get((b0, b1)), kept_d.get((b0, b1))
+            if dt is None:
+                dt = ARENA.get("wino_d", _wel() * pos * t * 4 * co, dev)
+                _lib.call("mvae_winograd_dy_transforms_upsample", dy[b0:b1].data_ptr(), None, dt.data_ptr(), nb, h, wd,
+                          co, mt, st)
+            if v is None:
+                v = ARENA.get("wino_v", _wel() * pos * t * c, dev)
+                _lib.call("mvae_winograd_input_transform", x[b0:b1].data_ptr(), v.data_ptr(), nb, h, wd, c, 0, mt, st)
+            m = ARENA.get("wino_mw", 4 * pos * 4 * co * c, dev)
+            ws = ARENA.get("ws", _lib.query("mvae_gemm_workspace_bytes", 4 * co, c, t, pos), dev)
+            _lib.call("mvae_winograd_wgrad_gemm", dt.data_ptr(), v.data_ptr(), m.data_ptr(), t, 4 * co, c, mt,
+                      ws.data_ptr(), ws.numel(), st)
+            _lib.call("mvae_winograd_wgrad_output", m.data_ptr(), dkc.data_ptr(), 0.0 if i == 0 else 1.0, 4 * co, c, mt,
+                      st)
+        _lib.call("mvae_winograd_upsample_fold", dkc.data_ptr(), dw.data_ptr(), float(beta), c, co, st)
+        return False
     if not deferred and _subpixel_upsample(g):
         nbytes = _lib.query("mvae_conv2d_wgrad_upsample_workspace_bytes", n, h, wd, c, co)
         ws = ARENA.get("ws", nbytes, dy.device)
@@ -1344,7 +1431,7 @@ class Conv2dFn(torch.autograd.Function):
         n_, c_, h_, w_ = x.shape
         dkeep = [] if (WINOGRAD_DY2 and side is None and dyb is None and ctx.needs_input_grad[0] and
                        ctx.needs_input_grad[1] and WINOGRAD_WGRAD and not g.pointwise and
-                       _wino_ok(g, n_, h_, w_, c_, w.shape[0])) else None
+                       (_wino_ok(g, n_, h_, w_, c_, w.shape[0]) or _wino_ups_ok(g, n_, h_, w_, c_, w.shape[0]))) else None
         if ctx.needs_input_grad[0]:
             dx = conv2d_dgrad_raw(dy, w, x.shape, g, link if ctx.x_sink is None else None, dys=dys, dyb=dyb,
                                   dkeep=dkeep)

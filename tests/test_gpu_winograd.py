@@ -766,3 +766,85 @@ def test_groupnorm_partials_from_winograd_input_gradient(dev, monkeypatch, _wino
     yr.backward(dy0.double())
     for a, b in zip(linked, (yr, xr.grad, war.grad, bar_.grad, gr.grad, br.grad, wbr.grad)):
         assert rel(a, b) < CONV_TOL
+
+
+UPS_CASES = [(2, 64, 64, 8, 8), (2, 32, 64, 16, 16), (1, 64, 32, 7, 7), (2, 128, 64, 4, 32)]
+
+
+@pytest.mark.parametrize("prec", ["32", "32-exact", "bf16-mixed"])
+@pytest.mark.parametrize("n,ci,co,h,w", UPS_CASES)
+def test_winograd_upsample_conv(dev, n, ci, co, h, w, prec, monkeypatch, _wino_on):
+    """The Upsample conv (nearest x2 + 3x3 / pad 1) as four class convs sharing one Winograd input transform: forward
+    with bias, input gradient and weight gradient through ops.conv2d, against float64 (3xBF16 at the conv bar, exact
+    fp32 at 5e-6) or, in the bf16 mode, against the float64 emulation of the same algorithm (tests/wino_ref.py)."""
+    import torch.nn.functional as F
+    import wino_ref as W
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    monkeypatch.setattr(ops, "WINOGRAD_TILE_BF16", _wino_on)
+    monkeypatch.setattr(ops, "WINOGRAD_BF16_MAX_W", 64)
+    g = torch.Generator().manual_seed(n * ci + co + h + w)
+    x0 = torch.randn(n, ci, h, w, generator=g)
+    w0 = torch.randn(co, ci, 3, 3, generator=g) / (3 * ci ** 0.5)
+    b0 = torch.randn(co, generator=g) * 0.1
+    dy0 = torch.randn(n, co, 2 * h, 2 * w, generator=g)
+    seen = []
+    orig = _lib.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return orig(name, *args)
+    x = cl(x0, dev).requires_grad_(True)
+    wt = w0.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    b = b0.to(dev).requires_grad_(True)
+    monkeypatch.setattr(_lib, "call", spy)
+    pv = ops.set_precision(prec)
+    try:
+        y = ops.conv2d(x, wt, b, ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, True))
+        y.backward(cl(dy0, dev))
+        torch.cuda.synchronize()
+    finally:
+        ops.restore_math_mode(pv)
+        monkeypatch.setattr(_lib, "call", orig)
+    assert {"mvae_winograd_output_transform_upsample", "mvae_winograd_dy_transforms_upsample",
+            "mvae_winograd_upsample_fold"} <= set(seen)
+    assert "mvae_conv2d_upsample_nhwc" not in seen and "mvae_conv2d_wgrad_upsample_nhwc" not in seen
+    assert tuple(y.shape) == (n, co, 2 * h, 2 * w)
+    if prec == "bf16-mixed":
+        m = _wino_on
+        refs = (W.ups_conv(x0, w0, m, W.bf16) + b0.double().view(1, -1, 1, 1), W.ups_dgrad(dy0, w0, m, W.bf16),
+                W.ups_wgrad(x0, dy0, m, W.bf16))
+        tol = 2e-4 if m == 2 else 1e-3
+    else:
+        xr, wr, br = (t.double().requires_grad_() for t in (x0, w0, b0))
+        yr = F.conv2d(F.interpolate(xr, scale_factor=2.0, mode="nearest"), wr, br, padding=1)
+        yr.backward(dy0.double())
+        refs = (yr, xr.grad, wr.grad)
+        tol = CONV_TOL if prec == "32" else 5e-6
+    errs = {k: rel(a, r) for k, a, r in zip(("y", "dx", "dw"), (y, x.grad, wt.grad), refs)}
+    assert all(v < tol for v in errs.values()), errs
+    assert rel(b.grad, dy0.double().sum((0, 2, 3))) < 1e-5
+
+
+def test_winograd_upsample_image_chunks(dev, monkeypatch, _wino_on):
+    """The Upsample conv's Winograd form over image chunks (5 images, chunks of 2 / 2 / 1 under a small descriptor
+    limit): the class kernels' gradients accumulate over the chunks before the fold."""
+    import torch.nn.functional as F
+    from medvae_disentangled_multimodal_amd import ops
+    n, c, co, h, w = 5, 32, 32, 8, 8
+    per_img = (_wino_on + 2) ** 2 * ops._wino_tiles(1, h, w) * 4 * co * 4
+    monkeypatch.setattr(ops, "_MAX_DESC_BYTES", 2 * per_img)
+    assert ops._wino_chunks(n, h, w, 4 * co) == [(0, 2), (2, 4), (4, 5)]
+    g = torch.Generator().manual_seed(8)
+    x0 = torch.randn(n, c, h, w, generator=g)
+    w0 = torch.randn(co, c, 3, 3, generator=g) / (3 * c ** 0.5)
+    dy0 = torch.randn(n, co, 2 * h, 2 * w, generator=g)
+    x = cl(x0, dev).requires_grad_(True)
+    wt = w0.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = ops.conv2d(x, wt, None, ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, True))
+    y.backward(cl(dy0, dev))
+    torch.cuda.synchronize()
+    xr, wr = x0.double().requires_grad_(), w0.double().requires_grad_()
+    yr = F.conv2d(F.interpolate(xr, scale_factor=2.0, mode="nearest"), wr, None, padding=1)
+    yr.backward(dy0.double())
+    for a, r in ((y, yr), (x.grad, xr.grad), (wt.grad, wr.grad)):
+        assert rel(a, r) < CONV_TOL

@@ -41,3 +41,17 @@ def test_bf16_emulation_error_levels():
     e2, e4 = rel(W.conv(x, wt, 2, W.bf16)), rel(W.conv(x, wt, 4, W.bf16))
     direct = rel(F.conv2d(W.bf16(x), W.bf16(wt), padding=1))
     assert 1e-3 < direct < 4e-3 and 2.5e-3 < e2 < 6e-3 and 1.5e-2 < e4 < 4e-2
+
+
+@pytest.mark.parametrize("m", [2, 4])
+def test_upsample_emulation_is_the_upsampled_convolution(m):
+    g = torch.Generator().manual_seed(3 + m)
+    x = torch.randn(2, 6, 7, 5, dtype=torch.float64, generator=g)
+    wt = torch.randn(4, 6, 3, 3, dtype=torch.float64, generator=g)
+    dy = torch.randn(2, 4, 14, 10, dtype=torch.float64, generator=g)
+    xr, wr = x.clone().requires_grad_(), wt.clone().requires_grad_()
+    y = F.conv2d(F.interpolate(xr, scale_factor=2.0, mode="nearest"), wr, padding=1)
+    y.backward(dy)
+    assert torch.allclose(W.ups_conv(x, wt, m, W.ident), y, atol=1e-11)
+    assert torch.allclose(W.ups_dgrad(dy, wt, m, W.ident), xr.grad, atol=1e-11)
+    assert torch.allclose(W.ups_wgrad(x, dy, m, W.ident), wr.grad, atol=1e-11)

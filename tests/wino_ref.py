@@ -110,3 +110,49 @@ def wgrad(x, dy, m, rnd, cols=None, chunk=8):
         dd = rnd(torch.einsum("ji,nktwjl,lm->nktwim", A, dt, A))  # A D A^T with A = (A^T)^T: [a, a]
         mm += torch.einsum("nktwij,nctwij->kcij", dd, v)
     return torch.einsum("ji,kcjl,lm->kcim", g, mm, g)
+
+
+UPS_TAP = ((0, 1, 1), (1, 1, 2))  # embedded tap of original tap r for output parity p (csrc/winograd.hip ups_tap)
+
+
+def ups_class_kernels(w):
+    """The Upsample conv's four class kernels K_pq [4, K, C, 3, 3] (float64) of w [K, C, 3, 3]: output pixel
+    (2i + p, 2j + q) of nearest-x2 + 3x3 / pad-1 conv = the 3x3 / pad-1 conv of the low-resolution input with K_pq."""
+    w = w.double()
+    kc = torch.zeros(4, *w.shape, dtype=torch.float64)
+    for pq in range(4):
+        p, q = pq >> 1, pq & 1
+        for r in range(3):
+            for s in range(3):
+                kc[pq, :, :, UPS_TAP[p][r], UPS_TAP[q][s]] += w[:, :, r, s]
+    return kc
+
+
+def ups_conv(x, w, m, rnd):
+    """Winograd emulation of the Upsample conv: [N, K, 2H, 2W]."""
+    kc = ups_class_kernels(w)
+    n, c, h, wd = x.shape
+    y = torch.zeros(n, w.shape[0], 2 * h, 2 * wd, dtype=torch.float64)
+    for pq in range(4):
+        y[:, :, pq >> 1::2, pq & 1::2] = conv(x, kc[pq], m, rnd)
+    return y
+
+
+def ups_dgrad(dy, w, m, rnd):
+    """... its input gradient [N, C, H, W]: sum over the classes of the class sub-images of dy through the flipped,
+    transposed class kernels."""
+    kc = ups_class_kernels(w)
+    return sum(conv(dy[:, :, pq >> 1::2, pq & 1::2], dgrad_weights(kc[pq]), m, rnd) for pq in range(4))
+
+
+def ups_wgrad(x, dy, m, rnd):
+    """... its weight gradient [K, C, 3, 3]: each class kernel's Winograd gradient, summed onto the taps it was built
+    from."""
+    dw = torch.zeros(dy.shape[1], x.shape[1], 3, 3, dtype=torch.float64)
+    for pq in range(4):
+        dk = wgrad(x, dy[:, :, pq >> 1::2, pq & 1::2], m, rnd)
+        p, q = pq >> 1, pq & 1
+        for r in range(3):
+            for s in range(3):
+                dw[:, :, r, s] += dk[:, :, UPS_TAP[p][r], UPS_TAP[q][s]]
+    return dw
