@@ -309,12 +309,17 @@ _MAX_DESC_BYTES = 0xFFFFFF00  # csrc/gemm_core.h MAX_DESC_BYTES
 # sharing one input transform, a position GEMM over N = 4 cout: (m+2)^2 / m^2 MACs per output pixel per channel pair
 # instead of the sub-pixel form's 4 (0.56x at m = 4) for the class-interleaving output transform. Same size rules as the
 # plain Winograd conv on the low-resolution image. MVAE_NO_WINOGRAD_UPSAMPLE=1: the sub-pixel GEMM.
+# Measured (same box, interleaved, profiles/r06_ab_c4_upsample_gnlink.txt, r06_ab_c5.txt): c4 725 -> 740 img/s; in the
+# bf16-mixed mode F(2x2) on the Upsample convs lost (c5 964 -> 942), so that mode keeps them on the LDS-DMA sub-pixel
+# GEMM (MVAE_WINOGRAD_UPSAMPLE_BF16=1 enables them there).
 WINOGRAD_UPSAMPLE = os.environ.get("MVAE_NO_WINOGRAD_UPSAMPLE") is None
+WINOGRAD_UPSAMPLE_BF16 = os.environ.get("MVAE_WINOGRAD_UPSAMPLE_BF16") is not None
 
 
 def _wino_ups_ok(g, n: int, h: int, wd: int, cin: int, cout: int) -> bool:
     """g an Upsample conv geometry, (h, wd) its low-resolution input."""
-    return (WINOGRAD_UPSAMPLE and _subpixel_upsample(g) and cout % 8 == 0 and _wino_ok(G3, n, h, wd, cin, 4 * cout) and
+    return (WINOGRAD_UPSAMPLE and (_MATH[0] != 1 or WINOGRAD_UPSAMPLE_BF16) and _subpixel_upsample(g) and
+            cout % 8 == 0 and _wino_ok(G3, n, h, wd, cin, 4 * cout) and
             min(cin, cout) >= (WINOGRAD_MIN_C_WIDE if wd >= 32 else WINOGRAD_MIN_C) and
             4 * n * h * wd * cout * 4 <= _MAX_DESC_BYTES)
 
@@ -365,9 +370,12 @@ WINOGRAD_DY2 = os.environ.get("MVAE_NO_WINOGRAD_DY2") is None
 # runs at the plain one's speed and c4 gains 2 % (704-706 -> 717-721 img/s, GroupNorm family 40.5 -> 31.9 ms; same box,
 # interleaved, profiles/r05_winograd_gn_ab.txt). MVAE_NO_WINOGRAD_GN=1 writes the GroupNorm output as before.
 WINOGRAD_GN = os.environ.get("MVAE_NO_WINOGRAD_GN") is None
-# ... and where that GroupNorm's backward streams (the large levels), its partial pass over x and dy comes from the
-# conv's Winograd input-gradient output transform instead; MVAE_NO_WINOGRAD_GN_LINK=1: the pass
-WINOGRAD_GN_LINK = os.environ.get("MVAE_NO_WINOGRAD_GN_LINK") is None
+# ... and where that GroupNorm's backward streams (the large levels), its partial pass over x and dy can come from the
+# conv's Winograd input-gradient output transform instead (MVAE_WINOGRAD_GN_LINK=1). Measured and left
+# opt-in: the GroupNorm family gets 3.5 ms per c4 step faster (31.5 -> 28.0 ms), but the input-gradient output transform
+# that also reads x and sums the fp64 partials costs more (c4 755 -> 740 img/s, same box, interleaved,
+# profiles/r06_ab_c4_upsample_gnlink.txt)
+WINOGRAD_GN_LINK = os.environ.get("MVAE_WINOGRAD_GN_LINK") is not None
 GN_LAZY_ATTR = "_mvae_gn_lazy"
 G3 = ConvGeom(3, 3, 1, 1, 1, 1, 1, False)  # the GroupNorm-fed convs' geometry (ResnetBlock conv1 / conv2, conv_out)
 

@@ -782,6 +782,7 @@ def test_winograd_upsample_conv(dev, n, ci, co, h, w, prec, monkeypatch, _wino_o
     from medvae_disentangled_multimodal_amd import _lib, ops
     monkeypatch.setattr(ops, "WINOGRAD_TILE_BF16", _wino_on)
     monkeypatch.setattr(ops, "WINOGRAD_BF16_MAX_W", 64)
+    monkeypatch.setattr(ops, "WINOGRAD_UPSAMPLE_BF16", True)
     g = torch.Generator().manual_seed(n * ci + co + h + w)
     x0 = torch.randn(n, ci, h, w, generator=g)
     w0 = torch.randn(co, ci, 3, 3, generator=g) / (3 * ci ** 0.5)
