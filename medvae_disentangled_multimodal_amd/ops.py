@@ -318,8 +318,10 @@ WINOGRAD_UPSAMPLE_BF16 = os.environ.get("MVAE_WINOGRAD_UPSAMPLE_BF16") is not No
 
 def _wino_ups_ok(g, n: int, h: int, wd: int, cin: int, cout: int) -> bool:
     """g an Upsample conv geometry, (h, wd) its low-resolution input."""
+    # (whole tiles only: c2's 7 -> 14 Upsample at 512 channels, in 2 x 2 tiles of 4 x 4 over a 7 x 7 image, lost 1.4 %,
+    # profiles/r06_ab_c2_upsample.txt)
     return (WINOGRAD_UPSAMPLE and (_MATH[0] != 1 or WINOGRAD_UPSAMPLE_BF16) and _subpixel_upsample(g) and
-            cout % 8 == 0 and _wino_ok(G3, n, h, wd, cin, 4 * cout) and
+            h % _wtile() == 0 and wd % _wtile() == 0 and cout % 8 == 0 and _wino_ok(G3, n, h, wd, cin, 4 * cout) and
             min(cin, cout) >= (WINOGRAD_MIN_C_WIDE if wd >= 32 else WINOGRAD_MIN_C) and
             4 * n * h * wd * cout * 4 <= _MAX_DESC_BYTES)
 
