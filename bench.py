@@ -100,7 +100,7 @@ def _pmc_traffic(config, family="gemm"):
     committed PMC passes (tools/gpu_evidence.sh traffic: FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc, separate passes) --
     counters cannot be read inside this timed run, so the profile of the same command is attached (newest round
     first)."""
-    for tag in ("r05", "r04", "r03", "r02", "r01"):
+    for tag in ("r06", "r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", f"{tag}_{config}_{family}_traffic.json")
         if os.path.exists(path):
             break
