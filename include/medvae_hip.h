@@ -336,6 +336,13 @@ size_t mvae_group_norm_colsum_workspace_bytes(int nb, int hw, int c);
 /* The same with dx also written as split4_bf16 groups (dx_split: 4 B per element at dx's element offsets, 16-B
  * aligned; mvae_split_bf16's layout) -- the fp32-class (3xBF16) GEMMs' pre-split dY operand of the producing conv's
  * input and weight gradients (MVAE_CONV_XSPLIT / MVAE_CONV_DYSPLIT), with the conv bias gradient as above. */
+/* ... with dx in fp32 only, plus the producing conv's bias gradient (the column sums of dx, accumulated with bias_beta):
+ * the exact-fp32 arithmetic's and the Winograd Upsample conv's replacement for a separate column-sum pass over dy. */
+int mvae_group_norm_bwd_colsum_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
+                                    const float* mean, const float* rstd, float* dx, const float* dx_add, float* dgamma,
+                                    float* dbeta, int nb, int hw, int c, int groups, int silu, float drop_p,
+                                    unsigned long long seed, void* workspace, size_t workspace_bytes, float* dbias,
+                                    float bias_beta, void* cs_workspace, size_t cs_workspace_bytes, void* stream);
 int mvae_group_norm_bwd_split_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
                                    const float* mean, const float* rstd, float* dx, const float* dx_add, float* dgamma,
                                    float* dbeta, int nb, int hw, int c, int groups, int silu, float drop_p,

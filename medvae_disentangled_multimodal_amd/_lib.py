@@ -89,6 +89,8 @@ SIGNATURES = {
                                           P]),
     "mvae_group_norm_bwd_split_nhwc": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, c_uint64, P, Z, P, P, F, P, Z,
                                           P]),
+    "mvae_group_norm_bwd_colsum_nhwc": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, c_uint64, P, Z, P, F, P, Z,
+                                           P]),
     "mvae_group_norm_colsum_workspace_bytes": (Z, [I, I, I]),
     "mvae_set_group_norm_path": (I, [I]),
     "mvae_reparam_fwd": (I, [P, P, L, P, P, L, I, P]),

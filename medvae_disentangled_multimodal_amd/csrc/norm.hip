@@ -443,6 +443,8 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
               ((uint4*)a.dxp)[off >> 2] = split4_bf16(float4{o[0], o[1], o[2], o[3]});
             else
               a.dxp[off >> 2] = uint2{pk_bf16x2(o[0], o[1]), pk_bf16x2(o[2], o[3])};
+          }
+          if (a.csp != nullptr) {  // (uniform) the producing conv's bias gradient
             cs[0] += o[0]; cs[1] += o[1]; cs[2] += o[2]; cs[3] += o[3];
           }
         }
@@ -827,9 +829,9 @@ __device__ __forceinline__ void gn_bwd_unit(const GnArgs& a, int SC, int u, cons
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{pk_bf16x2(o.x, o.y), pk_bf16x2(o.z, o.w)}, pr,
                                               (vo >> 1) + (unsigned)(i * (rstep >> 1)), 0, 0);
       }
-      if (rph + i * rpar < a.hw) {
-        cs[0] += o.x; cs[1] += o.y; cs[2] += o.z; cs[3] += o.w;
-      }
+    }
+    if (a.csp != nullptr && rph + i * rpar < a.hw) {  // (uniform) the producing conv's bias gradient
+      cs[0] += o.x; cs[1] += o.y; cs[2] += o.z; cs[3] += o.w;
     }
   }
   if (a.csp != nullptr) {  // (uniform) per-unit column sums -> csp[b][c0 .. c0 + SC)
@@ -1292,6 +1294,27 @@ int mvae_group_norm_bwd_pack_nhwc(const float* x, const float* dy, const float* 
                 workspace, workspace_bytes, dx_packed, dbias, bias_beta, cs_workspace, stream);
 }
 
+// as mvae_group_norm_bwd_pack_nhwc without the second dx copy: dx and the producing conv's bias gradient (dbias =
+// bias_beta * dbias + column sums of dx) -- for a conv that takes its dy in fp32 (the exact-fp32 arithmetic; the Upsample
+// conv's Winograd form), in place of a separate column-sum pass over dy
+int mvae_group_norm_bwd_colsum_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
+                                    const float* mean, const float* rstd, float* dx, const float* dx_add, float* dgamma,
+                                    float* dbeta, int nb, int hw, int c, int groups, int silu, float drop_p,
+                                    unsigned long long seed, void* workspace, size_t workspace_bytes, float* dbias,
+                                    float bias_beta, void* cs_workspace, size_t cs_workspace_bytes, void* stream) {
+  if (dbias == nullptr || cs_workspace == nullptr || ((uintptr_t)dx & 15) || ((uintptr_t)x & 15) ||
+      ((uintptr_t)dy & 15) || (dx_add && ((uintptr_t)dx_add & 15))) {
+    set_error("group_norm_bwd_colsum: 16-B aligned x / dy / dx, a bias gradient and a column-sum workspace");
+    return MVAE_EINVAL;
+  }
+  if (cs_workspace_bytes < mvae_group_norm_colsum_workspace_bytes(nb, hw, c)) {
+    set_error("group_norm_bwd_colsum: column-sum workspace too small");
+    return MVAE_EWORKSPACE;
+  }
+  return gn_bwd(x, dy, gamma, beta, mean, rstd, dx, dx_add, dgamma, dbeta, nb, hw, c, groups, silu, drop_p, seed,
+                workspace, workspace_bytes, nullptr, dbias, bias_beta, cs_workspace, stream);
+}
+
 // as mvae_group_norm_bwd_pack_nhwc, with dx also written as split4_bf16 groups (the 3xBF16 GEMMs' pre-split operand,
 // 4 B per element at dx's element offsets; 16-B aligned) instead of packed bf16
 int mvae_group_norm_bwd_split_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
@@ -1360,7 +1383,8 @@ static int gn_bwd(const float* x, const float* dy, const float* gamma, const flo
                          dbias, bias_beta);
     return launch_status();
   }
-  if (const int sc2 = dxp ? 0 : gn_unit2_slab(hw, c, groups)) {  // (the packed output: streaming chain)
+  // (the packed output, or the column sums: streaming chain -- the unit kernel writes neither)
+  if (const int sc2 = (dxp || dbias) ? 0 : gn_unit2_slab(hw, c, groups)) {
     double* pws = (double*)workspace;
     const int units = nb * (c / sc2);
     int dev = 0, cus = 0;

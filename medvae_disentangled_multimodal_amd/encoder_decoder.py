@@ -62,9 +62,9 @@ class Conv2d(nn.Module):
             nn.init.uniform_(self.bias, -bound, bound)
 
     def forward(self, x, residual=None, geom: Optional[ConvGeom] = None, res_sink=None, x_sink=None,
-                gn_stats: bool = False):
+                gn_stats: bool = False, gn_bias: bool = False):
         # gn_stats: the output feeds a Normalize; its statistics come out of the conv's epilogue
-        return ops.conv2d(x, self.weight, self.bias, geom or self.geom, residual, res_sink, x_sink, gn_stats)
+        return ops.conv2d(x, self.weight, self.bias, geom or self.geom, residual, res_sink, x_sink, gn_stats, gn_bias)
 
 
 class GroupNorm(nn.Module):
@@ -169,7 +169,8 @@ class Upsample(nn.Module):
         self.geom = ConvGeom(3, 3, 1, 1, 1, 1, 1, upsample=True)
 
     def forward(self, x):
-        return self.conv(x, geom=self.geom)
+        # (the output feeds the next level's ResnetBlock Normalize: gn_bias lets its backward give the bias gradient)
+        return self.conv(x, geom=self.geom, gn_bias=True)
 
 
 class Encoder(nn.Module):

@@ -1249,6 +1249,9 @@ DYPACK = os.environ.get("MVAE_NO_DYPACK") is None
 # operand, MVAE_CONV_XSPLIT; weight gradient: dY^T, MVAE_CONV_DYSPLIT), so neither splits dy in its K loop, and the
 # conv bias gradient summed in the same pass. MVAE_NO_DYSPLIT=1: the conv backward splits dy in registers as before.
 DYSPLIT = os.environ.get("MVAE_NO_DYSPLIT") is None
+# ... and, for a Winograd conv that reads dy in fp32, the bias gradient alone (mvae_group_norm_bwd_colsum_nhwc).
+# MVAE_NO_DYBIAS=1: a separate column-sum pass over dy.
+DYBIAS = os.environ.get("MVAE_NO_DYBIAS") is None
 # only for convs of at least this many MACs (the c4 levels): measured same box, interleaved (profiles/r05_dysplit_ab.txt),
 # c4 +0.9 % (dgrad 442 -> 459, wgrad 414 -> 426 TF/s against +4.3 ms of GroupNorm backward for the extra 4 B per
 # element), while c2 (-0.6 %) and c3 (-3.6 %) lose: their GEMMs gain less than the wider GroupNorm pass costs
@@ -1260,7 +1263,9 @@ class DyPack:
 
     def __init__(self, bias_ref, split: bool = False):
         self.bias_ref = bias_ref
-        self.split = split  # False: packed bf16 (bf16-mixed); True: split4_bf16 (3xBF16)
+        # False: packed bf16 (bf16-mixed); True: split4_bf16 (3xBF16); "bias": the bias gradient only (a conv that reads
+        # dy in fp32 -- the exact-fp32 Winograd convs, the Upsample conv's Winograd form)
+        self.split = split
         self.packed = self.dx_ref = self.dx_version = self.dx_shape = self.db = None
         self.bias_done = False
 
@@ -1375,7 +1380,16 @@ class Conv2dFn(torch.autograd.Function):
         dyb = None
         got = ctx.dypack.take(dy) if ctx.dypack is not None else None
         dys = None
-        if got is not None and ctx.dypack.split:  # dy pre-split (and the bias gradient) by the GroupNorm backward
+        if got is not None and ctx.dypack.split == "bias":  # the bias gradient (column sums of dx) by the GroupNorm
+            _, bias_done, db_ret = got
+            if not want_b:
+                db_ret = None
+            elif bias_done:
+                bt = _main_grad(ctx.bias_ref)
+                if bt is not None:
+                    bt.add_(db_ret)
+                    db_ret = None
+        elif got is not None and ctx.dypack.split:  # dy pre-split (and the bias gradient) by the GroupNorm backward
             dys, bias_done, db_ret = got
             if not want_b:
                 db_ret = None
@@ -1483,7 +1497,8 @@ def _conv_macs(x, weight, geom: ConvGeom) -> float:
     return float(n) * ho * wo * weight.shape[0] * c * geom.kh * geom.kw
 
 
-def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink=None, gn_stats: bool = False):
+def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink=None, gn_stats: bool = False,
+           gn_bias: bool = False):
     """gn_stats=True: the output feeds a Normalize (encoder_decoder.py:28-33) -- emit its statistics from the
     conv's epilogue so the GroupNorm skips its statistics pass (plain implicit-GEMM convs only)."""
     part = None
@@ -1509,6 +1524,14 @@ def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink
             not _subpixel_upsample(geom) and weight.shape[0] % 4 == 0 and geom.kh * geom.kw <= 32 and \
             torch.is_grad_enabled() and _conv_macs(x, weight, geom) >= DYSPLIT_MIN_MACS:
         dyp = DyPack(bias, split=True)
+    elif (gn_stats or gn_bias) and DYBIAS and bias is not None and bias.requires_grad and torch.is_grad_enabled() and \
+            x.dim() == 4 and weight.shape[0] % 4 == 0 and (
+                (_MATH[0] == 2 and not _subpixel_upsample(geom) and
+                 _wino_ok(geom, x.shape[0], x.shape[2], x.shape[3], x.shape[1], weight.shape[0])) or
+                _wino_ups_ok(geom, x.shape[0], x.shape[2], x.shape[3], x.shape[1], weight.shape[0])):
+        # a Winograd conv reading dy in fp32 whose output feeds a GroupNorm: the bias gradient comes out of that
+        # GroupNorm's backward (column sums of its dx) instead of a separate pass over dy
+        dyp = DyPack(bias, split="bias")
     y = Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink, part, link, dyp, torch.is_grad_enabled())
     if part is not None:
         setattr(y, GN_PART_ATTR, (part, y._version))
@@ -1626,10 +1649,18 @@ class GroupNormFn(torch.autograd.Function):
         gpart = ctx.link.take(dy) if ctx.link is not None and drop_p == 0.0 else None
         # algorithmic HBM bytes: read x, dy (and the residual branch's gradient when it is summed here); write dx
         req = ctx.dypack if ctx.dypack is not None and _al16(dy, dx) and (add is None or _al16(add)) else None
-        if req is not None and gpart is not None and not req.split:
+        if req is not None and gpart is not None and req.split is not True:
             req = None  # (the backward from the conv's partials writes split4 dy only)
+        bias_only = req is not None and req.split == "bias"
+        if bias_only and not (req.bias_ref is not None and req.bias_ref.requires_grad):
+            req = None
         packed = tgt = cs = None
-        if req is not None:
+        if bias_only and req is not None:
+            tgt = req.db = torch.empty(c, device=x.device, dtype=torch.float32)
+            csb = _lib.query("mvae_group_norm_colsum_workspace_bytes", n, h * w, c)
+            cs = ARENA.get("gncs", csb, x.device)
+            packed = True  # (DyPack.take's "produced" mark: no second copy of dx)
+        elif req is not None:
             # also dx as packed bf16 / split4 and the producing conv's bias gradient (DyPack)
             # packed bf16: 2 B per element; split4_bf16: 4 B per element, dx's layout (an fp32-sized buffer)
             packed = (torch.empty_like(x, memory_format=CL) if req.split else
@@ -1654,6 +1685,11 @@ class GroupNormFn(torch.autograd.Function):
                           gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
                           _ptr(add), _ptr(dg), _ptr(db), n, h * w, c, groups, silu, ws.data_ptr(), ws.numel(),
                           _stream(x))
+            elif bias_only and req is not None:
+                _lib.call("mvae_group_norm_bwd_colsum_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(),
+                          beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(add), _ptr(dg),
+                          _ptr(db), n, h * w, c, groups, silu, drop_p, seed, ws.data_ptr(), ws.numel(), tgt.data_ptr(),
+                          0.0, cs.data_ptr(), cs.numel(), _stream(x))
             elif req is not None:
                 _lib.call("mvae_group_norm_bwd_split_nhwc" if req.split else "mvae_group_norm_bwd_pack_nhwc",
                           x.data_ptr(), dy.data_ptr(), gamma.data_ptr(),
@@ -1717,7 +1753,7 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
             # the conv's Winograd input-gradient output transform also emits this GroupNorm's backward partials
             # (mvae_winograd_output_gnbwd: one extra read of x there) where the backward would otherwise make a partial
             # pass over x and dy (its streaming chain: the large levels, whose producing conv takes dy pre-split)
-            if (link is None and WINOGRAD_GN_LINK and x.requires_grad and dyp is not None and dyp.split and
+            if (link is None and WINOGRAD_GN_LINK and x.requires_grad and dyp is not None and dyp.split is True and
                     _wino_blocks(h, w) and c % groups == 0 and (c // groups) % 4 == 0 and
                     _lib.query("mvae_group_norm_bwd_streaming", n, h * w, c, groups, 1)):
                 link = GnBwdLink(groups, silu)

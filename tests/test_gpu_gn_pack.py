@@ -65,6 +65,49 @@ def test_gn_bwd_pack_matches_plain_backward(dev, shape, add, fmt):
     assert err < 1e-6, err
 
 
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("add", [False, True])
+def test_gn_bwd_colsum_matches_plain_backward(dev, shape, add):
+    """mvae_group_norm_bwd_colsum_nhwc: the plain backward's dx / dgamma / dbeta bit for bit, plus the producing conv's
+    bias gradient (column sums of dx accumulated onto the bias slot) without a second copy of dx"""
+    from medvae_disentangled_multimodal_amd._lib import call, query
+    nb, h, w, c, g = shape
+    gen = torch.Generator(device=dev).manual_seed(nb * c + h + 7)
+    x = torch.randn(nb, h, w, c, device=dev, generator=gen)
+    dy = torch.randn(nb, h, w, c, device=dev, generator=gen)
+    gamma = 1 + 0.1 * torch.randn(c, device=dev, generator=gen)
+    beta = 0.1 * torch.randn(c, device=dev, generator=gen)
+    dadd = torch.randn(nb, h, w, c, device=dev, generator=gen) if add else None
+    mean = x.view(nb, h * w, g, c // g).mean((1, 3)).reshape(-1).contiguous()
+    rstd = (x.view(nb, h * w, g, c // g).var((1, 3), unbiased=False) + 1e-6).rsqrt().reshape(-1).contiguous()
+    ws = torch.empty(query("mvae_group_norm_workspace_bytes", nb, h * w, c), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    dx0 = torch.empty_like(x)
+    dg0, db0 = torch.zeros(c, device=dev), torch.zeros(c, device=dev)
+    call("mvae_group_norm_bwd_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(),
+         rstd.data_ptr(), dx0.data_ptr(), ptr(dadd), dg0.data_ptr(), db0.data_ptr(), nb, h * w, c, g, 1, 0.0, 0,
+         ws.data_ptr(), ws.numel(), st)
+    dx1 = torch.empty_like(x)
+    dg1, db1 = torch.zeros(c, device=dev), torch.zeros(c, device=dev)
+    bias = torch.randn(c, device=dev, generator=gen)
+    bias0 = bias.clone()
+    cs = torch.empty(query("mvae_group_norm_colsum_workspace_bytes", nb, h * w, c), dtype=torch.uint8, device=dev)
+    call("mvae_group_norm_bwd_colsum_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+         mean.data_ptr(), rstd.data_ptr(), dx1.data_ptr(), ptr(dadd), dg1.data_ptr(), db1.data_ptr(), nb, h * w, c, g,
+         1, 0.0, 0, ws.data_ptr(), ws.numel(), bias.data_ptr(), 1.0, cs.data_ptr(), cs.numel(), st)
+    torch.cuda.synchronize()
+    assert torch.equal(dx1, dx0)
+    assert torch.equal(dg1, dg0) and torch.equal(db1, db0)
+    ref_bias = bias0.double() + dx0.double().sum((0, 1, 2))
+    err = float((bias.double() - ref_bias).abs().max() / ref_bias.abs().max())
+    assert err < 1e-6, err
+    with pytest.raises(RuntimeError, match="column-sum workspace"):
+        call("mvae_group_norm_bwd_colsum_nhwc", x.data_ptr(), dy.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+             mean.data_ptr(), rstd.data_ptr(), dx1.data_ptr(), None, None, None, nb, h * w, c, g, 1, 0.0, 0,
+             ws.data_ptr(), ws.numel(), bias.data_ptr(), 1.0, None, 0, st)
+
 def _model_grads(dev, dypack: bool, calls=None):
     import medvae_disentangled_multimodal_amd as M
     from medvae_disentangled_multimodal_amd import _lib, ops

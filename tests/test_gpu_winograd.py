@@ -849,3 +849,65 @@ def test_winograd_upsample_image_chunks(dev, monkeypatch, _wino_on):
     yr.backward(dy0.double())
     for a, r in ((y, yr), (x.grad, xr.grad), (wt.grad, wr.grad)):
         assert rel(a, r) < CONV_TOL
+
+
+def _conv_gn_bias(dev, monkeypatch, dybias, prec, ups, gn_path, x0, w0, b0, g0, be0, dy0):
+    """conv (3x3 with GroupNorm statistics, or the Upsample conv) -> GroupNorm(32)+SiLU, backward from dy0, with the
+    conv's bias gradient from the GroupNorm backward's column sums of dx (dybias) or from its own pass over dy."""
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    monkeypatch.setattr(ops, "DYBIAS", dybias)
+    seen = []
+    orig = _lib.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return orig(name, *args)
+    x = cl(x0, dev).requires_grad_(True)
+    wt = w0.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    b = b0.to(dev).requires_grad_(True)
+    gam, bet = g0.to(dev).requires_grad_(True), be0.to(dev).requires_grad_(True)
+    pv = ops.set_precision(prec)
+    orig_path = _lib.call("mvae_set_group_norm_path", gn_path)
+    monkeypatch.setattr(_lib, "call", spy)
+    try:
+        h = ops.conv2d(x, wt, b, ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, ups), gn_stats=not ups, gn_bias=ups)
+        y = ops.group_norm(h, gam, bet, 32, 1e-6, silu=True)
+        y.backward(cl(dy0, dev))
+        torch.cuda.synchronize()
+    finally:
+        monkeypatch.setattr(_lib, "call", orig)
+        _lib.call("mvae_set_group_norm_path", 0)
+        ops.restore_math_mode(pv)
+    del orig_path
+    return [t.detach().cpu() for t in (y, x.grad, wt.grad, b.grad, gam.grad, bet.grad)], seen
+
+
+@pytest.mark.parametrize("prec,ups", [("32-exact", False), ("32-exact", True), ("32", True)])
+@pytest.mark.parametrize("gn_path", [0, 1], ids=["auto", "streaming"])
+def test_conv_bias_gradient_from_groupnorm_backward(dev, monkeypatch, prec, ups, gn_path, _wino_on):
+    """A Winograd conv that reads dy in fp32 (exact fp32; the Upsample conv's Winograd form) and feeds a GroupNorm takes
+    its bias gradient from that GroupNorm's backward (mvae_group_norm_bwd_colsum_nhwc: column sums of dx, resident and
+    streaming kernels) instead of a column-sum pass over dy: every gradient equals the separate-pass path (bias: fp64
+    sums in another order, 1e-6) and float64."""
+    import torch.nn.functional as F
+    n, c, hw = 2, 64, (8 if ups else 16)
+    g = torch.Generator().manual_seed(41 + ups)
+    x0 = torch.randn(n, c, hw, hw, generator=g)
+    w0 = torch.randn(c, c, 3, 3, generator=g) / (3 * c ** 0.5)
+    b0 = torch.randn(c, generator=g) * 0.1
+    g0, be0 = torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1
+    ho = 2 * hw if ups else hw
+    dy0 = torch.randn(n, c, ho, ho, generator=g)
+    on, seen = _conv_gn_bias(dev, monkeypatch, True, prec, ups, gn_path, x0, w0, b0, g0, be0, dy0)
+    off, seen2 = _conv_gn_bias(dev, monkeypatch, False, prec, ups, gn_path, x0, w0, b0, g0, be0, dy0)
+    assert "mvae_group_norm_bwd_colsum_nhwc" in seen and "mvae_group_norm_bwd_colsum_nhwc" not in seen2
+    assert ("mvae_winograd_dy_transforms_upsample" if ups else "mvae_winograd_wgrad_gemm") in seen
+    for k, (a, b) in enumerate(zip(on, off)):
+        assert rel(a, b) < 1e-6, k
+    xr, wr, br, gr, bb = (t.double().requires_grad_() for t in (x0, w0, b0, g0, be0))
+    xi = F.interpolate(xr, scale_factor=2.0, mode="nearest") if ups else xr
+    yr = F.silu(F.group_norm(F.conv2d(xi, wr, br, padding=1), 32, gr, bb, eps=1e-6))
+    yr.backward(dy0.double())
+    tol = 5e-6 if prec == "32-exact" else CONV_TOL
+    for a, b in zip(on, (yr, xr.grad, wr.grad, br.grad, gr.grad, bb.grad)):
+        assert rel(a, b) < tol
