@@ -365,13 +365,17 @@ __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
   const __amdgpu_buffer_rsrc_t yr = make_rsrc(p.y, ybytes);
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res ? p.res : p.y, p.res ? ybytes : 0u);
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(GNB ? p.gx : p.y, GNB ? ybytes : 0u);
-  double s0[NBK], s1[NBK], g0[GNB ? NBK : 1][4], g1[GNB ? NBK : 1][4];
+  // (the GroupNorm-backward partials of one 32-pixel block are summed in fp32 -- 32 terms -- and stored as fp64: half
+  // the accumulator registers of fp64 sums, which with the full M tile in registers held this variant to one wave per
+  // SIMD)
+  double s0[NBK], s1[NBK];
+  float g0[GNB ? NBK : 1][4], g1[GNB ? NBK : 1][4];
 #pragma unroll
   for (int q = 0; q < NBK; ++q) s0[q] = s1[q] = 0.0;
 #pragma unroll
   for (int q = 0; q < (GNB ? NBK : 1); ++q)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) g0[q][u] = g1[q][u] = 0.0;
+    for (int u = 0; u < 4; ++u) g0[q][u] = g1[q][u] = 0.f;
   float ggm[4] = {0.f, 0.f, 0.f, 0.f}, gbt[4] = {0.f, 0.f, 0.f, 0.f};
   if constexpr (GNB) {
 #pragma unroll
@@ -381,6 +385,7 @@ __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
     }
   }
   const int cpg = GNB ? N / p.groups : 1;
+  const bool silu = GNB && p.silu != 0;
 #pragma unroll
   for (int tr = 0; tr < TR; ++tr)
 #pragma unroll 1
@@ -388,13 +393,13 @@ __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
       const int ti = ti0 + tr, tj = tj0 + tq;
       const long long t = ((long long)b * th + ti) * tw + tj;
       const unsigned mbase = (unsigned)(t * N4 + c4) * 16u;
+      constexpr auto at = [](int i, int k) { return wino_at<MT>(i, k); };
+      float4 r[MT][AL];
       float4 mv[AL][AL];
 #pragma unroll
       for (int i = 0; i < AL; ++i)
 #pragma unroll
         for (int j = 0; j < AL; ++j) mv[i][j] = bload4(mr, mbase + (unsigned)(i * AL + j) * mplane);
-      constexpr auto at = [](int i, int k) { return wino_at<MT>(i, k); };
-      float4 r[MT][AL];
 #pragma unroll
       for (int j = 0; j < AL; ++j) wlin<MT, AL>(&r[0][j], AL, &mv[0][j], AL, at);  // A^T M
 #pragma unroll
@@ -406,7 +411,8 @@ __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
 #pragma unroll
         for (int e = 0; e < MT; ++e) {
           const unsigned off = ((unsigned)((b * p.H + row) * p.W + tj * MT + e) * (unsigned)N + (unsigned)c4 * 4u) * 4u;
-          float4 val = f4add(f4add(o[e], bv), bload4(rr, off));
+          // (the input-gradient transform with GroupNorm partials has no bias / residual: mvae_winograd_output_gnbwd)
+          float4 val = GNB ? o[e] : f4add(f4add(o[e], bv), bload4(rr, off));
           bstore4(yr, off, val);
           if constexpr (ST) {
             s0[q] += ((double)val.x + (double)val.y) + ((double)val.z + (double)val.w);
@@ -421,13 +427,13 @@ __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
             for (int u = 0; u < 4; ++u) {
               float d = vs[u];
               const float xh = (xs[u] - mu) * rs;
-              if (p.silu) {
-                const float yn = xh * ggm[u] + gbt[u];
-                const float sg = sigmoid_f(yn);
-                d = d * sg * (1.f + yn * (1.f - sg));
-              }
+              // (branch-free: a per-element branch on the uniform silu flag held this variant to one wave per SIMD)
+              const float yn = xh * ggm[u] + gbt[u];
+              const float sg = sigmoid_f(yn);
+              const float ds = d * sg * (1.f + yn * (1.f - sg));
+              d = silu ? ds : d;
               g0[q][u] += d;
-              g1[q][u] += (double)d * xh;
+              g1[q][u] += d * xh;
             }
           }
         }
@@ -441,7 +447,7 @@ __global__ void __launch_bounds__(256) wino_out_kernel(WinoOut p) {
     if constexpr (GNB) {
       double* gp = p.gnb_part + (blk * N + c4 * 4) * 2;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) *(double2*)(gp + 2 * u) = double2{g0[q][u], g1[q][u]};
+      for (int u = 0; u < 4; ++u) *(double2*)(gp + 2 * u) = double2{(double)g0[q][u], (double)g1[q][u]};
     }
   }
 }

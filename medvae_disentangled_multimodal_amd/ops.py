@@ -373,11 +373,12 @@ WINOGRAD_DY2 = os.environ.get("MVAE_NO_WINOGRAD_DY2") is None
 # interleaved, profiles/r05_winograd_gn_ab.txt). MVAE_NO_WINOGRAD_GN=1 writes the GroupNorm output as before.
 WINOGRAD_GN = os.environ.get("MVAE_NO_WINOGRAD_GN") is None
 # ... and where that GroupNorm's backward streams (the large levels), its partial pass over x and dy can come from the
-# conv's Winograd input-gradient output transform instead (MVAE_WINOGRAD_GN_LINK=1). Measured and left
-# opt-in: the GroupNorm family gets 3.5 ms per c4 step faster (31.5 -> 28.0 ms), but the input-gradient output transform
-# that also reads x and sums the fp64 partials costs more (c4 755 -> 740 img/s, same box, interleaved,
-# profiles/r06_ab_c4_upsample_gnlink.txt)
-WINOGRAD_GN_LINK = os.environ.get("MVAE_WINOGRAD_GN_LINK") is not None
+# conv's Winograd input-gradient output transform instead: the GroupNorm family gets 3.5 ms per c4
+# step faster (31.5 -> 28.0 ms). Its first build branched on the SiLU flag per element and summed the partials in fp64,
+# one wave per SIMD: 2.1x the plain transform, c4 755 -> 740 img/s (profiles/r06_ab_c4_upsample_gnlink.txt); branch-free
+# with fp32 sums per 32-pixel block it runs at two waves per SIMD and c4 gains (752.8 -> 755.1, same box, interleaved,
+# profiles/r06_ab_c4_gnlink2.txt). MVAE_NO_WINOGRAD_GN_LINK=1: the GroupNorm backward's own partial pass.
+WINOGRAD_GN_LINK = os.environ.get("MVAE_NO_WINOGRAD_GN_LINK") is None
 GN_LAZY_ATTR = "_mvae_gn_lazy"
 G3 = ConvGeom(3, 3, 1, 1, 1, 1, 1, False)  # the GroupNorm-fed convs' geometry (ResnetBlock conv1 / conv2, conv_out)
 
