@@ -3,7 +3,10 @@
 transforms against the HBM roofline (algorithmic bytes: every operand read once, every output written once), the
 position GEMMs in executed TF/s.
 usage: tools/wino_bench.py [reps] [tile]
-env WB_SHAPES=i,j (indices into SHAPES) and WB_STAGES=gemm,wgemm restrict the run (PMC passes over one kernel)."""
+env WB_SHAPES=i,j (indices into SHAPES) and WB_STAGES=gemm,wgemm restrict the run (PMC passes over one kernel);
+WB_PREC=32-exact times the exact-fp32 arithmetic (bit-split operands, f32-input MFMA); WB_LIB=1 adds torch.bmm on the
+position GEMM's shape in the arithmetic's library dtype (fp32 for 32 / 32-exact: the hipBLASLt rate on the same batched
+short-K problem)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -13,7 +16,9 @@ dev = torch.device("cuda:0")
 REPS = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 MT = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 POS = (MT + 2) ** 2
-ops.set_precision("32")  # 3xBF16 (the Winograd path's arithmetic)
+PREC = os.environ.get("WB_PREC", "32")
+ops.set_precision(PREC)  # 3xBF16 (the Winograd path's default arithmetic) or exact fp32
+LIB = os.environ.get("WB_LIB") == "1"
 SHAPES = [(256, 8, 8, 2048, 2048), (256, 16, 16, 1024, 1024), (256, 32, 32, 512, 512), (128, 64, 64, 256, 256),
           (128, 64, 64, 512, 256),
           (256, 7, 7, 512, 512), (256, 14, 14, 256, 256), (256, 28, 28, 128, 128)]  # c2 levels (WB_SHAPES=5,6,7)
@@ -70,6 +75,10 @@ for nb, h, w, ci, co in SHAPES:
         ("wout", lambda: _lib.call("mvae_winograd_wgrad_output", mw.data_ptr(), dw.data_ptr(), 0.0, co, ci, MT, st),
          4.0 * co * ci * (POS + 9), 0),
     ]
+    if LIB:
+        va, ub = torch.randn(POS, t, ci, device=dev), torch.randn(POS, ci, co, device=dev)
+        mo = torch.empty(POS, t, co, device=dev)
+        stages.append(("lib_bmm", lambda: torch.bmm(va, ub, out=mo), 0, 2.0 * POS * t * ci * co))
     row = []
     for name, fn, nbytes, flops in stages:
         if ONLY and name not in ONLY and not (name == "in" and "wgemm" in ONLY) and not (name == "dy" and "wgemm" in ONLY):
