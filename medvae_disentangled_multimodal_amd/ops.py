@@ -536,14 +536,21 @@ class _FlatWeights:
     """The conv weights of a step prepared in one launch: fit_step converts the whole flat parameter buffer
     (optim.FlatParameters: every tensor 16-B aligned) into the forward GEMM's weight format -- split4_bf16 in the
     3xBF16 mode, packed bf16 in the bf16-mixed mode -- before the forward, and every conv forward then reads its
-    weight's slice instead of converting it (one launch per conv, ~30 per c3 step). Valid until the optimizer step."""
-    __slots__ = ("base", "end", "buf", "fmt", "fresh")
+    weight's slice instead of converting it (one launch per conv, ~30 per c3 step). Valid until the optimizer step.
+    Only the tensors a step actually reads in that format are converted once they are known: `want` records every
+    request of a step (data pointer -> elements), the next prep converts just those ranges (merged runs) and `covered`
+    holds what this step's copy contains -- a request outside it gets None (the caller converts its own weight) and is
+    covered from the next step on. c4: the Winograd convs (~90 % of the 927 M parameters) transform the fp32 weight
+    themselves, so the prep moves ~1/10 of the bytes."""
+    __slots__ = ("base", "end", "buf", "fmt", "fresh", "want", "covered")
 
     def __init__(self):
         self.base = self.end = 0
         self.buf = None
         self.fmt = 0
         self.fresh = False
+        self.want = {}
+        self.covered = None  # None: the whole buffer
 
 
 _FLATW = _FlatWeights()
@@ -655,6 +662,12 @@ def _weight_t(w, co, kh, kw, c, split, nbytes, st) -> int:
     return wt.data_ptr()
 
 
+# MVAE_NO_FLAT_PREP_WANTED=1: convert the whole flat buffer every step; MVAE_FLAT_PREP_GAP: runs closer than this many
+# elements are converted as one launch
+FLAT_PREP_WANTED = os.environ.get("MVAE_NO_FLAT_PREP_WANTED") is None
+FLAT_PREP_GAP = int(os.environ.get("MVAE_FLAT_PREP_GAP", str(1 << 20)))
+
+
 def prep_flat_weights(flat_data: torch.Tensor):
     """Convert the flat parameter buffer into the forward weight format of the current math mode (see
     _FlatWeights); a no-op in modes without a converted weight format."""
@@ -671,8 +684,27 @@ def prep_flat_weights(flat_data: torch.Tensor):
     fn = "mvae_split_bf16" if fmt == 1 else "mvae_pack_bf16"
     if ARENA.pinning is not None and not any(p is _FLATW.buf for p in ARENA.pinning):
         ARENA.pinning.append(_FLATW.buf)  # (a step graph being recorded bakes it in)
-    _lib.call(fn, flat_data.data_ptr(), _FLATW.buf.data_ptr(), n, _stream(flat_data))
-    _FLATW.base, _FLATW.end, _FLATW.fmt, _FLATW.fresh = flat_data.data_ptr(), flat_data.data_ptr() + 4 * n, fmt, True
+    base = flat_data.data_ptr()
+    same = _FLATW.base == base and _FLATW.end == base + 4 * n and _FLATW.fmt == fmt
+    want = _FLATW.want if same and FLAT_PREP_WANTED else {}
+    _FLATW.want = {}
+    if want:
+        runs = []
+        for p, numel in sorted(want.items()):
+            a = ((p - base) // 4) & ~7  # (whole 8-element groups: 16-B aligned source and packed destination)
+            e = min(n, ((p - base) // 4 + numel + 7) & ~7)
+            if runs and a - runs[-1][1] <= FLAT_PREP_GAP:
+                runs[-1][1] = max(runs[-1][1], e)
+            else:
+                runs.append([a, e])
+        eb = 4 if fmt == 1 else 2
+        for a, e in runs:
+            _lib.call(fn, base + 4 * a, _FLATW.buf.data_ptr() + eb * a, e - a, _stream(flat_data))
+        _FLATW.covered = set(want)
+    else:
+        _lib.call(fn, base, _FLATW.buf.data_ptr(), n, _stream(flat_data))
+        _FLATW.covered = None
+    _FLATW.base, _FLATW.end, _FLATW.fmt, _FLATW.fresh = base, base + 4 * n, fmt, True
 
 
 def release_weight_buffers():
@@ -681,6 +713,7 @@ def release_weight_buffers():
     parameters of c4 in the 3xBF16 mode) and forget the re-layout table. The next prepared step rebuilds them."""
     flat_weights_stale()
     _FLATW.buf, _FLATW.base, _FLATW.end = None, 0, 0
+    _FLATW.want, _FLATW.covered = {}, None
     _WT.slots, _WT.want, _WT.seen, _WT.idle = {}, {}, set(), {}
     _WT.table = _WT.buf = None
     _WT.n = _WT.blocks = 0
@@ -698,6 +731,9 @@ def _flat_weight_ptr(w: torch.Tensor, fmt: int) -> Optional[int]:
     if not (_FLATW.fresh and _FLATW.fmt == fmt and _FLATW.base <= p < _FLATW.end and
             w.is_contiguous(memory_format=CL)):
         return None
+    _FLATW.want[p] = w.numel()
+    if _FLATW.covered is not None and p not in _FLATW.covered:
+        return None  # (not in this step's copy: converted by the caller, and from the next step on by the prep)
     off = p - _FLATW.base
     return _FLATW.buf.data_ptr() + (off if fmt == 1 else off // 2)
 

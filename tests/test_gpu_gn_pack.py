@@ -251,3 +251,46 @@ def test_3xbf16_step_with_gn_split_dy_matches_register_split(dev):
     for p, off, name in zip(flat.params, flat.offsets, flat.names):
         a, b = g_on[off:off + p.numel()], g_off[off:off + p.numel()]
         assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max())), name
+
+
+def _fit_params(dev, wanted: bool, calls):
+    import medvae_disentangled_multimodal_amd as M
+    from medvae_disentangled_multimodal_amd import _lib, ops
+    kw = dict(input_channels=3, latent_dim=8, hidden_channels=64, ch_mult=(1, 2), num_res_blocks=1,
+              attn_resolutions=[16], dropout=0.0, resolution=32)
+    torch.manual_seed(0)
+    model = M.BaseVAE(**kw).to(dev)
+    mod = M.VAELightningModule(model, {"type": "adamw", "lr": 1e-3}, {"type": "none"}, {"type": "vae"},
+                               gradient_clip_val=1.0)
+    mod.configure_optimizers()
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(4, 3, 32, 32, generator=g) * 2 - 1).to(dev)
+    eps = torch.randn(4, 8, 16, 16, generator=g).to(dev)
+    saved, real_call = ops.FLAT_PREP_WANTED, _lib.call
+
+    def counting(name, *args):
+        if name == "mvae_split_bf16":
+            calls.append(args[2])
+        return real_call(name, *args)
+    ops.FLAT_PREP_WANTED, _lib.call = wanted, counting
+    ops.release_weight_buffers()
+    try:
+        for _ in range(3):
+            mod.fit_step((x, torch.zeros(4, 1, dtype=torch.long, device=dev)), 0, eps=eps)
+        torch.cuda.synchronize()
+    finally:
+        ops.FLAT_PREP_WANTED, _lib.call = saved, real_call
+        ops.release_weight_buffers()
+    return mod.flat.data.detach().cpu(), mod.flat.data.numel()
+
+
+def test_flat_weight_prep_converts_only_the_wanted_ranges(dev):
+    """From the second step on, the 3xBF16 step's weight prep splits only the flat-buffer ranges the previous step's
+    convs read in that format (_FlatWeights.want): the parameters after three AdamW steps are bitwise those of the
+    whole-buffer prep, and the later preps move fewer elements."""
+    c_on, c_off = [], []
+    p_on, n = _fit_params(dev, True, c_on)
+    p_off, _ = _fit_params(dev, False, c_off)
+    assert torch.equal(p_on, p_off)
+    assert c_off.count(n) == 3  # the whole buffer every step
+    assert c_on.count(n) == 1 and sum(c for c in c_on if c != n) < 2 * n
