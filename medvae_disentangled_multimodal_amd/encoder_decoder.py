@@ -62,9 +62,10 @@ class Conv2d(nn.Module):
             nn.init.uniform_(self.bias, -bound, bound)
 
     def forward(self, x, residual=None, geom: Optional[ConvGeom] = None, res_sink=None, x_sink=None,
-                gn_stats: bool = False, gn_bias: bool = False):
+                gn_stats: bool = False, gn_bias: bool = False, dx_sum=None):
         # gn_stats: the output feeds a Normalize; its statistics come out of the conv's epilogue
-        return ops.conv2d(x, self.weight, self.bias, geom or self.geom, residual, res_sink, x_sink, gn_stats, gn_bias)
+        return ops.conv2d(x, self.weight, self.bias, geom or self.geom, residual, res_sink, x_sink, gn_stats, gn_bias,
+                          dx_sum)
 
 
 class GroupNorm(nn.Module):
@@ -135,7 +136,8 @@ class AttnBlock(nn.Module):
     def forward(self, x):
         sink = ops.GradSink() if torch.is_grad_enabled() and x.requires_grad else None
         h = self.norm(x, grad_sink=sink)
-        o = ops.attention_core(self.q(h), self.k(h), self.v(h))
+        acc = ops.DxSum(3) if torch.is_grad_enabled() and x.requires_grad else None  # (h's gradient: one buffer)
+        o = ops.attention_core(self.q(h, dx_sum=acc), self.k(h, dx_sum=acc), self.v(h, dx_sum=acc))
         return self.proj_out(o, residual=x, res_sink=sink)
 
 

@@ -942,16 +942,21 @@ def split_dy(dy: torch.Tensor) -> Optional[torch.Tensor]:
     return ds
 
 
-def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=None, dkeep=None):
+def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=None, dkeep=None, out=None,
+                     beta: float = 0.0):
     """gn_link (GnBwdLink): the conv's input was silu?(GroupNorm(x)) -- also emit that GroupNorm's backward
     partials from the GEMM epilogue (mvae_conv2d_dgrad_gnbwd_nhwc) into gn_link.part when the launch allows it.
     dys: dy pre-split by split_dy (same values; used as the gathered GEMM operand when given).
     dyb: dy as packed bf16 (pack_dy; bf16-mixed mode).
-    dkeep (a list): on the Winograd path also keep the weight gradient's transformed dy per image chunk (_winograd)."""
+    dkeep (a list): on the Winograd path also keep the weight gradient's transformed dy per image chunk (_winograd).
+    out / beta (1x1 convs only): dx = beta * out + dy W into out (DxSum)."""
     n, c, h, wd = x_shape
     co = w.shape[0]
     _, _, ho, wo = dy.shape
-    dx = torch.empty((n, c, h, wd), device=dy.device, dtype=torch.float32, memory_format=CL)
+    if out is not None and not g.pointwise:
+        raise RuntimeError("conv2d_dgrad_raw: an accumulating output is for 1x1 convs")
+    dx = out if out is not None else torch.empty((n, c, h, wd), device=dy.device, dtype=torch.float32,
+                                                 memory_format=CL)
     st = _stream(dy)
     flops = 2.0 * n * ho * wo * co * c * g.kh * g.kw  # reference count
     shp = (n, c, h, wd, co, g.kh, g.stride, g.upsample)
@@ -1025,7 +1030,7 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
         # dx[m][c] = sum_n dy[m][n] W[n][c]  (W stored [K=cout][N=cin])
         with _timed("conv_dgrad", flops, shp):
             _lib.call("mvae_gemm_strided_batched", 0, 0, n * h * wd, c, co, 1.0, dy.data_ptr(), co, 0, w.data_ptr(), c,
-                      0, 0.0, dx.data_ptr(), c, 0, 1, None, None, 0, 0, None, 0, st)
+                      0, float(beta), dx.data_ptr(), c, 0, 1, None, None, 0, 0, None, 0, st)
         return dx
     # the dgrad GEMM's K runs over cout: transposed weights [cin][taps][cout], pre-split when cout % 4 == 0
     split = WEIGHT_SPLIT and _splits_ok() and co % 4 == 0 and _al16(dy) and g.kh * g.kw <= 32
@@ -1248,6 +1253,22 @@ def bias_grad_raw(dy2d_ptr, rows, n, out, beta, device, stream):
     _lib.call("mvae_bias_grad", dy2d_ptr, rows, n, n, out.data_ptr(), float(beta), ws.data_ptr(), ws.numel(), stream)
 
 
+class DxSum:
+    """The input gradient of several 1x1 convs that read the same tensor (AttnBlock's q, k and v of norm(x),
+    encoder_decoder.py:83-107): each conv's input-gradient GEMM accumulates into one buffer (beta = 1 after the first)
+    and only the last of them returns it, so autograd never sums the three activation-sized gradients (two adds of
+    [B, C, 16, 16] per attention block). Re-armed after the last, so a retained graph's next backward works alike; a conv
+    whose input gradient is not requested never touches it. MVAE_NO_DX_SUM=1: autograd sums them."""
+    __slots__ = ("n", "left", "buf")
+
+    def __init__(self, n: int):
+        self.n = self.left = n
+        self.buf = None
+
+
+DX_SUM = os.environ.get("MVAE_NO_DX_SUM") is None
+
+
 class GradSink:
     """Side channel for the two gradient branches of a block input x (ResnetBlock: norm1(x) and the
     residual / nin_shortcut(x), encoder_decoder.py:141-170; AttnBlock: norm(x) and the residual, :83-107).
@@ -1364,7 +1385,7 @@ def _overlap_ok(x, dy, g) -> bool:
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, geom: ConvGeom, res_sink=None, x_sink=None, gn_part=None,
-                gn_link=None, dypack=None, grad_on: bool = True):
+                gn_link=None, dypack=None, grad_on: bool = True, dx_sum=None):
         """grad_on: grad mode at the call (inside forward it is always off): no kept Winograd transform for a conv
         that will have no backward (eval / validation under torch.no_grad)."""
         _check(x, "conv input")
@@ -1395,6 +1416,7 @@ class Conv2dFn(torch.autograd.Function):
         ctx.bias_ref = bias
         ctx.res_sink, ctx.x_sink = res_sink, x_sink
         ctx.gn_link = gn_link
+        ctx.dx_sum = dx_sum
         ctx.dypack = dypack
         return y
 
@@ -1493,7 +1515,18 @@ class Conv2dFn(torch.autograd.Function):
         dkeep = [] if (WINOGRAD_DY2 and side is None and dyb is None and ctx.needs_input_grad[0] and
                        ctx.needs_input_grad[1] and WINOGRAD_WGRAD and not g.pointwise and
                        (_wino_ok(g, n_, h_, w_, c_, w.shape[0]) or _wino_ups_ok(g, n_, h_, w_, c_, w.shape[0]))) else None
-        if ctx.needs_input_grad[0]:
+        acc = ctx.dx_sum
+        if ctx.needs_input_grad[0] and acc is not None and g.pointwise and ctx.x_sink is None and _al16(dy):
+            # one of several 1x1 convs reading the same input: accumulate into the shared input gradient
+            first = acc.buf is None
+            if first:
+                acc.buf = torch.empty(tuple(x.shape), device=dy.device, dtype=torch.float32, memory_format=CL)
+            conv2d_dgrad_raw(dy, w, x.shape, g, out=acc.buf, beta=0.0 if first else 1.0)
+            acc.left -= 1
+            dx = None
+            if acc.left == 0:  # (the last of them returns the sum; re-armed for a retained graph's next backward)
+                dx, acc.buf, acc.left = acc.buf, None, acc.n
+        elif ctx.needs_input_grad[0]:
             dx = conv2d_dgrad_raw(dy, w, x.shape, g, link if ctx.x_sink is None else None, dys=dys, dyb=dyb,
                                   dkeep=dkeep)
             if ctx.x_sink is not None and ctx.x_sink.park(dx):
@@ -1519,7 +1552,7 @@ class Conv2dFn(torch.autograd.Function):
             _grad_done(ctx.weight_ref)
         if want_b and db_ret is None:
             _grad_done(ctx.bias_ref)
-        return dx, dw_ret, db_ret, dres, None, None, None, None, None, None, None
+        return dx, dw_ret, db_ret, dres, None, None, None, None, None, None, None, None
 
 
 # The GroupNorm statistics of a conv output emitted by its GEMM epilogue travel with the output tensor
@@ -1535,7 +1568,7 @@ def _conv_macs(x, weight, geom: ConvGeom) -> float:
 
 
 def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink=None, gn_stats: bool = False,
-           gn_bias: bool = False):
+           gn_bias: bool = False, dx_sum=None):
     """gn_stats=True: the output feeds a Normalize (encoder_decoder.py:28-33) -- emit its statistics from the
     conv's epilogue so the GroupNorm skips its statistics pass (plain implicit-GEMM convs only)."""
     part = None
@@ -1569,7 +1602,10 @@ def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink
         # a Winograd conv reading dy in fp32 whose output feeds a GroupNorm: the bias gradient comes out of that
         # GroupNorm's backward (column sums of its dx) instead of a separate pass over dy
         dyp = DyPack(bias, split="bias")
-    y = Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink, part, link, dyp, torch.is_grad_enabled())
+    if dx_sum is not None and not (DX_SUM and geom.pointwise and torch.is_grad_enabled()):
+        dx_sum = None
+    y = Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink, part, link, dyp, torch.is_grad_enabled(),
+                       dx_sum)
     if part is not None:
         setattr(y, GN_PART_ATTR, (part, y._version))
     if dyp is not None:

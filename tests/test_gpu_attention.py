@@ -170,3 +170,47 @@ def test_tile_attention_launch_count(dev):
     finally:
         ops.PROFILE = None
     assert len(rec) == 4
+
+
+def _attn_block_grads(dev, dx_sum: bool, prec: str, n_tok: int, retain: bool, calls):
+    from medvae_disentangled_multimodal_amd import _lib, encoder_decoder as ED, ops
+    torch.manual_seed(3)
+    blk = ED.AttnBlock(64).to(dev)
+    g = torch.Generator().manual_seed(9)
+    hw = int(n_tok ** 0.5)
+    x0 = torch.randn(2, 64, hw, hw, generator=g)
+    go = torch.randn(2, 64, hw, hw, generator=g)
+    x = x0.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    saved, real_call = ops.DX_SUM, _lib.call
+
+    def counting(name, *args):
+        calls[name] = calls.get(name, 0) + 1
+        return real_call(name, *args)
+    ops.DX_SUM, _lib.call = dx_sum, counting
+    prev = ops.set_precision(prec)
+    try:
+        y = blk(x)
+        gy = go.to(dev).contiguous(memory_format=torch.channels_last)
+        y.backward(gy, retain_graph=retain)
+        if retain:
+            y.backward(gy)  # (a retained graph's second backward: the sum re-armed)
+        torch.cuda.synchronize()
+    finally:
+        ops.DX_SUM, _lib.call = saved, real_call
+        ops.restore_math_mode(prev)
+    return [t.detach().double().cpu() for t in (x.grad, *[p.grad for p in blk.parameters()])]
+
+
+@pytest.mark.parametrize("prec", ["32", "bf16-mixed", "32-exact"])
+@pytest.mark.parametrize("n_tok,retain", [(64, False), (256, False), (256, True)])
+def test_attn_block_input_gradient_summed_in_the_dgrad_gemms(dev, prec, n_tok, retain):
+    """AttnBlock's q / k / v 1x1 convs accumulate the gradient of their shared input in one buffer (ops.DxSum: the
+    dgrad GEMMs with beta = 1 after the first) instead of autograd summing three activation-sized gradients: every
+    gradient equals the autograd-summed path within fp32 summation order (1e-6), also for a retained graph's second
+    backward, and no torch add runs over the activation."""
+    c_on, c_off = {}, {}
+    on = _attn_block_grads(dev, True, prec, n_tok, retain, c_on)
+    off = _attn_block_grads(dev, False, prec, n_tok, retain, c_off)
+    for a, b in zip(on, off):
+        assert _rel(a, b) < 1e-6
+    assert c_on.get("mvae_gemm_strided_batched", 0) == c_off.get("mvae_gemm_strided_batched", 0)
