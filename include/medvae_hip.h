@@ -369,7 +369,8 @@ int mvae_group_norm_bwd_part_nhwc(const float* x, const float* dy, const double*
                                   const float* dx_add, float* dgamma, float* dbeta, int nb, int hw, int c, int groups,
                                   int silu, void* workspace, size_t workspace_bytes, void* stream);
 /* ... with dx also written split4_bf16 and the producing conv's bias gradient (mvae_group_norm_bwd_split_nhwc's
- * outputs; the partials from the Winograd input-gradient output transform, mvae_winograd_output_gnbwd). */
+ * outputs; the partials from the Winograd input-gradient output transform, mvae_winograd_output_gnbwd). dx_split may be
+ * null when dbias is given: the bias column sums only (mvae_group_norm_bwd_colsum_nhwc's outputs, exact fp32). */
 int mvae_group_norm_bwd_part_split_nhwc(const float* x, const float* dy, const double* part, const float* gamma,
                                         const float* beta, const float* mean, const float* rstd, float* dx,
                                         const float* dx_add, float* dgamma, float* dbeta, int nb, int hw, int c,

@@ -1444,9 +1444,12 @@ int mvae_group_norm_bwd_part_split_nhwc(const float* x, const float* dy, const d
                                         int groups, int silu, void* workspace, size_t workspace_bytes, void* dx_split,
                                         float* dbias, float bias_beta, void* cs_workspace, size_t cs_workspace_bytes,
                                         void* stream) {
-  if (dx_split == nullptr || ((uintptr_t)dx_split & 15) || ((uintptr_t)dx & 15) || ((uintptr_t)x & 15) ||
-      ((uintptr_t)dy & 15) || (dx_add && ((uintptr_t)dx_add & 15)) || (dbias && cs_workspace == nullptr)) {
-    set_error("group_norm_bwd_part_split: 16-B aligned x / dy / dx / split output, a column-sum workspace");
+  // (dx_split null: the bias column sums only -- the exact-fp32 arithmetic's convs read dy in fp32)
+  if ((dx_split == nullptr && dbias == nullptr) || ((uintptr_t)dx_split & 15) || ((uintptr_t)dx & 15) ||
+      ((uintptr_t)x & 15) || ((uintptr_t)dy & 15) || (dx_add && ((uintptr_t)dx_add & 15)) ||
+      (dbias && cs_workspace == nullptr)) {
+    set_error("group_norm_bwd_part_split: 16-B aligned x / dy / dx / split output (or a bias gradient), a column-sum "
+              "workspace");
     return MVAE_EINVAL;
   }
   if (dbias && cs_workspace_bytes < mvae_group_norm_colsum_workspace_bytes(nb, hw, c)) {

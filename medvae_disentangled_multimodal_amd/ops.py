@@ -1722,8 +1722,8 @@ class GroupNormFn(torch.autograd.Function):
         gpart = ctx.link.take(dy) if ctx.link is not None and drop_p == 0.0 else None
         # algorithmic HBM bytes: read x, dy (and the residual branch's gradient when it is summed here); write dx
         req = ctx.dypack if ctx.dypack is not None and _al16(dy, dx) and (add is None or _al16(add)) else None
-        if req is not None and gpart is not None and req.split is not True:
-            req = None  # (the backward from the conv's partials writes split4 dy only)
+        if req is not None and gpart is not None and req.split is False:
+            req = None  # (the backward from the conv's partials writes split4 dy or the bias column sums only)
         bias_only = req is not None and req.split == "bias"
         if bias_only and not (req.bias_ref is not None and req.bias_ref.requires_grad):
             req = None
@@ -1751,8 +1751,8 @@ class GroupNormFn(torch.autograd.Function):
                 _lib.call("mvae_group_norm_bwd_part_split_nhwc", x.data_ptr(), dy.data_ptr(), gpart.data_ptr(),
                           gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
                           _ptr(add), _ptr(dg), _ptr(db), n, h * w, c, groups, silu, ws.data_ptr(), ws.numel(),
-                          packed.data_ptr(), _ptr(tgt), 0.0, _ptr(cs), cs.numel() if cs is not None else 0,
-                          _stream(x))
+                          None if bias_only else packed.data_ptr(), _ptr(tgt), 0.0, _ptr(cs),
+                          cs.numel() if cs is not None else 0, _stream(x))
             elif gpart is not None:  # reduction half emitted by the consuming conv's input-gradient GEMM
                 _lib.call("mvae_group_norm_bwd_part_nhwc", x.data_ptr(), dy.data_ptr(), gpart.data_ptr(),
                           gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
@@ -1826,7 +1826,7 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
             # the conv's Winograd input-gradient output transform also emits this GroupNorm's backward partials
             # (mvae_winograd_output_gnbwd: one extra read of x there) where the backward would otherwise make a partial
             # pass over x and dy (its streaming chain: the large levels, whose producing conv takes dy pre-split)
-            if (link is None and WINOGRAD_GN_LINK and x.requires_grad and dyp is not None and dyp.split is True and
+            if (link is None and WINOGRAD_GN_LINK and x.requires_grad and dyp is not None and dyp.split is not False and
                     _wino_blocks(h, w) and c % groups == 0 and (c // groups) % 4 == 0 and
                     _lib.query("mvae_group_norm_bwd_streaming", n, h * w, c, groups, 1)):
                 link = GnBwdLink(groups, silu)

@@ -706,7 +706,7 @@ def test_deferred_groupnorm_conv_at_32_channels(dev, monkeypatch, _wino_on):
         assert rel(a, b) < CONV_TOL
 
 
-def _conv_gn_conv(dev, monkeypatch, link_on, x0, wa0, ba0, g0, b0, wb0, dy0):
+def _conv_gn_conv(dev, monkeypatch, link_on, x0, wa0, ba0, g0, b0, wb0, dy0, prec="32"):
     """conv A (GroupNorm statistics from its epilogue) -> GroupNorm(32)+SiLU deferred -> conv B: the ResnetBlock's
     conv1 -> norm2 -> conv2 edge, with the GroupNorm backward's partials from conv B's Winograd input gradient (link_on)
     or from its own pass, and conv A's dy pre-split by the GroupNorm backward (DySplit) either way."""
@@ -727,6 +727,7 @@ def _conv_gn_conv(dev, monkeypatch, link_on, x0, wa0, ba0, g0, b0, wb0, dy0):
     wb = wb0.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
     geom = ops.ConvGeom(3, 3, 1, 1, 1, 1, 1, False)
     orig_path = _lib.call("mvae_set_group_norm_path", 1)  # (the streaming GroupNorm chain at this test size)
+    pv = ops.set_precision(prec)
     monkeypatch.setattr(_lib, "call", spy)
     try:
         h = ops.conv2d(x, wa, ba, geom, gn_stats=True)
@@ -737,14 +738,16 @@ def _conv_gn_conv(dev, monkeypatch, link_on, x0, wa0, ba0, g0, b0, wb0, dy0):
     finally:
         monkeypatch.setattr(_lib, "call", orig)
         _lib.call("mvae_set_group_norm_path", 0)
+        ops.restore_math_mode(pv)
     return [t.detach().cpu() for t in (y, x.grad, wa.grad, ba.grad, gam.grad, bet.grad, wb.grad)], seen
 
 
-def test_groupnorm_partials_from_winograd_input_gradient(dev, monkeypatch, _wino_on):
+@pytest.mark.parametrize("prec", ["32", "32-exact"])
+def test_groupnorm_partials_from_winograd_input_gradient(dev, monkeypatch, _wino_on, prec):
     """The deferred GroupNorm's backward takes its partials from the consuming Winograd conv's input-gradient output
     transform (mvae_winograd_output_gnbwd) and still writes the producing conv's dy pre-split with its bias gradient
-    (mvae_group_norm_bwd_part_split_nhwc): every output and gradient equals the path with the GroupNorm's own partial
-    pass (5e-6: the partials' fp64 sums in another order) and float64 (the conv bar)."""
+    (mvae_group_norm_bwd_part_split_nhwc; in exact fp32 the bias gradient alone): every output and gradient equals the
+    path with the GroupNorm's own partial pass (5e-6: the partials' sums in another order) and float64 (the conv bar)."""
     import torch.nn.functional as F
     n, c, h, w = 2, 128, 16, 16
     g = torch.Generator().manual_seed(31)
@@ -754,11 +757,12 @@ def test_groupnorm_partials_from_winograd_input_gradient(dev, monkeypatch, _wino
     g0, b0 = torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1
     wb0 = torch.randn(c, c, 3, 3, generator=g) / (3 * c ** 0.5)
     dy0 = torch.randn(n, c, h, w, generator=g)
-    linked, seen = _conv_gn_conv(dev, monkeypatch, True, x0, wa0, ba0, g0, b0, wb0, dy0)
+    linked, seen = _conv_gn_conv(dev, monkeypatch, True, x0, wa0, ba0, g0, b0, wb0, dy0, prec)
     assert "mvae_winograd_output_gnbwd" in seen and "mvae_group_norm_bwd_part_split_nhwc" in seen
-    assert "mvae_group_norm_bwd_split_nhwc" not in seen
-    plain, seen2 = _conv_gn_conv(dev, monkeypatch, False, x0, wa0, ba0, g0, b0, wb0, dy0)
-    assert "mvae_winograd_output_gnbwd" not in seen2 and "mvae_group_norm_bwd_split_nhwc" in seen2
+    own = "mvae_group_norm_bwd_colsum_nhwc" if prec == "32-exact" else "mvae_group_norm_bwd_split_nhwc"
+    assert own not in seen and "mvae_bias_grad" not in seen
+    plain, seen2 = _conv_gn_conv(dev, monkeypatch, False, x0, wa0, ba0, g0, b0, wb0, dy0, prec)
+    assert "mvae_winograd_output_gnbwd" not in seen2 and own in seen2
     for a, b in zip(linked, plain):
         assert rel(a, b) < 5e-6
     xr, war, bar_, gr, br, wbr = (t.double().requires_grad_() for t in (x0, wa0, ba0, g0, b0, wb0))
