@@ -325,7 +325,8 @@ size_t mvae_group_norm_workspace_bytes(int nb, int hw, int c);
  * + sum over rows of dx (fp64 partials in cs_workspace, fixed order): the output gradient and bias gradient of the
  * convolution whose output this GroupNorm normalizes (ResnetBlock conv1 -> norm2, the next block's norm1), in the
  * same pass as dx -- replaces mvae_pack_bf16_colsum over dx (the conv bias half of convolution_backward,
- * encoder_decoder.py:141-163). x, dy, dx, dx_add 16-B aligned. */
+ * encoder_decoder.py:141-163). x, dy, dx, dx_add 16-B aligned. dx may be null (this form, the split form and the
+ * partials form): the fp32 dx is not written when the producing conv -- its only consumer -- reads the copy alone. */
 int mvae_group_norm_bwd_pack_nhwc(const float* x, const float* dy, const float* gamma, const float* beta,
                                   const float* mean, const float* rstd, float* dx, const float* dx_add, float* dgamma,
                                   float* dbeta, int nb, int hw, int c, int groups, int silu, float drop_p,

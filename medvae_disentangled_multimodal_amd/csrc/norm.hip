@@ -437,7 +437,8 @@ __global__ void __launch_bounds__(256) gn_dx_kernel(GnArgs a, const float* __res
           if (ap != nullptr) {  // the other branch's gradient of x (ResnetBlock / AttnBlock residual): summed here
             o[0] += av[u].x; o[1] += av[u].y; o[2] += av[u].z; o[3] += av[u].w;
           }
-          *(float4*)(op + (long long)r * a.C) = float4{o[0], o[1], o[2], o[3]};
+          // (dx null: the producing conv, dx's only consumer, reads the split / packed copy alone -- uniform)
+          if (dx != nullptr) *(float4*)(op + (long long)r * a.C) = float4{o[0], o[1], o[2], o[3]};
           if (a.dxp != nullptr) {
             if (a.dxp_split)
               ((uint4*)a.dxp)[off >> 2] = split4_bf16(float4{o[0], o[1], o[2], o[3]});
@@ -794,7 +795,8 @@ __device__ __forceinline__ void gn_bwd_unit(const GnArgs& a, int SC, int u, cons
     q2[e] = sm.gk2[c4 * 4 + e];
     q3[e] = sm.gk3[c4 * 4 + e];
   }
-  const __amdgpu_buffer_rsrc_t dr = un.rsrc(dx);
+  // (dx null: an empty range, the fp32 stores are dropped -- the conv reads the split / packed copy alone)
+  const __amdgpu_buffer_rsrc_t dr = dx ? un.rsrc(dx) : __builtin_amdgcn_make_buffer_rsrc(nullptr, (short)0, 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t pr = a.dxp_split  // split4: fp32 offsets; packed bf16: half of them
       ? __builtin_amdgcn_make_buffer_rsrc((void*)((float*)a.dxp + un.ubase), (short)0, (int)un.bytes, 0x00020000)
       : __builtin_amdgcn_make_buffer_rsrc((void*)((__bf16*)a.dxp + un.ubase), (short)0, (int)(un.bytes >> 1), 0x00020000);
@@ -1344,6 +1346,10 @@ static int gn_bwd(const float* x, const float* dy, const float* gamma, const flo
     set_error("group_norm_bwd: bad geometry");
     return MVAE_EINVAL;
   }
+  if (dx == nullptr && dxp == nullptr) {
+    set_error("group_norm_bwd: dx may be null only when the split / packed copy is written");
+    return MVAE_EINVAL;
+  }
   if (workspace_bytes < mvae_group_norm_workspace_bytes(nb, hw, c)) {
     set_error("group_norm_bwd: workspace too small");
     return MVAE_EWORKSPACE;
@@ -1483,6 +1489,10 @@ static int gn_bwd_part(const float* x, const float* dy, const double* part, cons
                        void* stream) {
   if (nb <= 0 || hw <= 0 || c <= 0 || (c & 3) || groups <= 0 || c % groups || hw % 32 || part == nullptr) {
     set_error("group_norm_bwd_part: needs hw %% 32 == 0 and C %% 4 == 0");
+    return MVAE_EINVAL;
+  }
+  if (dx == nullptr && dx_split == nullptr) {
+    set_error("group_norm_bwd_part: dx may be null only when the split copy is written");
     return MVAE_EINVAL;
   }
   if (workspace_bytes < mvae_group_norm_workspace_bytes(nb, hw, c)) {

@@ -77,10 +77,11 @@ class GroupNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(num_channels))
         self.bias = nn.Parameter(torch.zeros(num_channels))
 
-    def forward(self, x, silu: bool = False, drop_p: float = 0.0, for_conv: bool = False, grad_sink=None):
+    def forward(self, x, silu: bool = False, drop_p: float = 0.0, for_conv: bool = False, grad_sink=None,
+                conv_dy_only: bool = False):
         seed = _next_seed() if drop_p > 0.0 else 0
         return ops.group_norm(x, self.weight, self.bias, self.num_groups, self.eps, silu, drop_p, seed, for_conv,
-                              grad_sink)
+                              grad_sink, conv_dy_only)
 
 
 def Normalize(in_channels: int, num_groups: int = 32) -> GroupNorm:
@@ -116,7 +117,8 @@ class ResnetBlock(nn.Module):
         # for_conv = the consuming conv's output channels (bf16-mixed: packed bf16 GroupNorm outputs, ops.group_norm)
         h = self.conv1(self.norm1(x, silu=True, for_conv=self.out_channels, grad_sink=sink), gn_stats=True)
         p = self.dropout.p if self.training else 0.0
-        h = self.norm2(h, silu=True, drop_p=p, for_conv=self.out_channels)
+        # (conv1's output has no other consumer: its gradient is norm2's dx alone -- conv_dy_only)
+        h = self.norm2(h, silu=True, drop_p=p, for_conv=self.out_channels, conv_dy_only=True)
         if self.in_channels != self.out_channels:
             sc = self.conv_shortcut if self.use_conv_shortcut else self.nin_shortcut
             return self.conv2(h, residual=sc(x, x_sink=sink), gn_stats=True)

@@ -1317,7 +1317,7 @@ DYSPLIT_MIN_MACS = 1e11
 
 
 class DyPack:
-    __slots__ = ("bias_ref", "packed", "dx_ref", "dx_version", "dx_shape", "bias_done", "db", "split")
+    __slots__ = ("bias_ref", "packed", "dx_ref", "dx_version", "dx_shape", "bias_done", "db", "split", "nodx")
 
     def __init__(self, bias_ref, split: bool = False):
         self.bias_ref = bias_ref
@@ -1326,6 +1326,7 @@ class DyPack:
         self.split = split
         self.packed = self.dx_ref = self.dx_version = self.dx_shape = self.db = None
         self.bias_done = False
+        self.nodx = False  # the GroupNorm wrote only the copy (its dx has this conv as its only consumer)
 
     def take(self, dy):
         """(packed dy, bias gradient done, returned bias gradient) when the GroupNorm backward produced them from
@@ -1333,13 +1334,16 @@ class DyPack:
         tracked by a weak reference, not its address: once autograd has summed another branch into a new tensor and
         freed dx, that address can come back from the allocator for an unrelated dy (a layout copy of the sum) --
         a stale address match the weak reference rules out."""
-        packed, ref, ver, shp = self.packed, self.dx_ref, self.dx_version, self.dx_shape
+        packed, ref, ver, shp, nodx = self.packed, self.dx_ref, self.dx_version, self.dx_shape, self.nodx
         out = (packed, self.bias_done, self.db)
         self.packed = self.dx_ref = self.dx_version = self.dx_shape = self.db = None
-        self.bias_done = False
+        self.bias_done = self.nodx = False
         dx = ref() if ref is not None else None
         if packed is None or dx is None or dy.data_ptr() != dx.data_ptr() or dy._version != ver or \
                 tuple(dy.shape) != shp or not dy.is_contiguous(memory_format=CL):
+            if nodx:
+                raise RuntimeError("conv2d backward: the GroupNorm wrote only the copy of its dx for this conv (its only "
+                                   "consumer), but the conv's output gradient is another tensor")
             return None
         return out
 
@@ -1657,7 +1661,8 @@ class GnBwdLink:
 class GroupNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool, drop_p: float, seed: int,
-                y_split: bool = False, grad_sink=None, part=None, link=None, dypack=None, lazy=None):
+                y_split: bool = False, grad_sink=None, part=None, link=None, dypack=None, lazy=None,
+                conv_dy_only: bool = False):
         _check(x, "group_norm input")
         x = nhwc(x)
         n, c, h, w = x.shape
@@ -1694,6 +1699,7 @@ class GroupNormFn(torch.autograd.Function):
         ctx.grad_sink = grad_sink
         ctx.link = link
         ctx.dypack = dypack
+        ctx.conv_dy_only = conv_dy_only
         if link is not None:
             link.x, link.gamma, link.beta, link.mean, link.rstd = x, gamma, beta, mean, rstd
         return y
@@ -1746,10 +1752,16 @@ class GroupNormFn(torch.autograd.Function):
                 tgt = req.db = torch.empty(c, device=x.device, dtype=torch.float32)
             csb = _lib.query("mvae_group_norm_colsum_workspace_bytes", n, h * w, c)
             cs = ARENA.get("gncs", csb, x.device) if tgt is not None else None
+        # x is the output of the conv that requested the copy and has no other consumer: that conv reads the copy alone,
+        # so the fp32 dx is left unwritten (its buffer is still autograd's gradient object)
+        nodx = bool(ctx.conv_dy_only and DX_COPY_ONLY and req is not None and not bias_only)
+        dxp = None if nodx else dx.data_ptr()
+        if nodx and DX_POISON:
+            dx.fill_(float("nan"))  # (test aid: any kernel that still reads the unwritten dx turns the step NaN)
         with _timed("gn_bwd", (12.0 + (4.0 if add is not None else 0.0)) * x.numel(), (n, c, h * w)):
             if gpart is not None and req is not None:  # reduction half from the conv + the conv's split dy / bias
                 _lib.call("mvae_group_norm_bwd_part_split_nhwc", x.data_ptr(), dy.data_ptr(), gpart.data_ptr(),
-                          gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                          gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dxp,
                           _ptr(add), _ptr(dg), _ptr(db), n, h * w, c, groups, silu, ws.data_ptr(), ws.numel(),
                           None if bias_only else packed.data_ptr(), _ptr(tgt), 0.0, _ptr(cs),
                           cs.numel() if cs is not None else 0, _stream(x))
@@ -1766,7 +1778,7 @@ class GroupNormFn(torch.autograd.Function):
             elif req is not None:
                 _lib.call("mvae_group_norm_bwd_split_nhwc" if req.split else "mvae_group_norm_bwd_pack_nhwc",
                           x.data_ptr(), dy.data_ptr(), gamma.data_ptr(),
-                          beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), _ptr(add), _ptr(dg),
+                          beta.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dxp, _ptr(add), _ptr(dg),
                           _ptr(db), n, h * w, c, groups, silu, drop_p, seed, ws.data_ptr(), ws.numel(),
                           packed.data_ptr(), _ptr(tgt), 0.0, _ptr(cs), cs.numel() if cs is not None else 0,
                           _stream(x))
@@ -1778,11 +1790,12 @@ class GroupNormFn(torch.autograd.Function):
             req.packed, req.dx_ref, req.dx_version, req.dx_shape = packed, weakref.ref(dx), dx._version, \
                 tuple(dx.shape)
             req.bias_done = tgt is not None
+            req.nodx = nodx
         if ctx.needs_input_grad[1] and dg_ret is None:
             _grad_done(ctx.gamma_ref)
         if ctx.needs_input_grad[2] and db_ret is None:
             _grad_done(ctx.beta_ref)
-        return dx, dg_ret, db_ret, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dg_ret, db_ret, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 # Activations handed to a convolution in the pre-split 3xBF16 operand layout carry this attribute
@@ -1795,7 +1808,15 @@ ACT_SPLIT = os.environ.get("MVAE_NO_ACT_SPLIT") is None
 BF16_ATTR = "_mvae_bf16"
 
 
-def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0, for_conv=False, grad_sink=None):
+# A GroupNorm whose input is a conv output with no other consumer (ResnetBlock norm2 of conv1's output, conv_dy_only):
+# when that conv takes its output gradient as the split / packed copy the backward writes, the fp32 dx is not written.
+# MVAE_NO_DX_COPY_ONLY=1: always written.
+DX_COPY_ONLY = os.environ.get("MVAE_NO_DX_COPY_ONLY") is None
+DX_POISON = os.environ.get("MVAE_DX_POISON") == "1"  # tests: fill the unwritten dx with NaN
+
+
+def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0, for_conv=False, grad_sink=None,
+               conv_dy_only: bool = False):
     """for_conv (True, or the consuming conv's output channel count): the caller feeds the result straight into
     ops.conv2d (3x3/stride-1, C % 4 == 0) -- the output is then written pre-split for the GEMM (GroupNorm -> conv is
     the ResnetBlock / norm_out pattern, encoder_decoder.py:141-163, :318-328); in the bf16-mixed mode, with a known
@@ -1830,7 +1851,8 @@ def group_norm(x, gamma, beta, groups, eps=1e-6, silu=False, drop_p=0.0, seed=0,
                     _wino_blocks(h, w) and c % groups == 0 and (c // groups) % 4 == 0 and
                     _lib.query("mvae_group_norm_bwd_streaming", n, h * w, c, groups, 1)):
                 link = GnBwdLink(groups, silu)
-    y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink, part, link, dyp, lazy)
+    y = GroupNormFn.apply(x, gamma, beta, groups, eps, silu, drop_p, seed, split, grad_sink, part, link, dyp, lazy,
+                          conv_dy_only)
     if lazy is not None:
         y = y.as_subclass(DeferredGnOutput)  # (same autograd node; any read of its values raises)
         setattr(y, GN_LAZY_ATTR, lazy)

@@ -294,3 +294,60 @@ def test_flat_weight_prep_converts_only_the_wanted_ranges(dev):
     assert torch.equal(p_on, p_off)
     assert c_off.count(n) == 3  # the whole buffer every step
     assert c_on.count(n) == 1 and sum(c for c in c_on if c != n) < 2 * n
+
+
+@pytest.mark.parametrize("prec", ["32", "bf16-mixed"])
+@pytest.mark.parametrize("wino", [False, True])
+def test_groupnorm_leaves_dx_unwritten_for_its_only_consumer(dev, prec, wino, monkeypatch):
+    """ResnetBlock's norm2 (conv1's output has no other consumer) writes only conv1's split / packed copy of its dx:
+    with the unwritten dx poisoned to NaN, a training step of a model whose ResnetBlocks run every conv1 path (implicit
+    GEMM, LDS-DMA bf16, Winograd) gives finite gradients equal to the step that writes dx (bitwise: the conv reads the
+    same copy either way)."""
+    import medvae_disentangled_multimodal_amd as M
+    from medvae_disentangled_multimodal_amd import ops
+    if wino:
+        for k, v in (("WINOGRAD_MIN_C", 1), ("WINOGRAD_MIN_C_WIDE", 1), ("WINOGRAD_MIN_MACS", 0.0),
+                     ("WINOGRAD_MAX_W", 64), ("WINOGRAD_BF16_MAX_W", 64)):
+            monkeypatch.setattr(ops, k, v)
+    else:
+        monkeypatch.setattr(ops, "WINOGRAD", False)
+    monkeypatch.setattr(ops, "DYSPLIT_MIN_MACS", 0.0)
+    kw = dict(input_channels=3, latent_dim=8, hidden_channels=64, ch_mult=(1, 2), num_res_blocks=1,
+              attn_resolutions=[], dropout=0.0, resolution=32)
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(4, 3, 32, 32, generator=g) * 2 - 1).to(dev)
+    eps = torch.randn(4, 8, 16, 16, generator=g).to(dev)
+    from medvae_disentangled_multimodal_amd import _lib
+    grads, skipped = [], []
+    real_call = _lib.call
+
+    def spy(name, *args):
+        if name in ("mvae_group_norm_bwd_split_nhwc", "mvae_group_norm_bwd_pack_nhwc") and args[6] is None:
+            skipped.append(name)
+        if name == "mvae_group_norm_bwd_part_split_nhwc" and args[7] is None:
+            skipped.append(name)
+        return real_call(name, *args)
+    monkeypatch.setattr(_lib, "call", spy)
+    for copy_only in (True, False):
+        monkeypatch.setattr(ops, "DX_COPY_ONLY", copy_only)
+        monkeypatch.setattr(ops, "DX_POISON", copy_only)
+        torch.manual_seed(0)
+        model = M.BaseVAE(**kw).to(dev)
+        mod = M.VAELightningModule(model, {"type": "adam", "lr": 1e-4}, {"type": "none"}, {"type": "vae"},
+                                   gradient_clip_val=None, precision=prec)
+        mod.configure_optimizers()
+        prev = ops.set_precision(prec)
+        try:
+            mod.optimizer.zero_grad()
+            ops.prep_flat_weights(mod.flat.data)
+            loss = mod.training_step((x, torch.zeros(4, 1, dtype=torch.long, device=dev)), 0, eps=eps)
+            loss.backward()
+            ops.flat_weights_stale()
+            torch.cuda.synchronize()
+        finally:
+            ops.restore_math_mode(prev)
+        grads.append(mod.flat.grad.detach().double().cpu())
+    assert len(skipped) >= 2  # (every ResnetBlock's norm2 left dx unwritten)
+    assert torch.isfinite(grads[0]).all()
+    rel = float((grads[0] - grads[1]).norm() / grads[1].norm())
+    assert rel < 1e-6, rel
