@@ -1317,7 +1317,8 @@ DYSPLIT_MIN_MACS = 1e11
 
 
 class DyPack:
-    __slots__ = ("bias_ref", "packed", "dx_ref", "dx_version", "dx_shape", "bias_done", "db", "split", "nodx")
+    __slots__ = ("bias_ref", "packed", "dx_ref", "dx_version", "dx_shape", "bias_done", "db", "split", "nodx",
+                 "copy_ok")
 
     def __init__(self, bias_ref, split: bool = False):
         self.bias_ref = bias_ref
@@ -1327,6 +1328,7 @@ class DyPack:
         self.packed = self.dx_ref = self.dx_version = self.dx_shape = self.db = None
         self.bias_done = False
         self.nodx = False  # the GroupNorm wrote only the copy (its dx has this conv as its only consumer)
+        self.copy_ok = False  # (set by conv2d: every backward path of this conv reads the copy, never the fp32 dy)
 
     def take(self, dy):
         """(packed dy, bias gradient done, returned bias gradient) when the GroupNorm backward produced them from
@@ -1594,10 +1596,14 @@ def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink
     if gn_stats and DYPACK and _dma_fmt() == 2 and not wino_bf16 and not geom.pointwise and weight.shape[0] % 8 == 0 and \
             geom.kh * geom.kw <= 32 and torch.is_grad_enabled():
         dyp = DyPack(bias)
+        # (the LDS-DMA input / weight gradients read the packed copy; GroupNorm-partials epilogues and odd channel
+        # counts fall back to kernels that read the fp32 dy)
+        dyp.copy_ok = not GN_BWD_FUSED and x.shape[1] % 8 == 0 and not geom.upsample
     elif gn_stats and DYSPLIT and ((_dma_fmt() == 0 and _MATH[0] == 0) or wino_bf16) and not geom.pointwise and \
             not _subpixel_upsample(geom) and weight.shape[0] % 4 == 0 and geom.kh * geom.kw <= 32 and \
             torch.is_grad_enabled() and _conv_macs(x, weight, geom) >= DYSPLIT_MIN_MACS:
         dyp = DyPack(bias, split=True)
+        dyp.copy_ok = not GN_BWD_FUSED  # (the 3xBF16 GEMMs and Winograd transforms read the split copy)
     elif (gn_stats or gn_bias) and DYBIAS and bias is not None and bias.requires_grad and torch.is_grad_enabled() and \
             x.dim() == 4 and weight.shape[0] % 4 == 0 and (
                 (_MATH[0] == 2 and not _subpixel_upsample(geom) and
@@ -1754,7 +1760,7 @@ class GroupNormFn(torch.autograd.Function):
             cs = ARENA.get("gncs", csb, x.device) if tgt is not None else None
         # x is the output of the conv that requested the copy and has no other consumer: that conv reads the copy alone,
         # so the fp32 dx is left unwritten (its buffer is still autograd's gradient object)
-        nodx = bool(ctx.conv_dy_only and DX_COPY_ONLY and req is not None and not bias_only)
+        nodx = bool(ctx.conv_dy_only and DX_COPY_ONLY and req is not None and not bias_only and req.copy_ok)
         dxp = None if nodx else dx.data_ptr()
         if nodx and DX_POISON:
             dx.fill_(float("nan"))  # (test aid: any kernel that still reads the unwritten dx turns the step NaN)
