@@ -1310,6 +1310,10 @@ DYSPLIT = os.environ.get("MVAE_NO_DYSPLIT") is None
 # ... and, for a Winograd conv that reads dy in fp32, the bias gradient alone (mvae_group_norm_bwd_colsum_nhwc).
 # MVAE_NO_DYBIAS=1: a separate column-sum pass over dy.
 DYBIAS = os.environ.get("MVAE_NO_DYBIAS") is None
+# The Winograd convs of the 3xBF16 and bf16 arithmetics take dy in fp32 too (their dy transform splits / rounds it in
+# registers) and get only the bias gradient from the GroupNorm backward: one 4-B write per element fewer wherever that
+# GroupNorm also writes dx (the next block's norm1). MVAE_WINOGRAD_DY_SPLIT=1: the split copy as before.
+WINOGRAD_DY_FP32 = os.environ.get("MVAE_WINOGRAD_DY_SPLIT") is None
 # only for convs of at least this many MACs (the c4 levels): measured same box, interleaved (profiles/r05_dysplit_ab.txt),
 # c4 +0.9 % (dgrad 442 -> 459, wgrad 414 -> 426 TF/s against +4.3 ms of GroupNorm backward for the extra 4 B per
 # element), while c2 (-0.6 %) and c3 (-3.6 %) lose: their GEMMs gain less than the wider GroupNorm pass costs
@@ -1591,23 +1595,26 @@ def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink
     dyp = None
     # (a Winograd conv of the bf16-mixed mode reads dy in fp32 or 3xBF16-split form, not packed: the GroupNorm backward
     # writes it split, as in the 3xBF16 mode)
-    wino_bf16 = _MATH[0] == 1 and x.dim() == 4 and _wino_ok(geom, x.shape[0], x.shape[2], x.shape[3], x.shape[1],
-                                                             weight.shape[0])
+    wino_any = x.dim() == 4 and _wino_ok(geom, x.shape[0], x.shape[2], x.shape[3], x.shape[1], weight.shape[0])
+    wino_bf16 = _MATH[0] == 1 and wino_any
+    # (a Winograd conv splits / rounds dy in its own memory-bound transform: the GroupNorm backward then writes no
+    # second copy of dx, only the bias gradient)
+    wino_fp32_dy = WINOGRAD_DY_FP32 and wino_any and not _subpixel_upsample(geom)
     if gn_stats and DYPACK and _dma_fmt() == 2 and not wino_bf16 and not geom.pointwise and weight.shape[0] % 8 == 0 and \
             geom.kh * geom.kw <= 32 and torch.is_grad_enabled():
         dyp = DyPack(bias)
         # (the LDS-DMA input / weight gradients read the packed copy; GroupNorm-partials epilogues and odd channel
         # counts fall back to kernels that read the fp32 dy)
         dyp.copy_ok = not GN_BWD_FUSED and x.shape[1] % 8 == 0 and not geom.upsample
-    elif gn_stats and DYSPLIT and ((_dma_fmt() == 0 and _MATH[0] == 0) or wino_bf16) and not geom.pointwise and \
+    elif gn_stats and DYSPLIT and ((_dma_fmt() == 0 and _MATH[0] == 0) or wino_bf16) and not wino_fp32_dy and \
+            not geom.pointwise and \
             not _subpixel_upsample(geom) and weight.shape[0] % 4 == 0 and geom.kh * geom.kw <= 32 and \
             torch.is_grad_enabled() and _conv_macs(x, weight, geom) >= DYSPLIT_MIN_MACS:
         dyp = DyPack(bias, split=True)
         dyp.copy_ok = not GN_BWD_FUSED  # (the 3xBF16 GEMMs and Winograd transforms read the split copy)
     elif (gn_stats or gn_bias) and DYBIAS and bias is not None and bias.requires_grad and torch.is_grad_enabled() and \
             x.dim() == 4 and weight.shape[0] % 4 == 0 and (
-                (_MATH[0] == 2 and not _subpixel_upsample(geom) and
-                 _wino_ok(geom, x.shape[0], x.shape[2], x.shape[3], x.shape[1], weight.shape[0])) or
+                (_MATH[0] == 2 and not _subpixel_upsample(geom) and wino_any) or wino_fp32_dy or
                 _wino_ups_ok(geom, x.shape[0], x.shape[2], x.shape[3], x.shape[1], weight.shape[0])):
         # a Winograd conv reading dy in fp32 whose output feeds a GroupNorm: the bias gradient comes out of that
         # GroupNorm's backward (column sums of its dx) instead of a separate pass over dy

@@ -307,8 +307,8 @@ def test_groupnorm_leaves_dx_unwritten_for_its_only_consumer(dev, prec, wino, mo
     from medvae_disentangled_multimodal_amd import ops
     if wino:
         for k, v in (("WINOGRAD_MIN_C", 1), ("WINOGRAD_MIN_C_WIDE", 1), ("WINOGRAD_MIN_MACS", 0.0),
-                     ("WINOGRAD_MAX_W", 64), ("WINOGRAD_BF16_MAX_W", 64)):
-            monkeypatch.setattr(ops, k, v)
+                     ("WINOGRAD_MAX_W", 64), ("WINOGRAD_BF16_MAX_W", 64), ("WINOGRAD_DY_FP32", False)):
+            monkeypatch.setattr(ops, k, v)  # (the split-copy form of the Winograd convs: MVAE_WINOGRAD_DY_SPLIT=1)
     else:
         monkeypatch.setattr(ops, "WINOGRAD", False)
     monkeypatch.setattr(ops, "DYSPLIT_MIN_MACS", 0.0)

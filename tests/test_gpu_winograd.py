@@ -742,11 +742,12 @@ def _conv_gn_conv(dev, monkeypatch, link_on, x0, wa0, ba0, g0, b0, wb0, dy0, pre
     return [t.detach().cpu() for t in (y, x.grad, wa.grad, ba.grad, gam.grad, bet.grad, wb.grad)], seen
 
 
-@pytest.mark.parametrize("prec", ["32", "32-exact"])
-def test_groupnorm_partials_from_winograd_input_gradient(dev, monkeypatch, _wino_on, prec):
+@pytest.mark.parametrize("prec,dy_split", [("32", False), ("32", True), ("32-exact", False)])
+def test_groupnorm_partials_from_winograd_input_gradient(dev, monkeypatch, _wino_on, prec, dy_split):
     """The deferred GroupNorm's backward takes its partials from the consuming Winograd conv's input-gradient output
     transform (mvae_winograd_output_gnbwd) and still writes the producing conv's dy pre-split with its bias gradient
-    (mvae_group_norm_bwd_part_split_nhwc; in exact fp32 the bias gradient alone): every output and gradient equals the
+    (mvae_group_norm_bwd_part_split_nhwc; for a Winograd producer, which splits dy itself, the bias gradient alone;
+    the split copy with MVAE_WINOGRAD_DY_SPLIT=1): every output and gradient equals the
     path with the GroupNorm's own partial pass (5e-6: the partials' sums in another order) and float64 (the conv bar)."""
     import torch.nn.functional as F
     n, c, h, w = 2, 128, 16, 16
@@ -757,9 +758,12 @@ def test_groupnorm_partials_from_winograd_input_gradient(dev, monkeypatch, _wino
     g0, b0 = torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1
     wb0 = torch.randn(c, c, 3, 3, generator=g) / (3 * c ** 0.5)
     dy0 = torch.randn(n, c, h, w, generator=g)
+    from medvae_disentangled_multimodal_amd import ops
+    monkeypatch.setattr(ops, "WINOGRAD_DY_FP32", not dy_split)
     linked, seen = _conv_gn_conv(dev, monkeypatch, True, x0, wa0, ba0, g0, b0, wb0, dy0, prec)
     assert "mvae_winograd_output_gnbwd" in seen and "mvae_group_norm_bwd_part_split_nhwc" in seen
-    own = "mvae_group_norm_bwd_colsum_nhwc" if prec == "32-exact" else "mvae_group_norm_bwd_split_nhwc"
+    # (a Winograd conv takes dy in fp32: the bias gradient alone; opt-in: the split copy)
+    own = "mvae_group_norm_bwd_split_nhwc" if dy_split else "mvae_group_norm_bwd_colsum_nhwc"
     assert own not in seen and "mvae_bias_grad" not in seen
     plain, seen2 = _conv_gn_conv(dev, monkeypatch, False, x0, wa0, ba0, g0, b0, wb0, dy0, prec)
     assert "mvae_winograd_output_gnbwd" not in seen2 and own in seen2
