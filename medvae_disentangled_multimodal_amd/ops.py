@@ -1526,8 +1526,11 @@ class Conv2dFn(torch.autograd.Function):
                        ctx.needs_input_grad[1] and WINOGRAD_WGRAD and not g.pointwise and
                        (_wino_ok(g, n_, h_, w_, c_, w.shape[0]) or _wino_ups_ok(g, n_, h_, w_, c_, w.shape[0]))) else None
         acc = ctx.dx_sum
-        if ctx.needs_input_grad[0] and acc is not None and g.pointwise and ctx.x_sink is None and _al16(dy):
-            # one of several 1x1 convs reading the same input: accumulate into the shared input gradient
+        if ctx.needs_input_grad[0] and acc is not None:
+            # one of several 1x1 convs reading the same input: accumulate into the shared input gradient (every one of
+            # them must take this branch, or the sum would never be returned)
+            if not _al16(dy):
+                dy = dy.clone(memory_format=CL)
             first = acc.buf is None
             if first:
                 acc.buf = torch.empty(tuple(x.shape), device=dy.device, dtype=torch.float32, memory_format=CL)
@@ -1619,7 +1622,7 @@ def conv2d(x, weight, bias, geom: ConvGeom, residual=None, res_sink=None, x_sink
         # a Winograd conv reading dy in fp32 whose output feeds a GroupNorm: the bias gradient comes out of that
         # GroupNorm's backward (column sums of its dx) instead of a separate pass over dy
         dyp = DyPack(bias, split="bias")
-    if dx_sum is not None and not (DX_SUM and geom.pointwise and torch.is_grad_enabled()):
+    if dx_sum is not None and not (DX_SUM and geom.pointwise and torch.is_grad_enabled() and x_sink is None):
         dx_sum = None
     y = Conv2dFn.apply(x, weight, bias, residual, geom, res_sink, x_sink, part, link, dyp, torch.is_grad_enabled(),
                        dx_sum)
