@@ -943,13 +943,14 @@ def split_dy(dy: torch.Tensor) -> Optional[torch.Tensor]:
 
 
 def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=None, dkeep=None, out=None,
-                     beta: float = 0.0):
+                     beta: float = 0.0, u_pre=None):
     """gn_link (GnBwdLink): the conv's input was silu?(GroupNorm(x)) -- also emit that GroupNorm's backward
     partials from the GEMM epilogue (mvae_conv2d_dgrad_gnbwd_nhwc) into gn_link.part when the launch allows it.
     dys: dy pre-split by split_dy (same values; used as the gathered GEMM operand when given).
     dyb: dy as packed bf16 (pack_dy; bf16-mixed mode).
     dkeep (a list): on the Winograd path also keep the weight gradient's transformed dy per image chunk (_winograd).
-    out / beta (1x1 convs only): dx = beta * out + dy W into out (DxSum)."""
+    out / beta (1x1 convs only): dx = beta * out + dy W into out (DxSum).
+    u_pre ((U', event)): the Winograd filter transform computed during the forward on a side stream (_upre_launch)."""
     n, c, h, wd = x_shape
     co = w.shape[0]
     _, _, ho, wo = dy.shape
@@ -997,6 +998,9 @@ def conv2d_dgrad_raw(dy, w, x_shape, g: ConvGeom, gn_link=None, dys=None, dyb=No
         part = torch.empty(n * h * wd // 32 * c * 2, device=dy.device, dtype=torch.float64) if link else None
         with _timed("conv_dgrad", _wino_alg(flops), shp, flops):
             u = None
+            if u_pre is not None:  # (made during the forward on the side stream: joined here)
+                torch.cuda.current_stream(dy.device).wait_event(u_pre[1])
+                u = u_pre[0]
             for b0, b1 in _wino_chunks(n, h, wd, max(c, co)):
                 nb = b1 - b0
                 m, u = _winograd(dya[b0:b1], w, nb, h, wd, co, c, dys is not None, True, st, u=u, key=dya,
@@ -1378,6 +1382,36 @@ def _bwd_side(t: torch.Tensor):
     return side
 
 
+# The Winograd input gradient's filter transform U' (the flipped, transposed filters in the transform domain) depends on
+# the weights alone: it is computed during the forward, on a side stream concurrent with the forward's compute-bound
+# position GEMMs, instead of on the backward's critical path (c4: 31 launches, 4.1 ms per step). The buffers live from
+# the forward to the backward (c4: ~10 GB). Off under graph capture and the bench's instrumented step. Measured neutral
+# (c4 769.1 vs 768.0, c5 976.9 vs 977.0 img/s, same box, interleaved, profiles/r06_ab_winograd_upre.txt: the side-stream
+# transform slows the concurrent GEMMs by about what it hides), so opt-in: MVAE_WINOGRAD_UPRE=1.
+WINOGRAD_UPRE = os.environ.get("MVAE_WINOGRAD_UPRE") is not None
+_UPRE = {}
+
+
+def _upre_launch(w: torch.Tensor, g: ConvGeom, x_shape):
+    """(U' buffer, event) for the conv's Winograd input gradient, launched now on a side stream, or None."""
+    n, c, h, wd = x_shape
+    co = w.shape[0]
+    if not WINOGRAD_UPRE or PROFILE is not None or not w.is_cuda or torch.cuda.is_current_stream_capturing() or \
+            g.upsample or not _wino_ok(g, n, h, wd, co, c) or not _al16(w):
+        return None
+    side = _UPRE.get(w.device)
+    if side is None:
+        side = _UPRE[w.device] = torch.cuda.Stream(w.device)
+    mt = _wtile()
+    u = torch.empty(_wel() * (mt + 2) ** 2 * c * co, dtype=torch.uint8, device=w.device)
+    side.wait_stream(torch.cuda.current_stream(w.device))  # (w as written by the weight prep / optimizer)
+    _lib.call("mvae_winograd_weight_transform", w.data_ptr(), u.data_ptr(), c, co, 1, mt, side.cuda_stream)
+    ev = side.record_event()
+    u.record_stream(side)
+    w.record_stream(side)
+    return u, ev
+
+
 # experiment knob: also overlap the two backward passes of the Winograd convs (their memory-bound transforms against the
 # other pass's GEMM), whatever their size
 BWD_OVERLAP_WINO = os.environ.get("MVAE_BWD_OVERLAP_WINO") is not None
@@ -1413,6 +1447,7 @@ class Conv2dFn(torch.autograd.Function):
             x = nhwc(x)
         keep = [] if (WINOGRAD_KEEP_V or lazy is not None) and want_w else None
         y = conv2d_forward_raw(x, w, bias, res, geom, xs, gn_part, x_bf16=xb16, keep_v=keep, lazy=lazy)
+        ctx.u_pre = _upre_launch(w, geom, tuple(x.shape)) if (grad_on and ctx.needs_input_grad[0]) else None
         ctx.wino_v = keep if keep else None
         ctx.lazy = lazy  # (the weight gradient re-derives V from it if the kept one is gone: a second backward)
         ctx.math = _MATH[0]  # the backward GEMMs run in the forward's arithmetic
@@ -1541,14 +1576,14 @@ class Conv2dFn(torch.autograd.Function):
                 dx, acc.buf, acc.left = acc.buf, None, acc.n
         elif ctx.needs_input_grad[0]:
             dx = conv2d_dgrad_raw(dy, w, x.shape, g, link if ctx.x_sink is None else None, dys=dys, dyb=dyb,
-                                  dkeep=dkeep)
+                                  dkeep=dkeep, u_pre=ctx.u_pre)
             if ctx.x_sink is not None and ctx.x_sink.park(dx):
                 dx = None
         if side is not None:
             main.wait_event(ev_join)
         elif ctx.needs_input_grad[1]:
             wgrad()
-        ctx.wino_v = dkeep = None  # (released after the join: a later main-stream allocation is ordered after its last use)
+        ctx.wino_v = dkeep = ctx.u_pre = None  # (released after the join: a later main-stream allocation is ordered after its last use)
         if ctx.has_bias and ctx.needs_input_grad[2] and not bias_done:
             tgt = _main_grad(ctx.bias_ref)
             n, co, ho, wo = dy.shape
