@@ -52,6 +52,22 @@ def _model_kind(model: nn.Module) -> str:
     return "plain"
 
 
+
+# The step's gradient zeroing (3.7 GB for c4's 927 M parameters) on a side stream, overlapped with the forward.
+# Off under graph capture (the captured step keeps one stream). MVAE_ZERO_GRAD_SIDE=0: on the current stream.
+ZERO_GRAD_SIDE = os.environ.get("MVAE_ZERO_GRAD_SIDE", "1") != "0"
+_ZERO_SIDE = {}
+
+
+def _zero_side(g):
+    if not ZERO_GRAD_SIDE or g is None or not g.is_cuda or torch.cuda.is_current_stream_capturing() or \
+            ops.PROFILE is not None:
+        return None
+    side = _ZERO_SIDE.get(g.device)
+    if side is None:
+        side = _ZERO_SIDE[g.device] = torch.cuda.Stream(g.device)
+    return side
+
 class VAELightningModule(_Base):
     def __init__(self, model: nn.Module, optimizer_config: Dict[str, Any], scheduler_config: Dict[str, Any],
                  loss_config: Dict[str, Any], gradient_clip_val: Optional[float] = None,
@@ -458,9 +474,19 @@ class VAELightningModule(_Base):
         """fit_step's first phase: gradients of this rank's batch in the flat buffer (exchange: the data-parallel
         bucket all-reduces launched from the backward's readiness hooks)."""
         self.model.train()
-        self.optimizer.zero_grad()
+        side = _zero_side(self.flat.grad)
+        if side is not None:
+            # the flat gradient is zeroed on a side stream, concurrent with the forward (which never touches it), and
+            # joined before the backward's first gradient write
+            side.wait_stream(torch.cuda.current_stream(self.flat.grad.device))
+            with torch.cuda.stream(side):
+                self.optimizer.zero_grad()
+        else:
+            self.optimizer.zero_grad()
         ops.prep_flat_weights(self.flat.data)  # every conv weight in the GEMM format, one launch
         loss = self.training_step(batch, batch_idx, eps=eps)
+        if side is not None:
+            torch.cuda.current_stream(self.flat.grad.device).wait_stream(side)
         if exchange and self.process_group is not None:
             self.process_group.begin_backward()
         loss.backward()
